@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""ricepp encode+decode benchmark on MI355X (BASELINE.json configs[1]).
+
+One step = encode every block of the shard on the GPU, all-gather the
+per-block encoded sizes over RCCL (N > 1), decode every block back.  Inputs
+are resident in HBM before the timed region; `value` is uncompressed bytes
+of all ranks per second (GiB/s), the accounting of
+ricepp/ricepp_benchmark.cpp:145-146,155-156 applied to the round trip.
+
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+         (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from dwarfs_amd import codec  # noqa: E402
+from dwarfs_amd import parallel  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def make_poisson_blocks(nblocks: int, n: int, lam: float, seed: int, device) -> torch.Tensor:
+    """Poisson(lam) sensor samples, stored big endian, generated on the GPU."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    out = torch.empty(nblocks * n, dtype=torch.int16, device=device)
+    chunk = 1 << 24
+    for s in range(0, nblocks * n, chunk):
+        e = min(s + chunk, nblocks * n)
+        v = torch.poisson(torch.full((e - s,), lam, device=device), generator=g).clamp_(0, 65535).to(torch.int32)
+        v = ((v & 0xFF) << 8) | ((v >> 8) & 0xFF)
+        out[s:e] = v.to(torch.int16)  # wraps to the same 16 bits
+    return out
+
+
+def cpu_baseline(sample: np.ndarray, nblocks: int, n: int, cfg: codec.CodecConfig, min_seconds: float):
+    """The CPU oracle (C restatement of ricepp, kind "port") on host cores."""
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("RICEPP_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    oc = O.cfg(cfg.block_size, cfg.component_stream_count, cfg.byteorder == "big", cfg.unused_lsb_count)
+    offs = (np.arange(nblocks, dtype=np.uint64) * n)
+    cap = O.worst_case_bytes(oc, n)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        out, oo, sz, st = O.encode_batch(oc, sample, offs, [n] * nblocks, cap, nthreads=threads)
+        dec, dst = O.decode_batch(oc, out, oo, sz, offs, [n] * nblocks, nblocks * n, nthreads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    assert (st == 0).all() and (dst == 0).all() and np.array_equal(dec, sample)
+    gib = reps * sample.nbytes / 2**30
+    return {
+        "value": round(gib / el, 4),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{nblocks} x 64 KiB Poisson(1000) BE bs128 cs1 blocks (first {nblocks} of the GPU workload), "
+                  f"encode+decode x{reps}, {el:.1f} s wall, {threads} threads over independent blocks",
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--blocks", type=int, default=4096)
+    ap.add_argument("--block-bytes", type=int, default=65536)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = codec.CodecConfig(block_size=128, component_stream_count=1, byteorder="big", unused_lsb_count=0)
+    nblocks, n = args.blocks, args.block_bytes // 2
+    x = make_poisson_blocks(nblocks, n, 1000.0, 42 + rank, dev)
+    in_offsets = np.arange(nblocks, dtype=np.int64) * n
+    pipe = parallel.ShardPipeline(cfg, x, in_offsets, np.full(nblocks, n, np.int64), group=dist.group.WORLD if world > 1 else None)
+
+    # correctness gate before timing: round trip must be exact
+    pipe.step()
+    torch.cuda.synchronize()
+    pipe.check(x)
+
+    for _ in range(args.warmup):
+        pipe.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel timing with events on the launch stream (torch's current stream)
+    k_enc, k_dec = pipe.kernel_times(iters=max(5, args.steps))
+    comp_bytes = int(pipe.enc.sizes.sum().item())
+    raw_bytes = nblocks * n * 2
+    enc_bytes = raw_bytes + comp_bytes + 8 * nblocks
+    dec_bytes = comp_bytes + raw_bytes
+    dominant = "decode" if k_dec >= k_enc else "encode"
+    kt, kb = (k_dec, dec_bytes) if dominant == "decode" else (k_enc, enc_bytes)
+    achieved = kb / kt / 1e9
+
+    traffic = None
+    pmc = ROOT / "profiles" / "pmc_latest.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get(f"rpp_{dominant}_kernel", {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    total_bytes = raw_bytes * world * args.steps
+    value = total_bytes / elapsed / 2**30
+    result = {
+        "metric": "ricepp encode+decode GiB/s, device-resident uint16 blocks, 1/2/4/8 GPUs",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic Poisson(1000) sensor samples, stored big endian, generated on device",
+        "config": {
+            "workload": f"{nblocks} independent {args.block_bytes // 1024} KiB uint16 blocks per GPU, "
+                        "ricepp bs128 cs1 BE ulsb0, encode+decode round trip (BASELINE.json configs[1])",
+            "blocks_per_gpu": nblocks,
+            "block_bytes": args.block_bytes,
+            "compression_ratio": round(comp_bytes / raw_bytes, 5),
+            "parallelism": f"shard{world} (blocks sharded, RCCL all-gather of encoded sizes)",
+            "encode_kernel_us": round(k_enc * 1e6, 2),
+            "decode_kernel_us": round(k_dec * 1e6, 2),
+            "encode_GiBps": round(raw_bytes / k_enc / 2**30, 2),
+            "decode_GiBps": round(raw_bytes / k_dec / 2**30, 2),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": f"rpp_{dominant}_kernel",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        nb = min(nblocks, 1024)
+        sample = x[: nb * n].cpu().numpy().view(np.uint16).copy()
+        result["cpu_baseline"] = cpu_baseline(sample, nb, n, cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+"""Loader for the native MI355X ricepp library (libricepp_amd.so).
+
+The library exports exactly the C ABI of ``include/ricepp_amd.h``.  There is
+no fallback: if the library is missing or fails to load, every entry point
+raises, so a GPU run can never silently pass on a non-native path.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("RICEPP_AMD_LIB", PKG / "lib" / "libricepp_amd.so"))
+
+RPP_OK = 0
+RPP_UNSUPPORTED_CONFIG = -1
+RPP_TRUNCATED_INPUT = -2
+RPP_INVALID_ARGUMENT = -3
+RPP_OUTPUT_TOO_SMALL = -4
+RPP_HIP_ERROR = -5
+
+STATUS_NAMES = {
+    RPP_OK: "OK",
+    RPP_UNSUPPORTED_CONFIG: "UNSUPPORTED_CONFIG",
+    RPP_TRUNCATED_INPUT: "TRUNCATED_INPUT",
+    RPP_INVALID_ARGUMENT: "INVALID_ARGUMENT",
+    RPP_OUTPUT_TOO_SMALL: "OUTPUT_TOO_SMALL",
+    RPP_HIP_ERROR: "HIP_ERROR",
+}
+
+# Every symbol declared in include/ricepp_amd.h.
+EXPORTED_SYMBOLS = (
+    "rpp_abi_version",
+    "rpp_check_config",
+    "rpp_worst_case_bytes",
+    "rpp_encode_batch",
+    "rpp_decode_batch",
+    "rpp_frame_header",
+    "rpp_parse_frame",
+)
+
+
+class RppConfig(C.Structure):
+    """``rpp_config`` (mirrors ricepp::codec_config, codec_config.h:36-41)."""
+
+    _fields_ = [
+        ("block_size", C.c_uint32),
+        ("component_stream_count", C.c_uint32),
+        ("big_endian", C.c_uint32),
+        ("unused_lsb_count", C.c_uint32),
+    ]
+
+
+class RppFrame(C.Structure):
+    _fields_ = [
+        ("uncompressed_bytes", C.c_uint64),
+        ("block_size", C.c_uint32),
+        ("component_count", C.c_uint32),
+        ("bytes_per_sample", C.c_uint32),
+        ("unused_lsb_count", C.c_uint32),
+        ("big_endian", C.c_uint32),
+        ("ricepp_version", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Returns the loaded native library; raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"native ricepp library not found at {LIB_PATH}; run `python __graft_entry__.py build`"
+            )
+        L = C.CDLL(str(LIB_PATH))
+        P = C.c_void_p
+        L.rpp_abi_version.restype = C.c_uint32
+        L.rpp_check_config.argtypes = [C.POINTER(RppConfig)]
+        L.rpp_check_config.restype = C.c_int
+        L.rpp_worst_case_bytes.argtypes = [C.POINTER(RppConfig), C.c_uint64]
+        L.rpp_worst_case_bytes.restype = C.c_uint64
+        L.rpp_encode_batch.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, P]
+        L.rpp_encode_batch.restype = C.c_int
+        L.rpp_decode_batch.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, P]
+        L.rpp_decode_batch.restype = C.c_int
+        L.rpp_frame_header.argtypes = [C.POINTER(RppFrame), P]
+        L.rpp_frame_header.restype = C.c_size_t
+        L.rpp_parse_frame.argtypes = [P, C.c_size_t, C.POINTER(RppFrame)]
+        L.rpp_parse_frame.restype = C.c_long
+        if L.rpp_abi_version() != 1:
+            raise RuntimeError("libricepp_amd.so ABI mismatch")
+        _lib = L
+    return _lib

@@ -1,0 +1,283 @@
+"""Host-side mirror of the ricepp library API over the MI355X kernels.
+
+Mirrors ``ricepp::create_encoder<uint16_t>`` / ``create_decoder<uint16_t>``
+(ricepp/include/ricepp/create_encoder.h:39-41, create_decoder.h:39-41) and the
+``encoder_interface`` / ``decoder_interface`` methods
+(ricepp/include/ricepp/encoder_interface.h:38-60, decoder_interface.h:37-50),
+plus batched device-resident entry points that are the MI355X-native way to
+drive the codec: many independent blocks per launch, one wavefront per block.
+
+Error behaviour follows the reference:
+  * invalid config  -> ``RuntimeError("Unsupported configuration")``
+    (ricepp/ricepp_cpuspecific.cpp:161,173)
+  * reading past the end of the input -> ``OutOfRange`` (an ``IndexError``,
+    the Python analogue of ``std::out_of_range``, bitstream_reader.h:150-152)
+
+Everything here calls the C ABI of ``include/ricepp_amd.h``; there is no CPU
+codec in this package.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+__all__ = [
+    "CodecConfig",
+    "OutOfRange",
+    "UnsupportedConfiguration",
+    "Encoder",
+    "Decoder",
+    "EncodedBatch",
+    "create_encoder",
+    "create_decoder",
+    "worst_case_encoded_bytes",
+    "encode_batch",
+    "decode_batch",
+]
+
+
+class UnsupportedConfiguration(RuntimeError):
+    """``std::runtime_error("Unsupported configuration")``."""
+
+    def __init__(self) -> None:
+        super().__init__("Unsupported configuration")
+
+
+class OutOfRange(IndexError):
+    """``std::out_of_range``: the decoder ran past the end of its input."""
+
+
+class CodecError(RuntimeError):
+    pass
+
+
+@dataclass(frozen=True)
+class CodecConfig:
+    """``ricepp::codec_config`` (ricepp/include/ricepp/codec_config.h:36-41)."""
+
+    block_size: int = 128
+    component_stream_count: int = 1
+    byteorder: str = "big"  # "big" or "little": byte order of the stored samples
+    unused_lsb_count: int = 0
+
+    def native(self) -> N.RppConfig:
+        if self.byteorder not in ("big", "little"):
+            raise ValueError(f"byteorder must be 'big' or 'little', not {self.byteorder!r}")
+        return N.RppConfig(
+            int(self.block_size),
+            int(self.component_stream_count),
+            1 if self.byteorder == "big" else 0,
+            int(self.unused_lsb_count),
+        )
+
+
+def _raise_status(st: int) -> None:
+    if st == N.RPP_OK:
+        return
+    if st == N.RPP_UNSUPPORTED_CONFIG:
+        raise UnsupportedConfiguration()
+    if st == N.RPP_TRUNCATED_INPUT:
+        raise OutOfRange("bitstream_reader::read_packet")
+    raise CodecError(f"ricepp_amd: {N.STATUS_NAMES.get(st, st)}")
+
+
+def _check(config: CodecConfig) -> N.RppConfig:
+    c = config.native()
+    _raise_status(N.lib().rpp_check_config(C.byref(c)))
+    return c
+
+
+def worst_case_encoded_bytes(config: CodecConfig, n_samples: int) -> int:
+    c = _check(config)
+    return int(N.lib().rpp_worst_case_bytes(C.byref(c), int(n_samples)))
+
+
+def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> C.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _dev_u64(values, device) -> torch.Tensor:
+    return torch.as_tensor(np.asarray(values, dtype=np.int64), device=device)
+
+
+def _as_u16_tensor(samples, device) -> torch.Tensor:
+    if isinstance(samples, torch.Tensor):
+        if samples.element_size() != 2:
+            raise TypeError("samples must be a 16-bit tensor")
+        t = samples.reshape(-1)
+        if t.device.type != "cuda":
+            t = t.to(device)
+        return t.contiguous()
+    a = np.ascontiguousarray(np.asarray(samples), dtype=np.uint16)
+    return torch.from_numpy(a.view(np.int16)).to(device)
+
+
+@dataclass
+class EncodedBatch:
+    """Device-resident result of :func:`encode_batch`."""
+
+    data: torch.Tensor          # uint8 [sum of per-block capacities]
+    offsets: np.ndarray         # int64 [nblocks] byte offset of each block's stream (host)
+    d_offsets: torch.Tensor     # same, on the device
+    sizes: torch.Tensor         # int64 [nblocks] encoded bytes (device)
+    status: torch.Tensor        # int32 [nblocks] (device)
+
+    def check(self) -> None:
+        st = self.status.cpu().numpy()
+        bad = np.nonzero(st)[0]
+        if len(bad):
+            _raise_status(int(st[bad[0]]))
+
+    def block(self, i: int) -> bytes:
+        n = int(self.sizes[i].item())
+        o = int(self.offsets[i])
+        return self.data[o:o + n].cpu().numpy().tobytes()
+
+
+def encode_batch(
+    config: CodecConfig,
+    samples: torch.Tensor,
+    in_offsets: Sequence[int],
+    n_samples: Sequence[int],
+    stream: Optional[torch.cuda.Stream] = None,
+    out: Optional[torch.Tensor] = None,
+    out_offsets: Optional[np.ndarray] = None,
+) -> EncodedBatch:
+    """Encodes independent blocks of device-resident samples in one launch.
+
+    ``samples`` is a 16-bit CUDA tensor of *stored* samples (the byte order
+    named by ``config.byteorder``); block ``b`` is
+    ``samples[in_offsets[b] : in_offsets[b] + n_samples[b]]``.
+    """
+    c = _check(config)
+    dev = samples.device
+    n_samples = np.asarray(n_samples, dtype=np.int64)
+    nb = len(n_samples)
+    if out_offsets is None:
+        caps = np.array([N.lib().rpp_worst_case_bytes(C.byref(c), int(n)) for n in n_samples], np.int64)
+        caps = (caps + 15) // 16 * 16
+        out_offsets = np.zeros(nb, np.int64)
+        if nb:
+            out_offsets[1:] = np.cumsum(caps)[:-1]
+        total = int(caps.sum()) if nb else 0
+    else:
+        total = None
+    if out is None:
+        out = torch.empty(max(total or 0, 16), dtype=torch.uint8, device=dev)
+    d_in_off = _dev_u64(in_offsets, dev)
+    d_n = _dev_u64(n_samples, dev)
+    d_out_off = _dev_u64(out_offsets, dev)
+    sizes = torch.empty(nb, dtype=torch.int64, device=dev)
+    status = torch.empty(nb, dtype=torch.int32, device=dev)
+    st = N.lib().rpp_encode_batch(
+        C.byref(c), C.c_void_p(samples.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
+        C.c_void_p(d_n.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),
+        C.c_void_p(sizes.data_ptr()), C.c_void_p(status.data_ptr()), _stream_ptr(stream))
+    _raise_status(st)
+    return EncodedBatch(out, np.asarray(out_offsets, np.int64), d_out_off, sizes, status)
+
+
+def decode_batch(
+    config: CodecConfig,
+    data: torch.Tensor,
+    in_offsets: Sequence[int],
+    in_bytes: Union[Sequence[int], torch.Tensor],
+    n_samples: Sequence[int],
+    stream: Optional[torch.cuda.Stream] = None,
+    out: Optional[torch.Tensor] = None,
+    out_offsets: Optional[Sequence[int]] = None,
+):
+    """Decodes independent blocks of a device-resident encoded buffer.
+
+    Returns ``(samples int16 tensor, status int32 tensor)``.  Block ``b``'s
+    samples land at ``out[out_offsets[b] : out_offsets[b] + n_samples[b]]``
+    (default: packed back to back).
+    """
+    c = _check(config)
+    dev = data.device
+    n_samples = np.asarray(n_samples, dtype=np.int64)
+    nb = len(n_samples)
+    if out_offsets is None:
+        out_offsets = np.zeros(nb, np.int64)
+        if nb:
+            out_offsets[1:] = np.cumsum(n_samples)[:-1]
+    out_offsets = np.asarray(out_offsets, np.int64)
+    if out is None:
+        total = int((out_offsets + n_samples).max()) if nb else 0
+        out = torch.empty(max(total, 8), dtype=torch.int16, device=dev)
+    d_in_off = in_offsets if isinstance(in_offsets, torch.Tensor) else _dev_u64(in_offsets, dev)
+    d_in_bytes = in_bytes if isinstance(in_bytes, torch.Tensor) else _dev_u64(in_bytes, dev)
+    d_n = _dev_u64(n_samples, dev)
+    d_out_off = _dev_u64(out_offsets, dev)
+    status = torch.empty(nb, dtype=torch.int32, device=dev)
+    st = N.lib().rpp_decode_batch(
+        C.byref(c), C.c_void_p(data.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
+        C.c_void_p(d_in_bytes.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),
+        C.c_void_p(d_n.data_ptr()), C.c_void_p(status.data_ptr()), _stream_ptr(stream))
+    _raise_status(st)
+    return out, status
+
+
+class Encoder:
+    """``encoder_interface<uint16_t>`` (encoder_interface.h:38-60)."""
+
+    def __init__(self, config: CodecConfig, device: Union[str, torch.device] = "cuda"):
+        _check(config)
+        self.config = config
+        self.device = torch.device(device)
+
+    def worst_case_encoded_bytes(self, n_or_samples) -> int:
+        n = n_or_samples if isinstance(n_or_samples, (int, np.integer)) else len(n_or_samples)
+        return worst_case_encoded_bytes(self.config, int(n))
+
+    def encode(self, samples) -> bytes:
+        """``encode(span<u16 const>) -> vector<u8>`` (ricepp_cpuspecific.cpp:53-56,91-99)."""
+        t = _as_u16_tensor(samples, self.device)
+        res = encode_batch(self.config, t, [0], [t.numel()])
+        res.check()
+        return res.block(0)
+
+    def encode_into(self, out: np.ndarray, samples) -> int:
+        """``encode(span<u8>, span<u16 const>) -> span<u8>``: returns the bytes used."""
+        data = self.encode(samples)
+        if len(out) < self.worst_case_encoded_bytes(samples):
+            raise ValueError("output buffer smaller than worst_case_encoded_bytes")
+        out[: len(data)] = np.frombuffer(data, np.uint8)
+        return len(data)
+
+
+class Decoder:
+    """``decoder_interface<uint16_t>`` (decoder_interface.h:37-50)."""
+
+    def __init__(self, config: CodecConfig, device: Union[str, torch.device] = "cuda"):
+        _check(config)
+        self.config = config
+        self.device = torch.device(device)
+
+    def decode(self, data: bytes, n_samples: int) -> np.ndarray:
+        """Decodes exactly ``n_samples`` stored uint16 samples."""
+        buf = np.frombuffer(bytes(data), np.uint8)
+        padded = np.zeros(max(len(buf), 1) + 16, np.uint8)
+        padded[: len(buf)] = buf
+        d = torch.from_numpy(padded).to(self.device)
+        out, status = decode_batch(self.config, d, [0], [len(buf)], [n_samples])
+        _raise_status(int(status[0].item()))
+        return out[:n_samples].cpu().numpy().view(np.uint16).copy()
+
+
+def create_encoder(config: CodecConfig, device="cuda") -> Encoder:
+    """``ricepp::create_encoder<uint16_t>`` (create_encoder.h:39-41)."""
+    return Encoder(config, device)
+
+
+def create_decoder(config: CodecConfig, device="cuda") -> Decoder:
+    """``ricepp::create_decoder<uint16_t>`` (create_decoder.h:39-41)."""
+    return Decoder(config, device)

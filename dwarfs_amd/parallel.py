@@ -1,0 +1,172 @@
+"""Block sharding across the GPUs of one node.
+
+ricepp blocks are independent streams (the codec's running state resets per
+stream, ricepp/include/ricepp/codec.h:69-74,81-86), so a batch of DwarFS
+blocks shards by contiguous block ranges with no data exchange.  The only
+collective is an all-gather of the per-block encoded sizes (RCCL over xGMI
+with the "nccl" backend; gloo on CPU in tests), from which every rank knows
+the global byte offset of each compressed block in the output image.  That is
+the multi-GPU analogue of filesystem_writer's per-block jobs
+(src/writer/filesystem_writer.cpp:255-287) whose compressed sizes are laid
+out one after another.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native as N
+from .codec import CodecConfig, _check, _raise_status
+
+
+def partition_blocks(block_bytes: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous block ranges [start, end) per rank, balanced by bytes.
+
+    Rank r takes the blocks whose byte midpoint falls in
+    [r * total / world, (r + 1) * total / world)."""
+    sizes = np.asarray(block_bytes, dtype=np.float64)
+    if world <= 1 or len(sizes) == 0:
+        return [(0, len(sizes))] + [(len(sizes), len(sizes))] * max(0, world - 1)
+    ends = np.cumsum(sizes)
+    mids = ends - sizes / 2
+    total = ends[-1] if len(ends) else 0.0
+    owner = np.minimum((mids * world / max(total, 1e-300)).astype(np.int64), world - 1)
+    ranges = []
+    for r in range(world):
+        idx = np.nonzero(owner == r)[0]
+        if len(idx):
+            ranges.append((int(idx[0]), int(idx[-1]) + 1))
+        else:
+            prev = ranges[-1][1] if ranges else 0
+            ranges.append((prev, prev))
+    return ranges
+
+
+def gather_sizes(local_sizes: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gathers int64 per-block sizes from every rank (ragged counts
+    allowed) and returns them concatenated in rank order."""
+    if group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return local_sizes
+    world = dist.get_world_size(group)
+    cnt = torch.tensor([local_sizes.numel()], dtype=torch.int64, device=local_sizes.device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts)
+    padded = torch.zeros(m, dtype=torch.int64, device=local_sizes.device)
+    padded[: local_sizes.numel()] = local_sizes
+    if local_sizes.device.type == "cuda":
+        out = torch.empty(world * m, dtype=torch.int64, device=local_sizes.device)
+        dist.all_gather_into_tensor(out, padded, group=group)
+        parts = out.view(world, m)
+        return torch.cat([parts[r, : counts[r]] for r in range(world)])
+    parts = [torch.zeros(m, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, padded, group=group)
+    return torch.cat([parts[r][: counts[r]] for r in range(world)])
+
+
+def global_offsets(all_sizes: torch.Tensor) -> torch.Tensor:
+    """Exclusive prefix sum: byte offset of every block in the concatenated image."""
+    off = torch.zeros_like(all_sizes)
+    if all_sizes.numel() > 1:
+        off[1:] = torch.cumsum(all_sizes[:-1], 0)
+    return off
+
+
+class ShardPipeline:
+    """This rank's shard of blocks, resident on its GPU, with every device
+    array preallocated so one step is three launches (encode, size gather,
+    decode) and no host-device synchronisation."""
+
+    def __init__(self, config: CodecConfig, samples: torch.Tensor, in_offsets, n_samples, group=None):
+        self.cfg = _check(config)
+        self.config = config
+        self.group = group
+        self.samples = samples
+        dev = samples.device
+        self.nblocks = len(n_samples)
+        n_samples = np.asarray(n_samples, np.int64)
+        caps = np.array([N.lib().rpp_worst_case_bytes(C.byref(self.cfg), int(n)) for n in n_samples], np.int64)
+        caps = (caps + 15) // 16 * 16
+        out_off = np.zeros(self.nblocks, np.int64)
+        if self.nblocks:
+            out_off[1:] = np.cumsum(caps)[:-1]
+        self.out_offsets = out_off
+        self.d_in_off = torch.as_tensor(np.asarray(in_offsets, np.int64), device=dev)
+        self.d_n = torch.as_tensor(n_samples, device=dev)
+        self.d_out_off = torch.as_tensor(out_off, device=dev)
+        self.data = torch.empty(max(int(caps.sum()), 16), dtype=torch.uint8, device=dev)
+        self.sizes = torch.zeros(self.nblocks, dtype=torch.int64, device=dev)
+        self.enc_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
+        dec_off = np.zeros(self.nblocks, np.int64)
+        if self.nblocks:
+            dec_off[1:] = np.cumsum(n_samples)[:-1]
+        self.d_dec_off = torch.as_tensor(dec_off, device=dev)
+        self.decoded = torch.empty(max(int(n_samples.sum()), 8), dtype=torch.int16, device=dev)
+        self.dec_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
+        self.all_sizes: Optional[torch.Tensor] = None
+        self.image_offsets: Optional[torch.Tensor] = None
+
+        class _Enc:
+            pass
+
+        self.enc = _Enc()
+        self.enc.sizes = self.sizes
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def encode(self) -> None:
+        _raise_status(N.lib().rpp_encode_batch(
+            C.byref(self.cfg), C.c_void_p(self.samples.data_ptr()), C.c_void_p(self.d_in_off.data_ptr()),
+            C.c_void_p(self.d_n.data_ptr()), self.nblocks, C.c_void_p(self.data.data_ptr()),
+            C.c_void_p(self.d_out_off.data_ptr()), C.c_void_p(self.sizes.data_ptr()),
+            C.c_void_p(self.enc_status.data_ptr()), self._stream()))
+
+    def decode(self) -> None:
+        _raise_status(N.lib().rpp_decode_batch(
+            C.byref(self.cfg), C.c_void_p(self.data.data_ptr()), C.c_void_p(self.d_out_off.data_ptr()),
+            C.c_void_p(self.sizes.data_ptr()), self.nblocks, C.c_void_p(self.decoded.data_ptr()),
+            C.c_void_p(self.d_dec_off.data_ptr()), C.c_void_p(self.d_n.data_ptr()),
+            C.c_void_p(self.dec_status.data_ptr()), self._stream()))
+
+    def gather(self) -> None:
+        self.all_sizes = gather_sizes(self.sizes, self.group)
+        self.image_offsets = global_offsets(self.all_sizes)
+
+    def step(self) -> None:
+        self.encode()
+        self.gather()
+        self.decode()
+
+    def check(self, reference: torch.Tensor) -> None:
+        if int(self.enc_status.abs().sum().item()) or int(self.dec_status.abs().sum().item()):
+            raise RuntimeError(f"codec status enc={self.enc_status.unique().tolist()} dec={self.dec_status.unique().tolist()}")
+        n = int(self.d_n.sum().item())
+        if not torch.equal(self.decoded[:n], reference[:n]):
+            raise RuntimeError("round trip mismatch")
+
+    def kernel_times(self, iters: int = 10) -> Tuple[float, float]:
+        """Average encode / decode kernel durations (s), HIP events on the
+        stream the kernels are launched on."""
+        s = torch.cuda.current_stream()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        self.encode()
+        self.decode()
+        torch.cuda.synchronize()
+        te = td = 0.0
+        for _ in range(iters):
+            e[0].record(s)
+            self.encode()
+            e[1].record(s)
+            self.decode()
+            e[2].record(s)
+            torch.cuda.synchronize()
+            te += e[0].elapsed_time(e[1]) / 1e3
+            td += e[1].elapsed_time(e[2]) / 1e3
+        return te / iters, td / iters

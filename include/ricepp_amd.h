@@ -1,0 +1,131 @@
+/*
+ * ricepp_amd.h -- C ABI of the MI355X-native ricepp block codec.
+ *
+ * This is the drop-in boundary: plain C types, device pointers and sizes, no
+ * torch or C++ types.  It replaces the inner ricepp library API that the
+ * DwarFS plugin binds (reference: /root/reference):
+ *
+ *   rpp_check_config      <- ricepp::create_encoder / create_decoder config
+ *                            validation (ricepp/ricepp_cpuspecific_traits.h:118-151,
+ *                            throws at ricepp/ricepp_cpuspecific.cpp:161,173)
+ *   rpp_worst_case_bytes  <- encoder_interface::worst_case_encoded_bytes
+ *                            (ricepp/include/ricepp/encoder_interface.h:38-60,
+ *                            ricepp/ricepp_cpuspecific.cpp:58-66,75-77,
+ *                            ricepp/include/ricepp/codec.h:142-151)
+ *   rpp_encode_batch      <- encoder_interface::encode(span<u8>, span<u16 const>)
+ *                            (ricepp/ricepp_cpuspecific.cpp:68-72,101-108), one
+ *                            call per DwarFS block in src/compression/ricepp.cpp:136-137,
+ *                            batched over many independent blocks
+ *   rpp_decode_batch      <- decoder_interface::decode(span<u16>, span<u8 const>)
+ *                            (ricepp/include/ricepp/decoder_interface.h:37-50,
+ *                            ricepp/ricepp_cpuspecific.cpp:127-144), called by
+ *                            src/compression/ricepp.cpp:215-232
+ *   rpp_frame_header /    <- the DwarFS block framing of src/compression/ricepp.cpp:
+ *   rpp_parse_frame          varint size + thrift-compact ricepp_block_header
+ *                            (:107-127 write, :186-201,237-249 read)
+ *
+ * Errors: C++ exceptions cannot cross this boundary.  Status codes map back to
+ * the reference's exceptions in the C++ facade (dwarfs_amd/csrc/ricepp_host.hpp):
+ *   RPP_UNSUPPORTED_CONFIG -> std::runtime_error("Unsupported configuration")
+ *   RPP_TRUNCATED_INPUT    -> std::out_of_range (bitstream_reader.h:150-152)
+ *
+ * Memory: every pointer passed to the *_batch calls is DEVICE memory owned by
+ * the caller (hipMalloc'd).  Calls are asynchronous on `stream` (a
+ * hipStream_t; NULL = default stream).  Per-block status / sizes are written
+ * to device arrays and are valid once the stream has been synchronised.
+ */
+#ifndef RICEPP_AMD_H
+#define RICEPP_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RPP_OK 0
+#define RPP_UNSUPPORTED_CONFIG (-1)
+#define RPP_TRUNCATED_INPUT (-2)
+#define RPP_INVALID_ARGUMENT (-3)
+#define RPP_OUTPUT_TOO_SMALL (-4)
+#define RPP_HIP_ERROR (-5)
+
+/* ricepp::codec_config (ricepp/include/ricepp/codec_config.h:36-41). */
+typedef struct rpp_config {
+  uint32_t block_size;             /* ricepp sub-block size, 1..512 */
+  uint32_t component_stream_count; /* 1 or 2 */
+  uint32_t big_endian;             /* stored sample byte order: 1 = big */
+  uint32_t unused_lsb_count;       /* 0..15 */
+} rpp_config;
+
+/* Largest single stream the kernels accept (bit positions are 32-bit). */
+#define RPP_MAX_STREAM_SAMPLES (UINT64_C(1) << 27)
+
+/* ABI version, bumped on any signature change. */
+uint32_t rpp_abi_version(void);
+
+/* RPP_OK or RPP_UNSUPPORTED_CONFIG. */
+int rpp_check_config(const rpp_config* cfg);
+
+/* ceil(cs * (16 + 4*ceil((n/cs)/bs) + 16*(n/cs)) / 8) bytes. */
+uint64_t rpp_worst_case_bytes(const rpp_config* cfg, uint64_t n_samples);
+
+/*
+ * Encode `nblocks` independent ricepp streams.
+ *   d_in          stored uint16 samples
+ *   d_in_offsets  [nblocks] start of block b in d_in, in samples, 8-aligned
+ *   d_n_samples   [nblocks] samples in block b (multiple of cs, < RPP_MAX_STREAM_SAMPLES)
+ *   d_out         output bytes
+ *   d_out_offsets [nblocks] byte offset of block b's output, 16-aligned;
+ *                 the region must hold rpp_worst_case_bytes(n_samples[b])
+ *   d_out_bytes   [nblocks] written: encoded size of block b
+ *   d_status      [nblocks] written: RPP_OK or an error code
+ * Returns RPP_OK if the launch was issued, else an error code.
+ */
+int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t* d_in_offsets,
+                     const uint64_t* d_n_samples, uint32_t nblocks, uint8_t* d_out,
+                     const uint64_t* d_out_offsets, uint64_t* d_out_bytes, int32_t* d_status,
+                     void* stream);
+
+/*
+ * Decode `nblocks` independent ricepp streams.
+ *   d_in          encoded bytes
+ *   d_in_offsets  [nblocks] byte offset of block b's stream, 4-aligned
+ *   d_in_bytes    [nblocks] encoded size of block b
+ *   d_out         decoded stored uint16 samples
+ *   d_out_offsets [nblocks] start of block b's output, in samples, 8-aligned
+ *   d_n_samples   [nblocks] samples to decode (multiple of cs)
+ *   d_status      [nblocks] RPP_OK, RPP_TRUNCATED_INPUT (the reference's
+ *                 std::out_of_range) or RPP_INVALID_ARGUMENT
+ */
+int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                     const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
+                     const uint64_t* d_out_offsets, const uint64_t* d_n_samples,
+                     int32_t* d_status, void* stream);
+
+/*
+ * DwarFS ricepp block framing (host memory).  rpp_frame_header writes
+ * varint(uncompressed_bytes) + the thrift-compact ricepp_block_header
+ * (thrift/compression.thrift:42-49) to `out` (>= 32 bytes) and returns its
+ * length.  rpp_parse_frame parses the same, returns the header length or a
+ * negative status.
+ */
+typedef struct rpp_frame {
+  uint64_t uncompressed_bytes;
+  uint32_t block_size;
+  uint32_t component_count;
+  uint32_t bytes_per_sample;
+  uint32_t unused_lsb_count;
+  uint32_t big_endian;
+  uint32_t ricepp_version;
+} rpp_frame;
+
+size_t rpp_frame_header(const rpp_frame* f, uint8_t* out);
+long rpp_parse_frame(const uint8_t* in, size_t in_len, rpp_frame* f);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RICEPP_AMD_H */

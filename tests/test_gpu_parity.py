@@ -1,0 +1,249 @@
+"""GPU parity tests: the HIP codec (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact.  Every encoded stream must equal the oracle's bytes, every
+decoded block must equal the oracle's decode of the same bytes (including
+error status for truncated or corrupt input), on the same seeded inputs.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import datagen
+from dwarfs_amd import codec
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
+
+
+def ocfg(c: codec.CodecConfig):
+    return O.cfg(c.block_size, c.component_stream_count, c.byteorder == "big", c.unused_lsb_count)
+
+
+def run_batch(cfg, blocks, in_align=8):
+    """Encodes the list of stored-sample arrays on the GPU, checks every
+    stream against the oracle, decodes on the GPU and checks the samples."""
+    oc = ocfg(cfg)
+    offs, pos = [], 0
+    for b in blocks:
+        pos = (pos + in_align - 1) // in_align * in_align if in_align else pos
+        offs.append(pos)
+        pos += len(b)
+    flat = np.zeros(max(pos, 1) + 8, np.uint16)
+    for o, b in zip(offs, blocks):
+        flat[o:o + len(b)] = b
+    d = torch.from_numpy(flat.view(np.int16)).to(DEV)
+    ns = [len(b) for b in blocks]
+    enc = codec.encode_batch(cfg, d, offs, ns)
+    torch.cuda.synchronize()
+    st = enc.status.cpu().numpy()
+    assert (st == 0).all(), st
+    wants = [O.encode(oc, b) for b in blocks]
+    sizes = enc.sizes.cpu().numpy()
+    data = enc.data.cpu().numpy()
+    for i, w in enumerate(wants):
+        got = data[enc.offsets[i]:enc.offsets[i] + sizes[i]].tobytes()
+        if got != w:
+            diff = next((k for k in range(min(len(got), len(w))) if got[k] != w[k]), None)
+            raise AssertionError(f"block {i} (n={ns[i]}): GPU {len(got)} B vs oracle {len(w)} B, first diff at {diff}")
+    out, dst = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns)
+    torch.cuda.synchronize()
+    assert (dst.cpu().numpy() == 0).all(), dst
+    outn = out.cpu().numpy().view(np.uint16)
+    pos = 0
+    for i, b in enumerate(blocks):
+        assert np.array_equal(outn[pos:pos + len(b)], b), f"decode mismatch block {i}"
+        pos += len(b)
+    return wants
+
+
+KIND_ORDER = ["poisson", "benchmark", "codec_test", "constant", "full_range", "ramp", "mixed", "spiky", "zeros"]
+
+
+@pytest.mark.parametrize("bs", [1, 7, 8, 13, 16, 29, 32, 64, 99, 128, 200, 256, 500, 512])
+@pytest.mark.parametrize("cs", [1, 2])
+def test_config_matrix(bs, cs):
+    rng = np.random.default_rng(1000 * bs + cs)
+    for be in (True, False):
+        for ulsb in (0, 4):
+            blocks = []
+            for ki, kind in enumerate(KIND_ORDER):
+                n = int(rng.integers(1, 3 * bs * cs + 700)) // cs * cs
+                blocks.append(datagen.KINDS[kind](rng, n, ulsb, be))
+            blocks.append(datagen.poisson_data(rng, cs * bs * 7, ulsb=ulsb, big_endian=be))
+            blocks.append(datagen.poisson_data(rng, cs, ulsb=ulsb, big_endian=be))
+            run_batch(codec.CodecConfig(bs, cs, "big" if be else "little", ulsb), blocks)
+
+
+@pytest.mark.parametrize("ulsb", list(range(0, 16)))
+def test_unused_lsb_sweep(ulsb):
+    rng = np.random.default_rng(ulsb)
+    blocks = [datagen.KINDS[k](rng, 3000, ulsb, True) for k in ("poisson", "benchmark", "codec_test")]
+    for bs in (16, 32, 128):
+        run_batch(codec.CodecConfig(bs, 1, "big", ulsb), blocks)
+
+
+def test_reference_configs_and_kats():
+    rng = np.random.default_rng(42)
+    run_batch(codec.CodecConfig(16, 1, "big", 0), [datagen.codec_test_data(rng, 12345)])
+    run_batch(codec.CodecConfig(13, 1, "big", 4), [datagen.codec_test_data(rng, 4321, 4)])
+    run_batch(codec.CodecConfig(32, 1, "big", 0), [datagen.mixed_data(rng, 1500)])
+    run_batch(codec.CodecConfig(29, 2, "big", 2), [datagen.codec_test_data(rng, 23456, 2)])
+    # codec_test.cpp:164-172: incompressible -> exactly the worst case 29138
+    wants = run_batch(codec.CodecConfig(29, 1, "big", 0), [datagen.full_range_data(rng, 14443)])
+    assert len(wants[0]) == 29138
+    assert codec.worst_case_encoded_bytes(codec.CodecConfig(29, 2, "big", 0), 28886) == 58275
+    for cs, pixels, ulsb, bs in [(1, 1000, 0, 16), (2, 1000, 2, 32), (1, 1000, 4, 64), (2, 3333, 6, 99)]:
+        run_batch(codec.CodecConfig(bs, cs, "big", ulsb), [datagen.dwarfs_test_data(rng, pixels, cs, ulsb)])
+
+
+def test_unsupported_configuration():
+    for bad in (codec.CodecConfig(513, 2), codec.CodecConfig(128, 3), codec.CodecConfig(0, 1)):
+        with pytest.raises(RuntimeError, match="Unsupported configuration"):
+            codec.create_encoder(bad)
+        with pytest.raises(RuntimeError, match="Unsupported configuration"):
+            codec.create_decoder(bad)
+
+
+@pytest.mark.parametrize("name,cs", [("dark.fits", 1), ("test.fits", 2), ("test.fits", 1)])
+def test_fits_fixtures(name, cs):
+    _, x = datagen.parse_fits(GOLDEN / name)
+    for bs in (16, 128, 512):
+        run_batch(codec.CodecConfig(bs, cs, "big", 0), [x, x[: len(x) // 2 // cs * cs]])
+
+
+def test_ragged_and_unaligned_blocks():
+    rng = np.random.default_rng(5)
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    sizes = [0, 1, 2, 3, 127, 128, 129, 255, 256, 257, 1023, 5000]
+    blocks = [datagen.poisson_data(rng, n) for n in sizes]
+    run_batch(cfg, blocks, in_align=1)  # odd sample offsets: scalar load path
+    run_batch(cfg, blocks, in_align=8)
+    cfg2 = codec.CodecConfig(64, 2, "little", 3)
+    blocks2 = [datagen.poisson_data(rng, n, lam=500, ulsb=3, big_endian=False) for n in (0, 2, 4, 126, 128, 130, 2222)]
+    run_batch(cfg2, blocks2, in_align=1)
+
+
+def test_api_facade_roundtrip():
+    rng = np.random.default_rng(9)
+    cfg = codec.CodecConfig(128, 2, "big", 2)
+    x = datagen.poisson_data(rng, 10000, lam=250, ulsb=2)
+    enc = codec.create_encoder(cfg)
+    data = enc.encode(x)
+    assert data == O.encode(ocfg(cfg), x)
+    assert enc.worst_case_encoded_bytes(x.size) == O.worst_case_bytes(ocfg(cfg), x.size)
+    dec = codec.create_decoder(cfg)
+    assert np.array_equal(dec.decode(data, x.size), x)
+
+
+def _oracle_status(oc, data, n):
+    try:
+        return 0, O.decode(oc, data, n)
+    except O.OracleError as e:
+        return e.status, None
+
+
+def test_truncated_input_status_matches_oracle():
+    rng = np.random.default_rng(11)
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    oc = ocfg(cfg)
+    x = datagen.poisson_data(rng, 3000)
+    full = O.encode(oc, x)
+    cuts = sorted(set([0, 1, 2, 3, 4, 8, 9, 100, len(full) // 2] + list(range(len(full) - 20, len(full) + 1))))
+    streams = [full[:c] for c in cuts]
+    offs = np.zeros(len(streams), np.int64)
+    buf = bytearray()
+    for i, s in enumerate(streams):
+        offs[i] = len(buf)
+        buf += s + bytes((-len(s)) % 16 + 16)
+    d = torch.from_numpy(np.frombuffer(bytes(buf), np.uint8).copy()).to(DEV)
+    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], [x.size] * len(streams))
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    outn = out.cpu().numpy().view(np.uint16)
+    for i, s in enumerate(streams):
+        want_st, want = _oracle_status(oc, s, x.size)
+        assert st[i] == want_st, (cuts[i], st[i], want_st)
+        if want_st == 0:
+            assert np.array_equal(outn[i * x.size:(i + 1) * x.size], want)
+
+
+@pytest.mark.parametrize("bs,cs", [(128, 1), (16, 2), (29, 1)])
+def test_corrupt_streams_match_oracle(bs, cs):
+    """Random bytes decode to whatever the reference decodes them to (or fail
+    the same way): the decoder follows the reference bit for bit."""
+    rng = np.random.default_rng(bs + cs)
+    cfg = codec.CodecConfig(bs, cs, "big", 1)
+    oc = ocfg(cfg)
+    nstreams, n = 64, 256 * cs
+    streams = []
+    for i in range(nstreams):
+        ln = int(rng.integers(4, 900))
+        raw = rng.integers(0, 256, ln, dtype=np.uint8)
+        if i % 3 == 0:  # sparse ones -> long unary runs
+            raw &= rng.integers(0, 256, ln, dtype=np.uint8) & rng.integers(0, 256, ln, dtype=np.uint8)
+        streams.append(raw.tobytes())
+    offs = np.zeros(nstreams, np.int64)
+    buf = bytearray()
+    for i, s in enumerate(streams):
+        offs[i] = len(buf)
+        buf += s + bytes((-len(s)) % 16 + 16)
+    d = torch.from_numpy(np.frombuffer(bytes(buf), np.uint8).copy()).to(DEV)
+    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], [n] * nstreams)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    outn = out.cpu().numpy().view(np.uint16)
+    for i, s in enumerate(streams):
+        want_st, want = _oracle_status(oc, s, n)
+        assert st[i] == want_st, (i, st[i], want_st)
+        if want_st == 0:
+            assert np.array_equal(outn[i * n:(i + 1) * n], want), i
+
+
+def _full_size(kind, nblocks=4096, n=32768, bs=128, cs=1, nthreads=8):
+    rng = np.random.default_rng(42)
+    if kind == "poisson":
+        x = datagen.poisson_data(rng, nblocks * n)
+    else:
+        x = datagen.benchmark_data(rng, nblocks * n)
+    cfg = codec.CodecConfig(bs, cs, "big", 0)
+    oc = ocfg(cfg)
+    offs = np.arange(nblocks, dtype=np.int64) * n
+    d = torch.from_numpy(x.view(np.int16)).to(DEV)
+    enc = codec.encode_batch(cfg, d, offs, [n] * nblocks)
+    torch.cuda.synchronize()
+    assert (enc.status.cpu().numpy() == 0).all()
+    cap = O.worst_case_bytes(oc, n)
+    ob, oo, osz, ost = O.encode_batch(oc, x, offs.astype(np.uint64), [n] * nblocks, cap, nthreads=nthreads)
+    assert (ost == 0).all()
+    sizes = enc.sizes.cpu().numpy()
+    assert np.array_equal(sizes, osz.astype(np.int64)), "encoded sizes differ from oracle"
+    data = enc.data.cpu().numpy()
+    for i in range(nblocks):
+        a = data[enc.offsets[i]:enc.offsets[i] + sizes[i]]
+        b = ob[int(oo[i]):int(oo[i]) + int(osz[i])]
+        assert np.array_equal(a, b), f"block {i} differs"
+    out, st = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, [n] * nblocks)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert torch.equal(out[: nblocks * n], d), "round trip mismatch"
+
+
+def test_full_size_4096x64k_poisson_bit_exact():
+    _full_size("poisson")
+
+
+def test_full_size_4096x64k_benchmark_generator_bit_exact():
+    _full_size("benchmark")
+
+
+@pytest.mark.parametrize("mib", [1, 4, 16])
+def test_large_blocks(mib):
+    rng = np.random.default_rng(mib)
+    n = mib * (1 << 20) // 2
+    blocks = [datagen.poisson_data(rng, n), datagen.benchmark_data(rng, n // 2)]
+    run_batch(codec.CodecConfig(128, 1, "big", 0), blocks)
+    run_batch(codec.CodecConfig(128, 2, "big", 0), [blocks[0]])
