@@ -29,6 +29,23 @@
 
 #include "ricepp_amd.h"
 
+#ifdef RPP_STATS
+// Diagnostic build only (-DRPP_STATS): loop trip counters, summed over waves.
+__device__ unsigned long long g_rpp_stats[16];
+#define RPP_STAT(i, v) (stat_acc[i] += (v))
+// phase timer: adds the s_memtime delta since the previous stamp to slot i
+#define RPP_TSTAMP(i)                                                   \
+  do {                                                                  \
+    unsigned long long now_;                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now_)::"memory"); \
+    stat_acc[i] += (uint32_t)(now_ - tprev_);                            \
+    tprev_ = now_;                                                      \
+  } while (0)
+#else
+#define RPP_STAT(i, v) ((void)0)
+#define RPP_TSTAMP(i) ((void)0)
+#endif
+
 namespace {
 
 constexpr int kWave = 64;
@@ -64,31 +81,67 @@ __device__ __forceinline__ uint32_t shfl_up(uint32_t v, int d) { return (uint32_
 __device__ __forceinline__ uint32_t shfl_down(uint32_t v, int d) { return (uint32_t)__shfl_down((int)v, d); }
 __device__ __forceinline__ uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m); }
 
-// sum over the aligned group of G lanes containing this lane (G pow2 <= 64)
+// DPP controls (gfx9 encoding)
+constexpr int kDppQuadXor1 = 0xB1;     // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;     // quad_perm [2,3,0,1]
+constexpr int kDppRowShr1 = 0x111;
+constexpr int kDppRowShr2 = 0x112;
+constexpr int kDppRowShr4 = 0x114;
+constexpr int kDppRowShr8 = 0x118;
+constexpr int kDppWaveShr1 = 0x138;
+constexpr int kDppRowMirror = 0x140;
+constexpr int kDppRowHalfMirror = 0x141;
+constexpr int kDppRowBcast15 = 0x142;
+constexpr int kDppRowBcast31 = 0x143;
+
+template <int Ctrl, int RowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  // lanes whose source is outside the row / not selected read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, 0xF, false);
+}
+
+// Sum over the aligned group of G lanes containing this lane (G pow2 <= 64),
+// broadcast to every lane of the group.  All lanes must be active.
 __device__ __forceinline__ uint32_t group_sum(uint32_t v, uint32_t G) {
-  for (uint32_t m = 1; m < G; m <<= 1) v += shfl_xor(v, (int)m);
+  if (G >= 2) v += dpp<kDppQuadXor1>(v);
+  if (G >= 4) v += dpp<kDppQuadXor2>(v);
+  if (G >= 8) v += dpp<kDppRowHalfMirror>(v);
+  if (G >= 16) v += dpp<kDppRowMirror>(v);
+  if (G >= 32) {
+    auto t = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = t[0] + t[1];
+  }
+  if (G >= 64) {
+    auto t = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = t[0] + t[1];
+  }
   return v;
 }
 
+// Inclusive prefix sum over the 64 lanes (all active).
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-  const uint32_t l = lane_id();
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint32_t t = shfl_up(v, d);
-    if (l >= (uint32_t)d) v += t;
-  }
+  v += dpp<kDppRowShr1>(v);
+  v += dpp<kDppRowShr2>(v);
+  v += dpp<kDppRowShr4>(v);
+  v += dpp<kDppRowShr8>(v);
+  v += dpp<kDppRowBcast15, 0xA>(v);
+  v += dpp<kDppRowBcast31, 0xC>(v);
   return v;
 }
 
+// Inclusive prefix max over the 64 lanes (all active, values >= 0).
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  const uint32_t l = lane_id();
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint32_t t = shfl_up(v, d);
-    if (l >= (uint32_t)d) v = v > t ? v : t;
-  }
+  v = max(v, dpp<kDppRowShr1>(v));
+  v = max(v, dpp<kDppRowShr2>(v));
+  v = max(v, dpp<kDppRowShr4>(v));
+  v = max(v, dpp<kDppRowShr8>(v));
+  v = max(v, dpp<kDppRowBcast15, 0xA>(v));
+  v = max(v, dpp<kDppRowBcast31, 0xC>(v));
   return v;
 }
+
+// Value of lane l-1 (0 for lane 0).
+__device__ __forceinline__ uint32_t from_left(uint32_t v) { return dpp<kDppWaveShr1>(v); }
 
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
@@ -109,26 +162,79 @@ struct EncParams {
   uint32_t bs, cs, be, ulsb;
 };
 
-// Loads the `cnt` (<= 8) samples p[0], p[cs], ... ; unused slots are 0.
-__device__ __forceinline__ void load8(const uint16_t* p, uint32_t cs, uint32_t comp, uint32_t cnt,
-                                      uint32_t raw[8]) {
-  if (cnt == 8 && cs == 1 && ((uintptr_t)p & 15) == 0) {
-    uint4 v = *reinterpret_cast<const uint4*>(p);
-    raw[0] = v.x & 0xFFFFu; raw[1] = v.x >> 16;
-    raw[2] = v.y & 0xFFFFu; raw[3] = v.y >> 16;
-    raw[4] = v.z & 0xFFFFu; raw[5] = v.z >> 16;
-    raw[6] = v.w & 0xFFFFu; raw[7] = v.w >> 16;
-  } else if (cnt == 8 && cs == 2 && ((uintptr_t)(p - comp) & 15) == 0) {
-    const uint4* q = reinterpret_cast<const uint4*>(p - comp);
-    uint4 a = q[0], b = q[1];
-    uint32_t sh = 16 * comp;
-    raw[0] = (a.x >> sh) & 0xFFFFu; raw[1] = (a.y >> sh) & 0xFFFFu;
-    raw[2] = (a.z >> sh) & 0xFFFFu; raw[3] = (a.w >> sh) & 0xFFFFu;
-    raw[4] = (b.x >> sh) & 0xFFFFu; raw[5] = (b.y >> sh) & 0xFFFFu;
-    raw[6] = (b.z >> sh) & 0xFFFFu; raw[7] = (b.w >> sh) & 0xFFFFu;
+// Per-lane sub-block geometry of one encode iteration.
+struct EncGeom {
+  uint32_t n;        // samples in this lane's sub-block (0: no sub-block)
+  uint32_t cnt;      // samples owned by this lane (<= 8)
+  uint32_t m_first;  // stream index of the lane's first sample
+  uint32_t comp;     // component stream
+};
+
+__device__ __forceinline__ EncGeom enc_geom(uint32_t s, uint32_t j, uint32_t nsb, uint32_t N, uint32_t bs,
+                                            uint32_t cs) {
+  EncGeom g;
+  // codec.h:88-97: chunks of cs*bs samples; component i takes i, i+cs, ...
+  const uint32_t chunk = cs == 1 ? s : s >> 1;
+  g.comp = s - chunk * cs;
+  const uint32_t cbase = chunk * cs * bs;
+  g.n = 0;
+  if (s < nsb) {
+    const uint32_t rem = (N - cbase) / cs;
+    g.n = rem < bs ? rem : bs;
+  }
+  const uint32_t k0 = 8 * j;
+  g.cnt = k0 < g.n ? min(g.n - k0, 8u) : 0u;
+  g.m_first = cbase + g.comp + cs * k0;
+  return g;
+}
+
+// Raw loads of one iteration, kept packed so the next iteration's loads can
+// be in flight while the current one is processed.
+struct EncLoad {
+  uint4 a, b;
+  uint32_t prev;
+};
+
+__device__ __forceinline__ EncLoad enc_load(const uint16_t* in, const EncGeom& g, uint32_t cs, bool vec_ok) {
+  EncLoad L;
+  // previous same-component sample (delta reference); the stream's first
+  // sample of a component is its own reference (codec.h:72-73: last = read(in[i]))
+  const uint32_t pi = g.cnt ? (g.m_first >= cs ? g.m_first - cs : g.m_first) : 0u;
+  L.prev = in[pi];
+  if (vec_ok) {
+    const uint4* q = reinterpret_cast<const uint4*>(g.cnt == 8 ? in + (g.m_first - g.comp) : in);
+    L.a = q[0];
+    L.b = cs == 2 ? q[1] : L.a;
+    if (g.cnt != 8 && g.cnt != 0) {  // stream tail
+      uint32_t w[8];
+      for (uint32_t i = 0; i < 8; ++i) w[i] = i < g.cnt ? (uint32_t)in[g.m_first + cs * i] : 0u;
+      L.a = make_uint4(w[0] | (w[1] << 16), w[2] | (w[3] << 16), w[4] | (w[5] << 16), w[6] | (w[7] << 16));
+      L.b = L.a;
+    }
   } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) raw[i] = (uint32_t)i < cnt ? (uint32_t)p[cs * i] : 0u;
+    uint32_t w[8];
+    for (uint32_t i = 0; i < 8; ++i) w[i] = i < g.cnt ? (uint32_t)in[g.m_first + cs * i] : 0u;
+    L.a = make_uint4(w[0] | (w[1] << 16), w[2] | (w[3] << 16), w[4] | (w[5] << 16), w[6] | (w[7] << 16));
+    L.b = L.a;
+  }
+  return L;
+}
+
+// Unpacks the lane's 8 raw samples.  `split` layout: cs == 2 vector loads
+// hold both components interleaved, the lane's samples in half `comp`.
+__device__ __forceinline__ void enc_unpack(const EncLoad& L, uint32_t cs, uint32_t comp, bool vec_full,
+                                           uint32_t raw[8]) {
+  if (cs == 2 && vec_full) {
+    const uint32_t sh = 16 * comp;
+    raw[0] = (L.a.x >> sh) & 0xFFFFu; raw[1] = (L.a.y >> sh) & 0xFFFFu;
+    raw[2] = (L.a.z >> sh) & 0xFFFFu; raw[3] = (L.a.w >> sh) & 0xFFFFu;
+    raw[4] = (L.b.x >> sh) & 0xFFFFu; raw[5] = (L.b.y >> sh) & 0xFFFFu;
+    raw[6] = (L.b.z >> sh) & 0xFFFFu; raw[7] = (L.b.w >> sh) & 0xFFFFu;
+  } else {
+    raw[0] = L.a.x & 0xFFFFu; raw[1] = L.a.x >> 16;
+    raw[2] = L.a.y & 0xFFFFu; raw[3] = L.a.y >> 16;
+    raw[4] = L.a.z & 0xFFFFu; raw[5] = L.a.z >> 16;
+    raw[6] = L.a.w & 0xFFFFu; raw[7] = L.a.w >> 16;
   }
 }
 
@@ -141,10 +247,10 @@ __device__ __forceinline__ uint32_t shr_sum8(const uint32_t d[8], uint32_t f) {
 
 // ORs the (<= 16 bit) code `v` into the window at bit `rel`.
 __device__ __forceinline__ void emit_bits(uint32_t* win, uint32_t rel, uint32_t v) {
-  uint32_t w = rel >> 5, sh = rel & 31u;
+  const uint32_t w = rel >> 5, sh = rel & 31u;
   atomicOr(&win[w], v << sh);
   if (sh) {
-    uint32_t hi = v >> (32u - sh);
+    const uint32_t hi = v >> (32u - sh);
     if (hi) atomicOr(&win[w + 1], hi);
   }
 }
@@ -167,6 +273,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint16_t* in = p.in + p.in_off[b];
   uint8_t* out8 = p.out + ooff;
   uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
+  const bool vec_ok = (bs & 7u) == 0 && ((uintptr_t)in & 15u) == 0 && N >= 8 * cs;
 
   for (uint32_t i = lane; i < (uint32_t)kWinWords; i += kWave) win[i] = 0;
   __syncthreads();
@@ -185,33 +292,28 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint32_t spw = kWave / G;
   const uint32_t g = lane / G, j = lane & (G - 1);
 
+  EncGeom ngeo = enc_geom(g, j, nsb, N, bs, cs);
+  EncLoad nld = enc_load(in, ngeo, cs, vec_ok);
   for (uint32_t s0 = 0; s0 < nsb; s0 += spw) {
-    // ---- sub-block geometry (codec.h:88-97: chunk of cs*bs, component i
-    //      takes samples i, i+cs, ...) ----
-    const uint32_t s = s0 + g;
-    const bool sb_valid = s < nsb;
-    const uint32_t chunk = s / cs, comp = s - chunk * cs;
-    const uint32_t cbase = chunk * chunk_len;
-    uint32_t n = 0;
-    if (sb_valid) {
-      uint32_t rem = (N - cbase) / cs;
-      n = rem < bs ? rem : bs;
+    const EncGeom geo = ngeo;
+    const EncLoad ld = nld;
+    if (s0 + spw < nsb) {  // prefetch the next group of sub-blocks
+      ngeo = enc_geom(s0 + spw + g, j, nsb, N, bs, cs);
+      nld = enc_load(in, ngeo, cs, vec_ok);
     }
-    const uint32_t k0 = 8 * j;
-    const uint32_t cnt = k0 < n ? (n - k0 < 8 ? n - k0 : 8) : 0;
-    const uint32_t m_first = cbase + comp + cs * k0;
+    const bool sb_valid = geo.n != 0;
+    const uint32_t n = geo.n, cnt = geo.cnt;
 
     // ---- zig-zag deltas (encode.h:116-123) ----
     uint32_t raw[8], d[8];
-    load8(in + m_first, cs, comp, cnt, raw);
-    uint32_t prev = 0;
-    if (cnt) prev = px_read(m_first >= cs ? (uint32_t)in[m_first - cs] : raw[0], be, ulsb);
+    enc_unpack(ld, cs, geo.comp, vec_ok && cnt == 8, raw);
+    uint32_t prev = px_read(ld.prev, be, ulsb);
     uint32_t lsum = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      uint32_t px = px_read(raw[i], be, ulsb);
+      const uint32_t px = px_read(raw[i], be, ulsb);
       d[i] = (uint32_t)i < cnt ? zigzag16(px, prev) : 0u;
-      prev = (uint32_t)i < cnt ? px : prev;
+      prev = px;
       lsum += d[i];
     }
     const uint32_t sum = group_sum(lsum, G);
@@ -235,13 +337,9 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
       if (!__any(act)) break;
       const uint32_t f = act ? (uint32_t)(cand + dir) : 0u;
       const uint32_t t = n * (f + 1) + group_sum(shr_sum8(d, f), G);
-      if (act) {
-        if (t > bits) {
-          walking = false;
-        } else {
-          bits = t;
-          cand += dir;
-        }
+      if (act && t <= bits) {
+        bits = t;
+        cand += dir;
       } else {
         walking = false;
       }
@@ -294,14 +392,14 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
     if (F > win_w0) {
       const uint32_t nch = (F - win_w0) >> 2;
       for (uint32_t c = lane; c < nch; c += kWave) {
-        uint4 v = *reinterpret_cast<const uint4*>(&win[4 * c]);
+        const uint4 v = *reinterpret_cast<const uint4*>(&win[4 * c]);
         *reinterpret_cast<uint4*>(&out32[win_w0 + 4 * c]) = v;
       }
       const uint32_t used = full_end - win_w0 + 1;
       const uint32_t tail0 = F - win_w0;
-      uint32_t keep = lane < 4 ? win[tail0 + lane] : 0u;
+      const uint32_t keep = lane < 4 ? win[tail0 + lane] : 0u;
       __syncthreads();
-      for (uint32_t i = lane; i < used && i < (uint32_t)kWinWords; i += kWave) win[i] = 0;
+      for (uint32_t i = lane; i < used; i += kWave) win[i] = 0;
       __syncthreads();
       if (lane < 4) win[lane] = keep;
       __syncthreads();
@@ -325,6 +423,12 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
 // ===========================================================================
 // DECODE
 // ===========================================================================
+// Two streams per wavefront: lanes 0-31 decode stream 2*blockIdx.x, lanes
+// 32-63 stream 2*blockIdx.x+1.  A Rice sub-block of ~1000 bits (Poisson
+// sensor data, bs 128) then covers one half-wave of 32 lanes x 32-bit words,
+// so every instruction of the serial sub-block loop serves two streams.  All
+// per-stream state is uniform within a half; cross-lane ops (DPP row shifts,
+// row_bcast15) never cross the half boundary.
 struct DecParams {
   const uint8_t* in;
   const uint64_t* in_off;
@@ -337,6 +441,32 @@ struct DecParams {
   uint32_t bs, cs, be, ulsb;
 };
 
+constexpr uint32_t kHalf = 32;                // lanes per stream
+constexpr uint32_t kRingWords = 1024;         // per-stream LDS ring of the compressed stream (4 KiB)
+constexpr uint32_t kRingMask = kRingWords - 1;
+constexpr uint32_t kChunkWords = 4 * kHalf;   // refill unit: 16 B per lane of a half
+constexpr uint32_t kAhead = 288;              // words kept resident ahead of the read position
+constexpr uint32_t kPosCap = 512;             // terminator positions of one Rice pass
+
+__device__ __forceinline__ uint32_t half_incl_sum(uint32_t v) {
+  v += dpp<kDppRowShr1>(v);
+  v += dpp<kDppRowShr2>(v);
+  v += dpp<kDppRowShr4>(v);
+  v += dpp<kDppRowShr8>(v);
+  v += dpp<kDppRowBcast15, 0xA>(v);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t half_last(uint32_t v) {
+  const uint32_t a = readlane(v, kHalf - 1), b = readlane(v, kWave - 1);
+  return lane_id() >= kHalf ? b : a;
+}
+
+__device__ __forceinline__ uint32_t half_ballot(bool pred) {
+  const uint64_t m = __ballot(pred);
+  return lane_id() >= kHalf ? (uint32_t)(m >> 32) : (uint32_t)m;
+}
+
 // 32-bit word `w` of the stream, zero past the end (bitstream_reader.h:165-166
 // zero-pads the last packet; reading beyond it is checked separately).
 __device__ __forceinline__ uint32_t stream_word(const uint8_t* in, uint32_t nbytes, uint32_t w) {
@@ -348,210 +478,341 @@ __device__ __forceinline__ uint32_t stream_word(const uint8_t* in, uint32_t nbyt
   return v;
 }
 
-// `width` (<= 16) bits at absolute bit position `pos`, LSB first.
-__device__ __forceinline__ uint32_t stream_bits(const uint8_t* in, uint32_t nbytes, uint32_t pos,
-                                                uint32_t width) {
-  const uint32_t w = pos >> 5, sh = pos & 31u;
-  uint64_t v = (uint64_t)stream_word(in, nbytes, w) | ((uint64_t)stream_word(in, nbytes, w + 1) << 32);
-  return (uint32_t)(v >> sh) & ((1u << width) - 1u);
+// This lane's 4 words of the 128-word chunk starting at word `w0`.
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* in, uint32_t nbytes, uint32_t w0, bool aligned16) {
+  const uint32_t w = w0 + 4 * (lane_id() & (kHalf - 1));
+  if (aligned16 && 4 * w + 16 <= nbytes) return *reinterpret_cast<const uint4*>(in + 4 * w);
+  return make_uint4(stream_word(in, nbytes, w), stream_word(in, nbytes, w + 1), stream_word(in, nbytes, w + 2),
+                    stream_word(in, nbytes, w + 3));
 }
 
 // Terminator chain through one 32-bit word: starting the unary search at bit
 // `entry`, mark every '1' that ends a unary run and skip its fs remainder
 // bits.  Returns the terminator mask; *exit = where the search continues in
-// the next word (0 if it runs off the word while searching).
-__device__ __forceinline__ uint32_t chain_word(uint32_t word, uint32_t entry, uint32_t fs,
-                                               uint32_t* exit) {
-  uint32_t T = 0, sigma = entry, ex = 0;
-  while (sigma < 32) {
-    const uint32_t y = word >> sigma;
-    if (y == 0) break;
-    const uint32_t t = sigma + (uint32_t)__builtin_ctz(y);
-    T |= 1u << t;
-    sigma = t + fs + 1;
+// the next word (0 if it runs off the word while searching).  Branch-free
+// body, wave-uniform trip count: sigma in [32, 45] = left the word after a
+// terminator, 63 = ran off while searching ((0:word) >> 63 == 0 keeps it).
+// Pass entry >= 32 for a lane that has nothing to do.
+__device__ __forceinline__ uint32_t chain_word(uint32_t word, uint32_t entry, uint32_t fs, uint32_t* exit,
+                                               uint32_t* iters = nullptr) {
+  uint32_t T = 0, sigma = entry;
+  const uint64_t w64 = word;
+  while (__any(sigma < 32)) {
+    if (iters) ++*iters;
+    const bool act = sigma < 32;
+    const uint32_t y = (uint32_t)(w64 >> sigma);  // 0 once sigma >= 32
+    const uint32_t t = sigma + (uint32_t)__builtin_ctz(y | 0x80000000u);
+    const bool hit = y != 0;
+    T = hit ? (T | (1u << t)) : T;
+    sigma = hit ? t + fs + 1 : (act ? 63u : sigma);
   }
-  if (sigma >= 32) ex = sigma - 32;
-  *exit = ex;
+  *exit = sigma < 63 ? sigma - 32 : 0u;
   return T;
 }
 
-__device__ __forceinline__ void set_status(int32_t* st, uint32_t b, int32_t v) {
-  if (lane_id() == 0) st[b] = v;
+// Exit state only (the lookback chain).
+__device__ __forceinline__ uint32_t chain_exit(uint32_t word, uint32_t entry, uint32_t fs) {
+  uint32_t sigma = entry;
+  const uint64_t w64 = word;
+  while (__any(sigma < 32)) {
+    const bool act = sigma < 32;
+    const uint32_t y = (uint32_t)(w64 >> sigma);
+    const uint32_t t = sigma + (uint32_t)__builtin_ctz(y | 0x80000000u);
+    sigma = y != 0 ? t + fs + 1 : (act ? 63u : sigma);
+  }
+  return sigma < 63 ? sigma - 32 : 0u;
+}
+
+// Exact terminator mask of this lane's 32-bit word.  A lane does not know
+// where the unary search enters its word (that depends on every code to its
+// left), so it runs the terminator chain for every possible entry state
+// 0..fs side by side (independent chains: instruction-level parallelism,
+// no speculation), giving its transfer function entry -> exit.  The first
+// lane of a half has one exact entry (e0).  Entries then resolve left to
+// right: a lane whose exit is the same for every entry (chains merged inside
+// the word, the common case) breaks the dependency, so the resolution takes
+// as many rounds as the longest run of entry-dependent lanes.
+template <int NCH>
+__device__ __forceinline__ uint32_t resolve_word(uint32_t own, uint32_t fs, uint32_t e0, bool first, bool act,
+                                                 uint32_t nit, uint32_t* ex_out) {
+  uint32_t sig[NCH], T[NCH];
+  const uint64_t w64 = own;
+#pragma unroll
+  for (int e = 0; e < NCH; ++e) {
+    const uint32_t se = first ? (e == 0 ? e0 : 63u) : ((uint32_t)e <= fs ? (uint32_t)e : 63u);
+    sig[e] = act ? se : 63u;
+    T[e] = 0;
+  }
+  for (uint32_t it = 0; it < nit; ++it) {
+#pragma unroll
+    for (int e = 0; e < NCH; ++e) {
+      const bool a = sig[e] < 32;
+      const uint32_t y = (uint32_t)(w64 >> sig[e]);
+      const uint32_t t = sig[e] + (uint32_t)__builtin_ctz(y | 0x80000000u);
+      const bool hit = y != 0;
+      T[e] = hit ? (T[e] | (1u << t)) : T[e];
+      sig[e] = hit ? t + fs + 1 : (a ? 63u : sig[e]);
+    }
+  }
+  uint64_t F = 0;
+  bool cst = true;
+  const uint32_t x0 = sig[0] < 63 ? sig[0] - 32 : 0u;
+#pragma unroll
+  for (int e = 0; e < NCH; ++e) {
+    const uint32_t x = sig[e] < 63 ? sig[e] - 32 : 0u;
+    F |= (uint64_t)x << (4 * e);
+    cst = cst && (first || (uint32_t)e > fs || x == x0);
+  }
+  // resolve entry states left to right
+  uint32_t entry = 0;
+  bool known = first || !act;
+  for (;;) {
+    const bool out_known = known || cst;
+    const uint32_t out_val = (uint32_t)(F >> (4 * entry)) & 15u;
+    const bool lk = from_left(out_known ? 1u : 0u) != 0;
+    const uint32_t lv = from_left(out_val);
+    entry = (!known && lk) ? lv : entry;
+    known = known || lk;
+    if (!__any(!known)) break;
+  }
+  uint32_t Tt = T[0];
+#pragma unroll
+  for (int e = 1; e < NCH; ++e) Tt = entry == (uint32_t)e ? T[e] : Tt;
+  *ex_out = (uint32_t)(F >> (4 * entry)) & 15u;
+  return Tt;
 }
 
 __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
-  __shared__ __attribute__((aligned(16))) uint16_t tile[kTileSamples];
-  const uint32_t b = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) uint32_t ring_s[2][kRingWords];
+  __shared__ __attribute__((aligned(16))) uint16_t tile_s[2][kTileSamples];
+  __shared__ uint32_t pos_s[2][kPosCap + 1];  // + one dummy slot
   const uint32_t lane = lane_id();
+  const uint32_t h = lane >> 5, hl = lane & (kHalf - 1);
+  uint32_t* ring = ring_s[h];
+  uint16_t* tile = tile_s[h];
+  uint32_t* posbuf = pos_s[h];
   const uint32_t bs = p.bs, cs = p.cs, be = p.be, ulsb = p.ulsb;
-  const uint64_t n64 = p.n_samples[b];
-  const uint64_t ioff = p.in_off[b];
-  const uint64_t nbytes64 = p.in_bytes[b];
-  if (n64 % cs != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ioff & 3u) || nbytes64 >= (UINT64_C(1) << 29)) {
-    set_status(p.status, b, RPP_INVALID_ARGUMENT);
-    return;
+  const uint32_t b = 2 * blockIdx.x + h;
+#ifdef RPP_STATS
+  uint32_t stat_acc[16] = {0};
+  uint32_t* itp2 = &stat_acc[3];
+  unsigned long long tprev_;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
+#else
+  uint32_t* itp2 = nullptr;
+#endif
+
+  // ---- per-stream setup (uniform within the half) ----
+  int32_t status = RPP_OK;
+  uint32_t N = 0, nbytes = 0;
+  const uint8_t* in = p.in;
+  uint16_t* out = p.out;
+  if (b < p.nblocks) {
+    const uint64_t n64 = p.n_samples[b];
+    const uint64_t ioff = p.in_off[b];
+    const uint64_t nb64 = p.in_bytes[b];
+    if (n64 % cs != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ioff & 3u) || nb64 >= (UINT64_C(1) << 29)) {
+      status = RPP_INVALID_ARGUMENT;
+    } else {
+      N = (uint32_t)n64;
+      nbytes = (uint32_t)nb64;
+      in = p.in + ioff;
+      out = p.out + p.out_off[b];
+    }
   }
-  const uint32_t N = (uint32_t)n64;
-  const uint32_t nbytes = (uint32_t)nbytes64;
-  const uint8_t* in = p.in + ioff;
-  uint16_t* out = p.out + p.out_off[b];
+  const bool aligned16 = ((uintptr_t)in & 15u) == 0;
   // last readable bit + 1: the reader pulls whole 8-byte packets
   // (bitstream_reader.h:149-183), so it only throws past this point.
   const uint32_t lim = 64u * ((nbytes + 7u) >> 3);
-
-  if (16 * cs > lim) {
-    set_status(p.status, b, RPP_TRUNCATED_INPUT);
-    return;
-  }
-  uint32_t last[2];
-  last[0] = stream_bits(in, nbytes, 0, 16);
-  last[1] = cs > 1 ? stream_bits(in, nbytes, 16, 16) : 0u;
-  uint32_t P = 16 * cs;
-
   const uint32_t chunk_len = cs * bs;
-  const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
-  for (uint32_t chunk = 0; chunk < nchunks; ++chunk) {
-    const uint32_t cbase = chunk * chunk_len;
-    const uint32_t clen = N - cbase < chunk_len ? N - cbase : chunk_len;
-    const uint32_t n = clen / cs;
-    for (uint32_t comp = 0; comp < cs; ++comp) {
-      // decode.h:60: 4-bit fs+1 header
-      if (P + 4 > lim) {
-        set_status(p.status, b, RPP_TRUNCATED_INPUT);
-        return;
-      }
-      const uint32_t fsp1 = stream_bits(in, nbytes, P, 4);
-      P += 4;
-      uint32_t acc = last[comp];
-      if (fsp1 == 0) {
-        // decode.h:79-80: all samples = write(last)
-        const uint32_t v = px_write(acc, be, ulsb);
-        for (uint32_t k = lane; k < n; k += kWave) tile[comp + cs * k] = (uint16_t)v;
-      } else if (fsp1 == 15) {
-        // decode.h:72-77: raw stored values; last = read(last sample)
-        if ((uint64_t)P + 16ull * n > lim) {
-          set_status(p.status, b, RPP_TRUNCATED_INPUT);
-          return;
-        }
-        for (uint32_t k = lane; k < n; k += kWave)
-          tile[comp + cs * k] = (uint16_t)stream_bits(in, nbytes, P + 16 * k, 16);
-        acc = px_read(stream_bits(in, nbytes, P + 16 * (n - 1), 16), be, ulsb);
-        P += 16 * n;
-      } else {
-        // decode.h:62-71: Rice codes, fs = fsp1 - 1
-        const uint32_t fs = fsp1 - 1;
-        const uint32_t lowmask = (1u << fs) - 1u;
-        uint32_t K = 0;             // codes decoded in earlier passes
-        uint32_t sigma_carry = P;   // search start of the next code
-        uint32_t W0 = P >> 5;       // first word of this pass
-        uint32_t e0 = P & 31u;      // exact entry state of lane 0
-        for (;;) {
-          if (32ull * W0 >= lim) {
-            set_status(p.status, b, RPP_TRUNCATED_INPUT);
-            return;
-          }
-          const uint32_t own = stream_word(in, nbytes, W0 + lane);
-          uint32_t nxt = shfl_down(own, 1);
-          if (lane == kWave - 1) nxt = stream_word(in, nbytes, W0 + kWave);
-          const uint32_t prv = shfl_up(own, 1);
-          // speculative entry state from the left neighbour's word
-          uint32_t entry = e0, ex;
-          if (lane != 0) chain_word(prv, 0, fs, &entry);
-          uint32_t T = chain_word(own, entry, fs, &ex);
-          // verify entry == left lane's exit; re-run until consistent
-          for (;;) {
-            const uint32_t left_exit = shfl_up(ex, 1);
-            const bool bad = lane != 0 && left_exit != entry;
-            if (!__any(bad)) break;
-            if (bad) {
-              entry = left_exit;
-              T = chain_word(own, entry, fs, &ex);
-            }
-          }
-          const uint32_t c = (uint32_t)__builtin_popcount(T);
-          const uint32_t cincl = wave_incl_sum(c);
-          const uint32_t cexcl = cincl - c;
-          const uint32_t ctot = readlane(cincl, kWave - 1);
-          const uint32_t wbit = 32u * (W0 + lane);
-          const uint32_t my_last_sigma = c ? wbit + (31u - (uint32_t)__clz(T)) + fs + 1 : 0u;
-          const uint32_t smax = wave_incl_max(my_last_sigma);
-          uint32_t sprev = shfl_up(smax, 1);
-          if (lane == 0) sprev = 0;
-          const uint32_t sigma_in = sprev > sigma_carry ? sprev : sigma_carry;
-          const uint64_t own64 = (uint64_t)own | ((uint64_t)nxt << 32);
+  const uint32_t nsb = b < p.nblocks && status == RPP_OK ? ((N + chunk_len - 1) / chunk_len) * cs : 0u;
 
-          // pass A: this lane's delta sum over codes with index < n
-          uint32_t dsum = 0;
-          {
-            uint32_t TT = T, sig = sigma_in, k = K + cexcl;
-            while (TT) {
-              const uint32_t t = (uint32_t)__builtin_ctz(TT);
-              TT &= TT - 1;
-              const uint32_t tabs = wbit + t;
-              const uint32_t q = tabs - sig;
-              const uint32_t rem = (uint32_t)(own64 >> (t + 1)) & lowmask;
-              const uint32_t diff = (q << fs) | rem;
-              const uint32_t delta = (diff >> 1) ^ (0u - (diff & 1u));
-              if (k < n) dsum += delta;
-              ++k;
-              sig = tabs + fs + 1;
-            }
+  // ---- fill the ring; refills are synchronous but only every ~8 sub-blocks
+  //      (a register-carried prefetch made the compiler wait on every
+  //      iteration for the output stores queued behind it) ----
+  uint32_t fill_w = 0;
+  auto refill = [&](bool go) {  // appends 2 chunks (256 words) to this half's ring
+    if (go) {
+      const uint4 v0 = load_chunk(in, nbytes, fill_w, aligned16);
+      const uint4 v1 = load_chunk(in, nbytes, fill_w + kChunkWords, aligned16);
+      *reinterpret_cast<uint4*>(&ring[(fill_w + 4 * hl) & kRingMask]) = v0;
+      *reinterpret_cast<uint4*>(&ring[(fill_w + kChunkWords + 4 * hl) & kRingMask]) = v1;
+    }
+    fill_w = go ? fill_w + 2 * kChunkWords : fill_w;
+  };
+  refill(true);
+  refill(true);
+  __syncthreads();
+  // keeps words [w - 1, w + kAhead) of this half's stream resident
+  auto ensure = [&](uint32_t w, bool act) {
+    while (__any(act && fill_w < w + kAhead)) refill(act && fill_w < w + kAhead);
+    __syncthreads();
+  };
+  auto rbits = [&](uint32_t pos, uint32_t width) -> uint32_t {  // width <= 16
+    const uint32_t w = pos >> 5;
+    const uint64_t v = (uint64_t)ring[w & kRingMask] | ((uint64_t)ring[(w + 1) & kRingMask] << 32);
+    return (uint32_t)(v >> (pos & 31u)) & ((1u << width) - 1u);
+  };
+
+  uint32_t last0 = 0, last1 = 0, P = 16 * cs;
+  if (nsb != 0 || (b < p.nblocks && status == RPP_OK)) {
+    if (16 * cs > lim) status = RPP_TRUNCATED_INPUT;
+    last0 = rbits(0, 16);
+    last1 = cs > 1 ? rbits(16, 16) : 0u;
+  }
+
+  for (uint32_t s = 0;; ++s) {
+    bool active = s < nsb && status == RPP_OK;
+    if (!__any(active)) break;
+    const uint32_t chunk = cs == 1 ? s : s >> 1;
+    const uint32_t comp = s - chunk * cs;
+    const uint32_t cbase = chunk * chunk_len;
+    const uint32_t clen = active ? min(N - cbase, chunk_len) : 0u;
+    const uint32_t n = clen / cs;
+    ensure(P >> 5, active);
+    // decode.h:60: 4-bit fs+1 header
+    if (active && P + 4 > lim) {
+      status = RPP_TRUNCATED_INPUT;
+      active = false;
+    }
+    const uint32_t fsp1 = active ? rbits(P, 4) : 0u;
+    P += 4;
+    RPP_STAT(6, 1);
+    uint32_t acc = comp ? last1 : last0;
+    if (active && fsp1 == 0) {
+      // decode.h:79-80: all samples = write(last)
+      const uint32_t v = px_write(acc, be, ulsb);
+      for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = (uint16_t)v;
+    }
+    if (active && fsp1 == 15) {
+      // decode.h:72-77: raw stored values; last = read(last sample)
+      if ((uint64_t)P + 16ull * n > lim) {
+        status = RPP_TRUNCATED_INPUT;
+        active = false;
+      } else {
+        for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = (uint16_t)rbits(P + 16 * k, 16);
+        acc = px_read(rbits(P + 16 * (n - 1), 16), be, ulsb);
+        P += 16 * n;
+      }
+    }
+    bool rdo = active && fsp1 != 0 && fsp1 != 15;
+    RPP_TSTAMP(9);
+    if (__any(rdo)) {
+      // decode.h:62-71: Rice codes, fs = fsp1 - 1
+      const uint32_t fs = rdo ? fsp1 - 1 : 0u;
+      const uint32_t lowmask = (1u << fs) - 1u;
+      // wave-uniform chain shape: entries = max fs + 1, steps = ceil(32 / (min fs + 1))
+      const uint32_t fa = readlane(rdo ? fs : 0u, 0), fb = readlane(rdo ? fs : 0u, kHalf);
+      const bool ra = readlane(rdo ? 1u : 0u, 0) != 0, rb = readlane(rdo ? 1u : 0u, kHalf) != 0;
+      const uint32_t fmax = max(ra ? fa : 0u, rb ? fb : 0u);
+      const uint32_t fmin = min(ra ? fa : 15u, rb ? fb : 15u);
+      const uint32_t nch = fmax + 1;
+      const uint32_t nit = (32 + fmin) / (fmin + 1);
+      uint32_t K = 0;            // codes decoded in earlier passes
+      uint32_t sigma_carry = P;  // search start of the next code
+      uint32_t W0 = P >> 5;      // first word of this pass
+      uint32_t e0 = P & 31u;     // exact entry state of lane 0 of the half
+      while (__any(rdo)) {
+        RPP_STAT(0, 1);
+        if (rdo && 32ull * W0 >= lim) {
+          status = RPP_TRUNCATED_INPUT;
+          rdo = false;
+        }
+        ensure(W0, rdo);
+        RPP_TSTAMP(9);
+        const uint32_t own = ring[(W0 + hl) & kRingMask];
+        // chains for every entry state, then left-to-right resolution
+        uint32_t ex, T;
+        switch (nch) {
+#define RPP_RESOLVE_CASE(k) \
+  case k: T = resolve_word<k>(own, fs, e0, hl == 0, rdo, nit, &ex); break;
+          RPP_RESOLVE_CASE(1) RPP_RESOLVE_CASE(2) RPP_RESOLVE_CASE(3) RPP_RESOLVE_CASE(4)
+          RPP_RESOLVE_CASE(5) RPP_RESOLVE_CASE(6) RPP_RESOLVE_CASE(7) RPP_RESOLVE_CASE(8)
+          RPP_RESOLVE_CASE(9) RPP_RESOLVE_CASE(10) RPP_RESOLVE_CASE(11) RPP_RESOLVE_CASE(12)
+          RPP_RESOLVE_CASE(13)
+          default: T = resolve_word<14>(own, fs, e0, hl == 0, rdo, nit, &ex); break;
+#undef RPP_RESOLVE_CASE
+        }
+        RPP_TSTAMP(10);
+        RPP_TSTAMP(11);
+        const uint32_t c = (uint32_t)__builtin_popcount(T);
+        const uint32_t cincl = half_incl_sum(c);
+        const uint32_t cexcl = cincl - c;
+        const uint32_t ctot = half_last(cincl);
+        const uint32_t need = rdo ? min(ctot, n - K) : 0u;
+        const uint32_t wbit = 32u * (W0 + hl);
+        // materialise the absolute positions of the first `need` terminators
+        {
+          uint32_t TT = T, idx = cexcl;
+          for (uint32_t it = 0; it < nit; ++it) {  // popcount(T) <= nit
+            const bool hit = TT != 0 && idx < need;
+            const uint32_t t = (uint32_t)__builtin_ctz(TT | 0x80000000u);
+            posbuf[hit ? idx : kPosCap] = wbit + t;
+            TT &= TT - 1;
+            ++idx;
           }
-          const uint32_t dincl = wave_incl_sum(dsum);
-          // pass B: values
-          uint32_t endpos = 0;
-          {
-            uint32_t TT = T, sig = sigma_in, k = K + cexcl;
-            uint32_t v = acc + dincl - dsum;
-            while (TT) {
-              const uint32_t t = (uint32_t)__builtin_ctz(TT);
-              TT &= TT - 1;
-              const uint32_t tabs = wbit + t;
-              const uint32_t q = tabs - sig;
-              const uint32_t rem = (uint32_t)(own64 >> (t + 1)) & lowmask;
-              const uint32_t diff = (q << fs) | rem;
-              v += (diff >> 1) ^ (0u - (diff & 1u));
-              if (k < n) tile[comp + cs * k] = (uint16_t)px_write(v, be, ulsb);
-              if (k == n - 1) endpos = tabs + fs + 1;
-              ++k;
-              sig = tabs + fs + 1;
-            }
-          }
-          if (K + ctot >= n) {
-            const uint32_t idx = n - 1 - K;
-            const uint64_t owner = __ballot(cexcl <= idx && idx < cincl);
-            const int L = (int)__builtin_ctzll(owner);
-            const uint32_t E = readlane(endpos, L);
-            acc += readlane(dincl, kWave - 1);
-            if (E > lim) {
-              set_status(p.status, b, RPP_TRUNCATED_INPUT);
-              return;
-            }
-            P = E;
-            break;
-          }
+        }
+        __syncthreads();
+        RPP_TSTAMP(12);
+        // code-parallel extraction: code i of this pass on lane i % 32
+        for (uint32_t r = 0; __any(r < need); r += kHalf) {
+          const uint32_t i = r + hl;
+          const bool valid = i < need;
+          const uint32_t ii = valid ? i : 0u;
+          const uint32_t t = posbuf[ii];
+          const uint32_t sig = ii == 0 ? sigma_carry : posbuf[ii - 1] + fs + 1;
+          const uint32_t rp = t + 1, rw = rp >> 5;
+          const uint64_t v = (uint64_t)ring[rw & kRingMask] | ((uint64_t)ring[(rw + 1) & kRingMask] << 32);
+          const uint32_t rem = (uint32_t)(v >> (rp & 31u)) & lowmask;
+          const uint32_t diff = ((t - sig) << fs) | rem;
+          const uint32_t delta = valid ? (diff >> 1) ^ (0u - (diff & 1u)) : 0u;
+          const uint32_t incl = half_incl_sum(delta);
+          if (valid) tile[comp + cs * (K + i)] = (uint16_t)px_write(acc + incl, be, ulsb);
+          acc += half_last(incl);
+        }
+        RPP_TSTAMP(13);
+        const uint32_t ex_last = half_last(ex);
+        const bool fin = rdo && K + ctot >= n;
+        const uint32_t E = posbuf[fin ? n - 1 - K : 0u] + fs + 1;
+        const uint32_t lastpos = posbuf[ctot ? ctot - 1 : 0u] + fs + 1;
+        __syncthreads();
+        if (fin) {
+          if (E > lim) status = RPP_TRUNCATED_INPUT;
+          P = E;
+          rdo = false;
+        }
+        if (rdo) {
+          sigma_carry = ctot ? lastpos : sigma_carry;
           K += ctot;
-          acc += readlane(dincl, kWave - 1);
-          const uint32_t sm = readlane(smax, kWave - 1);
-          sigma_carry = sm > sigma_carry ? sm : sigma_carry;
-          e0 = readlane(ex, kWave - 1);
-          W0 += kWave;
+          e0 = ex_last;
+          W0 += kHalf;
         }
       }
-      last[comp] = acc & 0xFFFFu;
+    }
+    RPP_TSTAMP(14);
+    if (active && status == RPP_OK) {
+      if (comp) last1 = acc & 0xFFFFu;
+      else last0 = acc & 0xFFFFu;
     }
     __syncthreads();
-    // ---- flush the chunk tile ----
-    uint16_t* dst = out + cbase;
-    if (((uintptr_t)dst & 15) == 0 && (clen & 7) == 0) {
-      for (uint32_t i = lane; i < clen / 8; i += kWave)
-        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(tile)[i];
-    } else {
-      for (uint32_t i = lane; i < clen; i += kWave) dst[i] = tile[i];
+    // ---- chunk complete: flush this half's tile ----
+    if (active && status == RPP_OK && comp == cs - 1) {
+      uint16_t* dst = out + cbase;
+      if (((uintptr_t)dst & 15) == 0 && (clen & 7) == 0) {
+        for (uint32_t i = hl; i < clen / 8; i += kHalf)
+          reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(tile)[i];
+      } else {
+        for (uint32_t i = hl; i < clen; i += kHalf) dst[i] = tile[i];
+      }
     }
     __syncthreads();
   }
-  set_status(p.status, b, RPP_OK);
+  RPP_TSTAMP(15);
+  if (b < p.nblocks && hl == 0) p.status[b] = status;
+#ifdef RPP_STATS
+  if (lane == 0)
+    for (int i = 0; i < 16; ++i) atomicAdd(&g_rpp_stats[i], (unsigned long long)stat_acc[i]);
+#endif
 }
 
 }  // namespace
@@ -562,6 +823,18 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
 extern "C" {
 
 uint32_t rpp_abi_version(void) { return 1; }
+
+#ifdef RPP_STATS
+// Diagnostic build only: copies (and optionally clears) the loop counters.
+int rpp_stats_fetch(uint64_t* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rpp_stats), sizeof(uint64_t) * 16) != hipSuccess) return RPP_HIP_ERROR;
+  if (reset) {
+    uint64_t z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rpp_stats), z, sizeof z) != hipSuccess) return RPP_HIP_ERROR;
+  }
+  return RPP_OK;
+}
+#endif
 
 int rpp_check_config(const rpp_config* c) {
   if (!c) return RPP_INVALID_ARGUMENT;
@@ -608,7 +881,7 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   DecParams p{d_in, d_in_offsets, d_in_bytes, d_out, d_out_offsets, d_n_samples, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count};
-  hipLaunchKernelGGL(rpp_decode_kernel, dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(rpp_decode_kernel, dim3((nblocks + 1) / 2), dim3(kWave), 0, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
