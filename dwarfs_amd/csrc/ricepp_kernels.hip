@@ -535,33 +535,38 @@ __device__ __forceinline__ uint32_t chain_exit(uint32_t word, uint32_t entry, ui
 template <int NCH>
 __device__ __forceinline__ uint32_t resolve_word(uint32_t own, uint32_t fs, uint32_t e0, bool first, bool act,
                                                  uint32_t nit, uint32_t* ex_out) {
+  // sig[e]: next search start of the chain entered at e; >= 32 = left the
+  // word, exit state sig - 32 (a search that runs off the word -> 32, exit 0)
   uint32_t sig[NCH], T[NCH];
   const uint64_t w64 = own;
+  const uint32_t fs1 = fs + 1;
 #pragma unroll
   for (int e = 0; e < NCH; ++e) {
-    const uint32_t se = first ? (e == 0 ? e0 : 63u) : ((uint32_t)e <= fs ? (uint32_t)e : 63u);
-    sig[e] = act ? se : 63u;
+    const uint32_t se = first ? (e == 0 ? e0 : 32u) : ((uint32_t)e <= fs ? (uint32_t)e : 32u);
+    sig[e] = act ? se : 32u;
     T[e] = 0;
   }
+  // stage by stage across the NCH independent chains (keeps them interleaved)
   for (uint32_t it = 0; it < nit; ++it) {
+    uint32_t y[NCH], tz[NCH];
+#pragma unroll
+    for (int e = 0; e < NCH; ++e) y[e] = (uint32_t)(w64 >> sig[e]);  // 0 once sig >= 32
+#pragma unroll
+    for (int e = 0; e < NCH; ++e) tz[e] = (uint32_t)__builtin_ctz(y[e] | 0x80000000u);
 #pragma unroll
     for (int e = 0; e < NCH; ++e) {
-      const bool a = sig[e] < 32;
-      const uint32_t y = (uint32_t)(w64 >> sig[e]);
-      const uint32_t t = sig[e] + (uint32_t)__builtin_ctz(y | 0x80000000u);
-      const bool hit = y != 0;
-      T[e] = hit ? (T[e] | (1u << t)) : T[e];
-      sig[e] = hit ? t + fs + 1 : (a ? 63u : sig[e]);
+      const bool hit = y[e] != 0;
+      T[e] |= (hit ? 1u : 0u) << (sig[e] + tz[e]);
+      sig[e] = hit ? sig[e] + tz[e] + fs1 : max(sig[e], 32u);
     }
   }
   uint64_t F = 0;
   bool cst = true;
-  const uint32_t x0 = sig[0] < 63 ? sig[0] - 32 : 0u;
 #pragma unroll
   for (int e = 0; e < NCH; ++e) {
-    const uint32_t x = sig[e] < 63 ? sig[e] - 32 : 0u;
+    const uint32_t x = sig[e] - 32;
     F |= (uint64_t)x << (4 * e);
-    cst = cst && (first || (uint32_t)e > fs || x == x0);
+    cst = cst && (first || (uint32_t)e > fs || x == sig[0] - 32);
   }
   // resolve entry states left to right
   uint32_t entry = 0;
