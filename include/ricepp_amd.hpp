@@ -1,0 +1,110 @@
+// ricepp_amd.hpp -- C++ host facade over the C ABI of ricepp_amd.h.
+//
+// Mirrors the two interfaces the reference exposes for this path:
+//
+//  * the ricepp library API used by DwarFS's plugin
+//      ricepp::create_encoder<uint16_t> / create_decoder<uint16_t>
+//        (ricepp/include/ricepp/create_encoder.h:39-41, create_decoder.h:39-41)
+//      encoder_interface<uint16_t>::encode / worst_case_encoded_bytes
+//        (ricepp/include/ricepp/encoder_interface.h:38-60)
+//      decoder_interface<uint16_t>::decode (decoder_interface.h:37-50)
+//    Errors: std::runtime_error("Unsupported configuration") for a bad
+//    config, std::out_of_range when decoding runs past the input.
+//
+//  * the DwarFS block codec behind block_compressor / block_decompressor
+//      ricepp_block_compressor / ricepp_block_decompressor
+//        (src/compression/ricepp.cpp:57-182, 184-255)
+//    with the same framing, metadata JSON, constraints and error messages.
+//
+// Host spans in, host spans out: the facade stages through device buffers on
+// its own HIP stream (one per object; objects are safe to use from one thread
+// at a time -- clone() per worker thread, as DwarFS does with
+// block_compressor::impl).  The device-resident batch API (rpp_encode_batch /
+// rpp_decode_batch) is the fast path; this facade is the drop-in.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <optional>
+#include <span>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ricepp_amd.h"
+
+namespace ricepp_amd {
+
+enum class byteorder { little, big };
+
+// ricepp::codec_config (ricepp/include/ricepp/codec_config.h:36-41)
+struct codec_config {
+  size_t block_size;
+  size_t component_stream_count;
+  byteorder order;
+  unsigned unused_lsb_count;
+};
+
+class encoder {
+ public:
+  virtual ~encoder() = default;
+  virtual std::vector<uint8_t> encode(std::span<uint16_t const> input) const = 0;
+  virtual size_t worst_case_encoded_bytes(size_t pixel_count) const = 0;
+  virtual size_t worst_case_encoded_bytes(std::span<uint16_t const> input) const = 0;
+  virtual std::span<uint8_t> encode(std::span<uint8_t> output, std::span<uint16_t const> input) const = 0;
+};
+
+class decoder {
+ public:
+  virtual ~decoder() = default;
+  virtual void decode(std::span<uint16_t> output, std::span<uint8_t const> input) const = 0;
+};
+
+// throw std::runtime_error("Unsupported configuration") like
+// ricepp/ricepp_cpuspecific.cpp:161,173
+std::unique_ptr<encoder> create_encoder(codec_config const& config);
+std::unique_ptr<decoder> create_decoder(codec_config const& config);
+
+// ---- DwarFS block codec (src/compression/ricepp.cpp) ----
+
+// compression_type::RICEPP (include/dwarfs/compression.h, RICEPP = 7)
+inline constexpr int compression_type_ricepp = 7;
+
+class block_compressor {
+ public:
+  explicit block_compressor(size_t block_size = 128);  // "ricepp:block_size=N", N in [16, 512]
+  static std::unique_ptr<block_compressor> create(std::string const& spec);
+
+  std::unique_ptr<block_compressor> clone() const;
+  std::vector<uint8_t> compress(std::span<uint8_t const> data, std::string const* metadata) const;
+  int type() const { return compression_type_ricepp; }
+  std::string describe() const;
+  std::string metadata_requirements() const;
+  size_t compression_granularity(std::string const& metadata) const;  // get_compression_constraints
+  size_t estimate_memory_usage(size_t data_size) const { return data_size; }
+
+ private:
+  size_t block_size_;
+};
+
+class block_decompressor {
+ public:
+  explicit block_decompressor(std::span<uint8_t const> data);
+
+  int type() const { return compression_type_ricepp; }
+  std::optional<std::string> metadata() const;
+  size_t uncompressed_size() const { return frame_.uncompressed_bytes; }
+  void start_decompression(std::vector<uint8_t>* target);
+  bool decompress_frame(size_t frame_size = 0);  // decodes everything on the first call
+  // convenience: block_decompressor::decompress (src/block_decompressor.cpp:41-49)
+  static std::vector<uint8_t> decompress(std::span<uint8_t const> data);
+
+ private:
+  rpp_frame frame_{};
+  std::span<uint8_t const> data_;
+  std::unique_ptr<decoder> decoder_;
+  std::vector<uint8_t>* target_ = nullptr;
+};
+
+}  // namespace ricepp_amd

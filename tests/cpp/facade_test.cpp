@@ -1,0 +1,171 @@
+// C++ facade test (runs on a GPU box).  Mirrors the reference tests of the
+// path: ricepp/test/codec_test.cpp (round trips, worst-case KATs, error
+// contract) and test/ricepp_compressor_test.cpp (block_compressor spec
+// round trip), checking every stream against the CPU oracle byte for byte.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ricepp_amd.hpp"
+
+extern "C" {  // CPU oracle (oracle/ricepp_oracle.c), the checker
+struct rpo_config {
+  uint32_t block_size, component_stream_count, big_endian, unused_lsb_count;
+};
+size_t rpo_worst_case_bytes(const rpo_config*, size_t);
+int rpo_encode(const rpo_config*, const uint16_t*, size_t, uint8_t*, size_t, size_t*);
+size_t rpo_frame_header(uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, uint32_t);
+}
+
+static int failures = 0;
+#define CHECK(cond)                                                         \
+  do {                                                                      \
+    if (!(cond)) {                                                          \
+      std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                           \
+    }                                                                       \
+  } while (0)
+
+template <class E, class F>
+static bool throws(F&& f, char const* msg = nullptr) {
+  try {
+    f();
+  } catch (E const& e) {
+    return !msg || std::string(e.what()) == msg;
+  } catch (...) {
+    return false;
+  }
+  return false;
+}
+
+static uint16_t bswap(uint16_t v) { return (uint16_t)((v >> 8) | (v << 8)); }
+
+// codec_test.cpp:43-61 shape: noise U[20000,21000], full-range outliers
+static std::vector<uint16_t> make_data(size_t n, unsigned ulsb, bool be, unsigned full_chance, uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  std::uniform_int_distribution<unsigned> dist(0, full_chance);
+  std::uniform_int_distribution<unsigned> noise(20000, 21000), full(0, 65535);
+  std::vector<uint16_t> v(n);
+  uint16_t mask = (uint16_t)(0xFFFFu << ulsb);
+  for (auto& x : v) {
+    uint16_t s = (uint16_t)((dist(rng) == 0 ? full(rng) : noise(rng)) & mask);
+    x = be ? bswap(s) : s;
+  }
+  return v;
+}
+
+static std::vector<uint8_t> oracle_encode(ricepp_amd::codec_config const& c, std::vector<uint16_t> const& x) {
+  rpo_config oc{(uint32_t)c.block_size, (uint32_t)c.component_stream_count,
+                c.order == ricepp_amd::byteorder::big ? 1u : 0u, c.unused_lsb_count};
+  std::vector<uint8_t> out(rpo_worst_case_bytes(&oc, x.size()) + 1);
+  size_t n = 0;
+  if (rpo_encode(&oc, x.data(), x.size(), out.data(), out.size(), &n) != 0) std::abort();
+  out.resize(n);
+  return out;
+}
+
+static void roundtrip(ricepp_amd::codec_config const& c, size_t n, unsigned full_chance, uint64_t seed) {
+  auto x = make_data(n, c.unused_lsb_count, c.order == ricepp_amd::byteorder::big, full_chance, seed);
+  auto enc = ricepp_amd::create_encoder(c);
+  auto bytes = enc->encode(x);
+  CHECK(bytes == oracle_encode(c, x));
+  auto dec = ricepp_amd::create_decoder(c);
+  std::vector<uint16_t> y(x.size());
+  dec->decode(y, bytes);
+  CHECK(y == x);
+}
+
+int main() {
+  using ricepp_amd::byteorder;
+  // codec_test.cpp:65-152
+  roundtrip({16, 1, byteorder::big, 0}, 12345, 50, 1);
+  roundtrip({13, 1, byteorder::big, 4}, 4321, 50, 2);
+  roundtrip({32, 1, byteorder::big, 0}, 1500, 0, 3);
+  roundtrip({29, 2, byteorder::big, 2}, 23456, 50, 4);
+  roundtrip({128, 1, byteorder::little, 0}, 65536, 50, 5);
+  roundtrip({512, 2, byteorder::little, 3}, 10000, 50, 6);
+
+  // codec_test.cpp:154-196: worst-case KATs; incompressible == worst case
+  {
+    ricepp_amd::codec_config c{29, 1, byteorder::big, 0};
+    auto enc = ricepp_amd::create_encoder(c);
+    auto x = make_data(14443, 0, true, 0, 7);
+    CHECK(enc->worst_case_encoded_bytes(x) == 29138);
+    std::vector<uint8_t> buf(29138);
+    auto used = enc->encode(buf, x);
+    CHECK(used.size() == 29138);
+    auto enc2 = ricepp_amd::create_encoder({29, 2, byteorder::big, 0});
+    CHECK(enc2->worst_case_encoded_bytes(28886) == 58275);
+  }
+  // codec_test.cpp:198-222
+  CHECK(throws<std::runtime_error>([] { ricepp_amd::create_encoder({513, 2, byteorder::big, 0}); },
+                                   "Unsupported configuration"));
+  CHECK(throws<std::runtime_error>([] { ricepp_amd::create_decoder({128, 3, byteorder::big, 0}); },
+                                   "Unsupported configuration"));
+  // bitstream_reader.h:150-152: running out of input is std::out_of_range
+  {
+    ricepp_amd::codec_config c{128, 1, byteorder::big, 0};
+    auto x = make_data(4096, 0, true, 50, 8);
+    auto bytes = ricepp_amd::create_encoder(c)->encode(x);
+    bytes.resize((bytes.size() - 1) / 8 * 8);
+    std::vector<uint16_t> y(x.size());
+    auto dec = ricepp_amd::create_decoder(c);
+    CHECK(throws<std::out_of_range>([&] { dec->decode(y, bytes); }));
+  }
+
+  // test/ricepp_compressor_test.cpp:124-161 through the block codec
+  struct P {
+    int cs, pixels, ulsb, block;
+  };
+  for (P p : {P{1, 1000, 0, 16}, P{2, 1000, 2, 32}, P{1, 1000, 4, 64}, P{2, 3333, 6, 99}}) {
+    auto x = make_data((size_t)p.cs * p.pixels, (unsigned)p.ulsb, true, 50, 9);
+    std::vector<uint8_t> data(x.size() * 2);
+    std::memcpy(data.data(), x.data(), data.size());
+    std::string meta = "{\"endianness\":\"big\",\"bytes_per_sample\":2,\"unused_lsb_count\":" +
+                       std::to_string(p.ulsb) + ",\"component_count\":" + std::to_string(p.cs) + "}";
+    auto comp = ricepp_amd::block_compressor::create("ricepp:block_size=" + std::to_string(p.block));
+    CHECK(comp->describe() == "ricepp [block_size=" + std::to_string(p.block) + "]");
+    CHECK(comp->compression_granularity(meta) == (size_t)(2 * p.cs));
+    auto compressed = comp->compress(data, &meta);
+    // framing + bitstream identical to the reference layout
+    std::vector<uint8_t> want(64);
+    size_t h = rpo_frame_header(want.data(), data.size(), (uint32_t)p.block, (uint32_t)p.cs, 2, (uint32_t)p.ulsb, 1, 1);
+    want.resize(h);
+    auto body = oracle_encode({(size_t)p.block, (size_t)p.cs, byteorder::big, (unsigned)p.ulsb}, x);
+    want.insert(want.end(), body.begin(), body.end());
+    CHECK(compressed == want);
+    CHECK(compressed.size() < 7 * data.size() / 10);
+    auto back = ricepp_amd::block_decompressor::decompress(compressed);
+    CHECK(back == data);
+    ricepp_amd::block_decompressor d{compressed};
+    CHECK(d.uncompressed_size() == data.size());
+    CHECK(*d.metadata() == "{\"bytes_per_sample\":2,\"component_count\":" + std::to_string(p.cs) +
+                               ",\"endianness\":\"big\",\"unused_lsb_count\":" + std::to_string(p.ulsb) + "}");
+  }
+  // plugin error contract (src/compression/ricepp.cpp:70-73, 86-91, 196-200, 243-247)
+  {
+    ricepp_amd::block_compressor comp{128};
+    std::vector<uint8_t> odd(7);
+    std::string meta = R"({"endianness":"big","bytes_per_sample":2,"unused_lsb_count":0,"component_count":1})";
+    CHECK(throws<std::runtime_error>([&] { comp.compress(odd, nullptr); },
+                                     "internal error: ricepp compression requires metadata"));
+    CHECK(throws<std::runtime_error>([&] { comp.compress(odd, &meta); },
+                                     "unexpected data configuration: 7 bytes to compress, 1 components, 2 bytes per sample"));
+    std::vector<uint8_t> v2(64);
+    v2.resize(rpo_frame_header(v2.data(), 16, 128, 1, 2, 0, 1, 2));
+    CHECK(throws<std::runtime_error>([&] { ricepp_amd::block_decompressor d{v2}; }, "[RICEPP] unsupported version: 2"));
+    std::vector<uint8_t> b3(64);
+    b3.resize(rpo_frame_header(b3.data(), 16, 128, 1, 3, 0, 1, 1));
+    CHECK(throws<std::runtime_error>([&] { ricepp_amd::block_decompressor d{b3}; },
+                                     "[RICEPP] unsupported bytes per sample: 3"));
+    CHECK(throws<std::runtime_error>([] { ricepp_amd::block_compressor::create("ricepp:block_size=8"); }));
+    CHECK(comp.metadata_requirements() ==
+          R"({"bytes_per_sample":["set",[2]],"component_count":["range",1,2],"endianness":["set",["big","little"]],"unused_lsb_count":["range",0,8]})");
+  }
+  std::printf("facade_test: %s (%d failures)\n", failures ? "FAILED" : "OK", failures);
+  return failures ? 1 : 0;
+}
