@@ -1,0 +1,26 @@
+"""Copies the rocprofv3 summaries of a GPU session into profiles/ (tracked)
+and derives profiles/pmc_latest.json (HBM bytes per launch) for bench.py.
+
+HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950
+FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads and
+WRITE_SIZE is exact for 16 B/lane stores (MI355X_MICROARCH.md, HBM)."""
+import json
+import shutil
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+src = ROOT / "gpurun_out" / "prof"
+dst = ROOT / "profiles"
+dst.mkdir(exist_ok=True)
+shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / f"{tag}_bench_kernel_stats.csv")
+shutil.copy(src / "pmc_summary.txt", dst / f"{tag}_pmc_summary.txt")
+pmc = json.loads((src / "pmc_summary.json").read_text())
+latest = {"source": f"profiles/{tag}_pmc_summary.txt", "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+for k, v in pmc.items():
+    if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        latest[k] = {"hbm_bytes_per_launch": int((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024),
+                     "fetch_kb": v["FETCH_SIZE"], "write_kb": v["WRITE_SIZE"]}
+(dst / "pmc_latest.json").write_text(json.dumps(latest, indent=1) + "\n")
+print(json.dumps(latest, indent=1))
