@@ -188,75 +188,222 @@ __device__ __forceinline__ EncGeom enc_geom(uint32_t s, uint32_t j, uint32_t nsb
   return g;
 }
 
-// Raw loads of one iteration, kept packed so the next iteration's loads can
-// be in flight while the current one is processed.
-struct EncLoad {
-  uint4 a, b;
-  uint32_t prev;
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef short ss2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// The lane's 8 stored samples as 4 packed pairs (sample 2k in the low half
+// of w[k]) plus the previous same-component sample (the delta reference).
+struct EncRaw {
+  uint4 a, c;     // cs == 1: a holds the 8 samples; cs == 2: a, c hold 16 interleaved
+  uint32_t prev;  // samples, this lane's component is picked at use (not at load)
 };
 
-__device__ __forceinline__ EncLoad enc_load(const uint16_t* in, const EncGeom& g, uint32_t cs, bool vec_ok) {
-  EncLoad L;
-  // previous same-component sample (delta reference); the stream's first
-  // sample of a component is its own reference (codec.h:72-73: last = read(in[i]))
+__device__ __forceinline__ void enc_words(const EncRaw& r, uint32_t cs, uint32_t comp, uint32_t w[4]) {
+  if (cs == 1) {
+    w[0] = r.a.x; w[1] = r.a.y; w[2] = r.a.z; w[3] = r.a.w;
+  } else {
+    const uint32_t sel = comp ? 0x07060302u : 0x05040100u;
+    w[0] = __builtin_amdgcn_perm(r.a.y, r.a.x, sel);
+    w[1] = __builtin_amdgcn_perm(r.a.w, r.a.z, sel);
+    w[2] = __builtin_amdgcn_perm(r.c.y, r.c.x, sel);
+    w[3] = __builtin_amdgcn_perm(r.c.w, r.c.z, sel);
+  }
+}
+
+// Full iterations (every lane owns 0 or 8 samples): branch-free 16-byte
+// loads, so a double-buffered prefetch stays in flight.
+__device__ __forceinline__ EncRaw enc_load_vec(const uint16_t* in, const EncGeom& g, uint32_t cs) {
+  EncRaw r;
+  // codec.h:72-73: a component's first sample is its own reference (last = read(in[i]))
   const uint32_t pi = g.cnt ? (g.m_first >= cs ? g.m_first - cs : g.m_first) : 0u;
-  L.prev = in[pi];
-  if (vec_ok) {
-    const uint4* q = reinterpret_cast<const uint4*>(g.cnt == 8 ? in + (g.m_first - g.comp) : in);
-    L.a = q[0];
-    L.b = cs == 2 ? q[1] : L.a;
-    if (g.cnt != 8 && g.cnt != 0) {  // stream tail
-      uint32_t w[8];
-      for (uint32_t i = 0; i < 8; ++i) w[i] = i < g.cnt ? (uint32_t)in[g.m_first + cs * i] : 0u;
-      L.a = make_uint4(w[0] | (w[1] << 16), w[2] | (w[3] << 16), w[4] | (w[5] << 16), w[6] | (w[7] << 16));
-      L.b = L.a;
-    }
-  } else {
-    uint32_t w[8];
-    for (uint32_t i = 0; i < 8; ++i) w[i] = i < g.cnt ? (uint32_t)in[g.m_first + cs * i] : 0u;
-    L.a = make_uint4(w[0] | (w[1] << 16), w[2] | (w[3] << 16), w[4] | (w[5] << 16), w[6] | (w[7] << 16));
-    L.b = L.a;
-  }
-  return L;
+  r.prev = in[pi];
+  const uint4* q = reinterpret_cast<const uint4*>(g.cnt ? in + (g.m_first - g.comp) : in);
+  r.a = q[0];
+  r.c = cs == 2 ? q[1] : r.a;
+  return r;
 }
 
-// Unpacks the lane's 8 raw samples.  `split` layout: cs == 2 vector loads
-// hold both components interleaved, the lane's samples in half `comp`.
-__device__ __forceinline__ void enc_unpack(const EncLoad& L, uint32_t cs, uint32_t comp, bool vec_full,
-                                           uint32_t raw[8]) {
-  if (cs == 2 && vec_full) {
-    const uint32_t sh = 16 * comp;
-    raw[0] = (L.a.x >> sh) & 0xFFFFu; raw[1] = (L.a.y >> sh) & 0xFFFFu;
-    raw[2] = (L.a.z >> sh) & 0xFFFFu; raw[3] = (L.a.w >> sh) & 0xFFFFu;
-    raw[4] = (L.b.x >> sh) & 0xFFFFu; raw[5] = (L.b.y >> sh) & 0xFFFFu;
-    raw[6] = (L.b.z >> sh) & 0xFFFFu; raw[7] = (L.b.w >> sh) & 0xFFFFu;
-  } else {
-    raw[0] = L.a.x & 0xFFFFu; raw[1] = L.a.x >> 16;
-    raw[2] = L.a.y & 0xFFFFu; raw[3] = L.a.y >> 16;
-    raw[4] = L.a.z & 0xFFFFu; raw[5] = L.a.z >> 16;
-    raw[6] = L.a.w & 0xFFFFu; raw[7] = L.a.w >> 16;
-  }
-}
-
-__device__ __forceinline__ uint32_t shr_sum8(const uint32_t d[8], uint32_t f) {
-  uint32_t s = 0;
+// Ragged tail / unaligned streams: per-sample loads.
+__device__ __forceinline__ EncRaw enc_load_scalar(const uint16_t* in, const EncGeom& g, uint32_t cs) {
+  EncRaw r;
+  const uint32_t pi = g.m_first >= cs ? g.m_first - cs : g.m_first;
+  r.prev = g.cnt ? (uint32_t)in[pi] : 0u;
+  uint32_t v[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s += d[i] >> f;
-  return s;
+  for (uint32_t i = 0; i < 8; ++i) v[i] = i < g.cnt ? (uint32_t)in[g.m_first + cs * i] : 0u;
+  // stored as the cs == 1 layout (this lane's samples only)
+  r.a = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
+  r.c = r.a;
+  return r;
 }
 
-// ORs the (<= 16 bit) code `v` into the window at bit `rel`.
+// ORs the (<= 16 bit) code `v` into the window at bit `rel` (two ds_or_b32;
+// the second is 0 when the code does not straddle a word).
 __device__ __forceinline__ void emit_bits(uint32_t* win, uint32_t rel, uint32_t v) {
   const uint32_t w = rel >> 5, sh = rel & 31u;
   atomicOr(&win[w], v << sh);
-  if (sh) {
-    const uint32_t hi = v >> (32u - sh);
-    if (hi) atomicOr(&win[w + 1], hi);
+  atomicOr(&win[w + 1], (v >> 1) >> (31u - sh));
+}
+
+constexpr uint32_t kEncWin = 1024;      // LDS output window (words, 4 KiB)
+constexpr uint32_t kEncFlushWords = 256;  // stream out once >= 1 KiB of whole 64-byte lines is ready
+
+struct EncState {
+  uint32_t* win;
+  uint32_t* out32;
+  uint32_t win_w0;  // global word index held in win[0] (multiple of 16)
+  uint32_t base;    // absolute bit position of the next sub-block
+};
+
+// One group of 64/G sub-blocks: zig-zag deltas, compute_best_split replay,
+// bit positions by one wave scan, codes OR-ed into the LDS window.
+__device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, const EncGeom& geo, uint32_t G,
+                                              uint32_t j, uint32_t be, uint32_t ulsb, bool mask_tail,
+                                              uint32_t cs_layout) {
+  const uint32_t n = geo.n, cnt = geo.cnt;
+  uint32_t rw[4];
+  enc_words(r, cs_layout, geo.comp, rw);
+  const bool sb_valid = n != 0;
+  // ---- pixel values (ricepp_cpuspecific_traits.h:63-67) and zig-zag deltas
+  //      (encode.h:116-123), two samples per instruction ----
+  us2 v[4], d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = be ? __builtin_amdgcn_perm(rw[k], rw[k], 0x02030001u) : rw[k];
+    v[k] = as_us2(x) >> (us2)(unsigned short)ulsb;
+  }
+  const uint32_t pv = px_read(r.prev, be, ulsb);
+  uint32_t prevw = pv << 16;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const us2 pp = as_us2(__builtin_amdgcn_alignbit(as_u32(v[k]), prevw, 16));
+    prevw = as_u32(v[k]);
+    const us2 diff = v[k] - pp;
+    d[k] = (diff << (us2)1) ^ as_us2(__builtin_bit_cast(uint32_t, (__builtin_bit_cast(ss2, diff) >> (ss2)15)));
+  }
+  if (mask_tail) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t keep = (2u * k < cnt ? 0xFFFFu : 0u) | (2u * k + 1 < cnt ? 0xFFFF0000u : 0u);
+      d[k] = as_us2(as_u32(d[k]) & keep);
+    }
+  }
+  const us2 one = {1, 1};
+  uint32_t lsum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) lsum = __builtin_amdgcn_udot2(d[k], one, lsum, false);
+  auto shr_sum = [&](uint32_t f) -> uint32_t {
+    const us2 fv = (us2)(unsigned short)f;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc = __builtin_amdgcn_udot2(d[k] >> fv, one, acc, false);
+    return acc;
+  };
+  const uint32_t sum = group_sum(lsum, G);
+
+  // ---- compute_best_split replay (encode.h:43-90) ----
+  // start = max(0, bit_width(sum / n) - 2) without a division:
+  // bit_width(floor(s/n)) = t + (s >= n << t), t = floor(log2 s) - floor(log2 n)
+  uint32_t bwq = 0;
+  if (n != 0 && sum >= n) {
+    const uint32_t t = (uint32_t)__clz(n) - (uint32_t)__clz(sum);
+    bwq = t + ((n << t) <= sum ? 1u : 0u);
+  }
+  const uint32_t start = bwq >= 2 ? bwq - 2 : 0u;
+  const uint32_t bits0 = n * (start + 1) + group_sum(shr_sum(start), G);
+  const uint32_t bits1 = n * (start + 2) + group_sum(shr_sum(start + 1), G);
+  int cand, dir;
+  uint32_t bits;
+  if (bits1 <= bits0) {
+    cand = (int)start + 1; bits = bits1; dir = 1;
+  } else {
+    cand = (int)start; bits = bits0; dir = -1;
+  }
+  bool walking = sb_valid && sum != 0 && bits0 != bits1;
+  for (;;) {
+    const bool act = walking && cand > 0 && cand < 14;
+    if (!__any(act)) break;
+    const uint32_t f = act ? (uint32_t)(cand + dir) : 0u;
+    const uint32_t t = n * (f + 1) + group_sum(shr_sum(f), G);
+    if (act && t <= bits) {
+      bits = t;
+      cand += dir;
+    } else {
+      walking = false;
+    }
+  }
+  // encode.h:127-156: 0 = all-zero, 1 = Rice, 2 = raw
+  uint32_t mode = 0, fs = 0;
+  if (sb_valid && sum != 0) {
+    fs = (uint32_t)cand;
+    mode = (fs < 14 && bits < 16 * n) ? 1u : 2u;
+  }
+
+  // ---- bit positions: one wave-wide scan ----
+  uint32_t lbits = (sb_valid && j == 0) ? 4u : 0u;
+  if (mode == 1) lbits += shr_sum(fs) + cnt * (fs + 1);
+  else if (mode == 2) lbits += 16 * cnt;
+  const uint32_t incl = wave_incl_sum(lbits);
+  const uint32_t total = readlane(incl, kWave - 1);
+  uint32_t pos = st.base + incl - lbits - 32 * st.win_w0;  // window-relative
+
+  // ---- emit codes into the LDS window ----
+  if (sb_valid && j == 0) {
+    emit_bits(st.win, pos, mode == 0 ? 0u : (mode == 1 ? fs + 1 : 15u));
+    pos += 4;
+  }
+  if (mode == 1) {
+    const uint32_t lowmask = (1u << fs) - 1u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if ((uint32_t)i < cnt) {
+        const uint32_t di = (i & 1) ? (as_u32(d[i >> 1]) >> 16) : (as_u32(d[i >> 1]) & 0xFFFFu);
+        pos += di >> fs;  // unary zeros are implicit (the window is zeroed)
+        emit_bits(st.win, pos, 1u | ((di & lowmask) << 1));
+        pos += fs + 1;
+      }
+    }
+  } else if (mode == 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if ((uint32_t)i < cnt) {
+        const uint32_t ri = (i & 1) ? (rw[i >> 1] >> 16) : (rw[i >> 1] & 0xFFFFu);
+        emit_bits(st.win, pos, ri);  // raw stored value (encode.h:148-151)
+        pos += 16;
+      }
+    }
+  }
+  st.base += total;
+}
+
+// Streams whole 64-byte lines out once >= kEncFlushWords are complete.
+__device__ __forceinline__ void enc_flush(EncState& st, bool final_flush) {
+  const uint32_t lane = lane_id();
+  __syncthreads();
+  const uint32_t full_end = st.base >> 5;  // words before it are complete
+  const uint32_t F = full_end & ~15u;
+  if (F >= st.win_w0 + kEncFlushWords || (final_flush && F > st.win_w0)) {
+    const uint32_t nch = (F - st.win_w0) >> 2;
+    for (uint32_t c = lane; c < nch; c += kWave) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&st.win[4 * c]);
+      *reinterpret_cast<uint4*>(&st.out32[st.win_w0 + 4 * c]) = v;
+    }
+    const uint32_t used = full_end - st.win_w0 + 1;
+    const uint32_t tail0 = F - st.win_w0;
+    const uint32_t keep = lane < 16 ? st.win[tail0 + lane] : 0u;
+    __syncthreads();
+    for (uint32_t i = lane; i < used; i += kWave) st.win[i] = 0;
+    __syncthreads();
+    if (lane < 16) st.win[lane] = keep;
+    __syncthreads();
+    st.win_w0 = F;
   }
 }
 
 __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
-  __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
+  __shared__ __attribute__((aligned(16))) uint32_t win[kEncWin];
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t bs = p.bs, cs = p.cs, be = p.be, ulsb = p.ulsb;
@@ -272,16 +419,13 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint32_t N = (uint32_t)n64;
   const uint16_t* in = p.in + p.in_off[b];
   uint8_t* out8 = p.out + ooff;
-  uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
-  const bool vec_ok = (bs & 7u) == 0 && ((uintptr_t)in & 15u) == 0 && N >= 8 * cs;
 
-  for (uint32_t i = lane; i < (uint32_t)kWinWords; i += kWave) win[i] = 0;
+  for (uint32_t i = lane; i < kEncWin; i += kWave) win[i] = 0;
   __syncthreads();
 
+  EncState st{win, reinterpret_cast<uint32_t*>(out8), 0u, 16 * cs};
   // codec.h:69-74,81-86: 16-bit initial value read(in[i]) per component.
   if (lane < cs) emit_bits(win, 16 * lane, N ? px_read(in[lane], be, ulsb) : 0u);
-  uint32_t win_w0 = 0;      // global word index held in win[0]
-  uint32_t base = 16 * cs;  // absolute bit position of the next sub-block
 
   const uint32_t chunk_len = cs * bs;
   const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
@@ -291,129 +435,52 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   while (G < m8) G <<= 1;
   const uint32_t spw = kWave / G;
   const uint32_t g = lane / G, j = lane & (G - 1);
+  // full iterations: every sub-block complete, lanes own 0 or 8 samples
+  const bool vec_ok = (bs & 7u) == 0 && ((uintptr_t)in & 15u) == 0;
+  const uint32_t nsb_full = vec_ok ? (N / chunk_len) * cs : 0u;
+  const uint32_t nfull = nsb_full / spw;
+  const bool empty_lanes = G * 8 != bs;
 
-  EncGeom ngeo = enc_geom(g, j, nsb, N, bs, cs);
-  EncLoad nld = enc_load(in, ngeo, cs, vec_ok);
-  for (uint32_t s0 = 0; s0 < nsb; s0 += spw) {
-    const EncGeom geo = ngeo;
-    const EncLoad ld = nld;
-    if (s0 + spw < nsb) {  // prefetch the next group of sub-blocks
-      ngeo = enc_geom(s0 + spw + g, j, nsb, N, bs, cs);
-      nld = enc_load(in, ngeo, cs, vec_ok);
-    }
-    const bool sb_valid = geo.n != 0;
-    const uint32_t n = geo.n, cnt = geo.cnt;
-
-    // ---- zig-zag deltas (encode.h:116-123) ----
-    uint32_t raw[8], d[8];
-    enc_unpack(ld, cs, geo.comp, vec_ok && cnt == 8, raw);
-    uint32_t prev = px_read(ld.prev, be, ulsb);
-    uint32_t lsum = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t px = px_read(raw[i], be, ulsb);
-      d[i] = (uint32_t)i < cnt ? zigzag16(px, prev) : 0u;
-      prev = px;
-      lsum += d[i];
-    }
-    const uint32_t sum = group_sum(lsum, G);
-
-    // ---- compute_best_split replay (encode.h:43-90) ----
-    const uint32_t avg = n ? sum / n : 0u;
-    const uint32_t bw = avg ? 32u - (uint32_t)__clz(avg) : 0u;
-    const uint32_t start = bw >= 2 ? bw - 2 : 0u;
-    const uint32_t bits0 = n * (start + 1) + group_sum(shr_sum8(d, start), G);
-    const uint32_t bits1 = n * (start + 2) + group_sum(shr_sum8(d, start + 1), G);
-    int cand, dir;
-    uint32_t bits;
-    if (bits1 <= bits0) {
-      cand = (int)start + 1; bits = bits1; dir = 1;
-    } else {
-      cand = (int)start; bits = bits0; dir = -1;
-    }
-    bool walking = sb_valid && sum != 0 && bits0 != bits1;
-    for (;;) {
-      const bool act = walking && cand > 0 && cand < 14;
-      if (!__any(act)) break;
-      const uint32_t f = act ? (uint32_t)(cand + dir) : 0u;
-      const uint32_t t = n * (f + 1) + group_sum(shr_sum8(d, f), G);
-      if (act && t <= bits) {
-        bits = t;
-        cand += dir;
-      } else {
-        walking = false;
+  // ---- full iterations, double buffered (no register copies between the
+  //      load and its use, so the next group's loads stay in flight) ----
+  uint32_t it = 0;
+  if (nfull) {
+    EncGeom ga = enc_geom(g, j, nsb, N, bs, cs), gb;
+    EncRaw ra = enc_load_vec(in, ga, cs), rb;
+    for (; it + 1 < nfull; it += 2) {
+      gb = enc_geom((it + 1) * spw + g, j, nsb, N, bs, cs);
+      rb = enc_load_vec(in, gb, cs);
+      enc_iteration(st, ra, ga, G, j, be, ulsb, empty_lanes, cs);
+      enc_flush(st, false);
+      if (it + 2 < nfull) {
+        ga = enc_geom((it + 2) * spw + g, j, nsb, N, bs, cs);
+        ra = enc_load_vec(in, ga, cs);
       }
+      enc_iteration(st, rb, gb, G, j, be, ulsb, empty_lanes, cs);
+      enc_flush(st, false);
     }
-    // encode.h:127-156: 0 = all-zero, 1 = Rice, 2 = raw
-    uint32_t mode = 0, fs = 0;
-    if (sb_valid && sum != 0) {
-      fs = (uint32_t)cand;
-      mode = (fs < 14 && bits < 16 * n) ? 1u : 2u;
-    }
-
-    // ---- bit positions: one wave-wide scan ----
-    uint32_t lbits = (sb_valid && j == 0) ? 4u : 0u;
-    if (mode == 1) lbits += shr_sum8(d, fs) + cnt * (fs + 1);
-    else if (mode == 2) lbits += 16 * cnt;
-    const uint32_t incl = wave_incl_sum(lbits);
-    const uint32_t total = readlane(incl, kWave - 1);
-    uint32_t pos = base + incl - lbits - 32 * win_w0;  // window-relative
-
-    // ---- emit codes into the LDS window ----
-    if (sb_valid && j == 0) {
-      emit_bits(win, pos, mode == 0 ? 0u : (mode == 1 ? fs + 1 : 15u));
-      pos += 4;
-    }
-    if (mode == 1) {
-      const uint32_t lowmask = (1u << fs) - 1u;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if ((uint32_t)i < cnt) {
-          pos += d[i] >> fs;  // unary zeros are implicit (window is zeroed)
-          emit_bits(win, pos, 1u | ((d[i] & lowmask) << 1));
-          pos += fs + 1;
-        }
-      }
-    } else if (mode == 2) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if ((uint32_t)i < cnt) {
-          emit_bits(win, pos, raw[i]);  // raw stored value (encode.h:148-151)
-          pos += 16;
-        }
-      }
-    }
-    base += total;
-    __syncthreads();
-
-    // ---- stream completed 16-byte chunks to HBM ----
-    const uint32_t full_end = base >> 5;
-    const uint32_t F = full_end & ~3u;
-    if (F > win_w0) {
-      const uint32_t nch = (F - win_w0) >> 2;
-      for (uint32_t c = lane; c < nch; c += kWave) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&win[4 * c]);
-        *reinterpret_cast<uint4*>(&out32[win_w0 + 4 * c]) = v;
-      }
-      const uint32_t used = full_end - win_w0 + 1;
-      const uint32_t tail0 = F - win_w0;
-      const uint32_t keep = lane < 4 ? win[tail0 + lane] : 0u;
-      __syncthreads();
-      for (uint32_t i = lane; i < used; i += kWave) win[i] = 0;
-      __syncthreads();
-      if (lane < 4) win[lane] = keep;
-      __syncthreads();
-      win_w0 = F;
+    if (it < nfull) {
+      enc_iteration(st, ra, ga, G, j, be, ulsb, empty_lanes, cs);
+      enc_flush(st, false);
+      ++it;
     }
   }
+  // ---- ragged tail / unaligned streams: per-sample loads ----
+  for (uint32_t s0 = it * spw; s0 < nsb; s0 += spw) {
+    const EncGeom geo = enc_geom(s0 + g, j, nsb, N, bs, cs);
+    const EncRaw r = enc_load_scalar(in, geo, cs);
+    enc_iteration(st, r, geo, G, j, be, ulsb, true, 1u);
+    enc_flush(st, false);
+  }
+  enc_flush(st, true);
 
-  // ---- final flush: full words, then the ceil(bits/8) tail bytes
+  // ---- final words and the ceil(bits/8) tail bytes
   //      (bitstream_writer.h:110-120,139-145) ----
-  const uint32_t total_bytes = (base + 7) >> 3;
-  const uint32_t full_end = base >> 5;
-  for (uint32_t w = win_w0 + lane; w < full_end; w += kWave) out32[w] = win[w - win_w0];
+  const uint32_t total_bytes = (st.base + 7) >> 3;
+  const uint32_t full_end = st.base >> 5;
+  for (uint32_t w = st.win_w0 + lane; w < full_end; w += kWave) st.out32[w] = win[w - st.win_w0];
   const uint32_t tail_bytes = total_bytes - 4 * full_end;
-  if (lane < tail_bytes) out8[4 * full_end + lane] = (uint8_t)(win[full_end - win_w0] >> (8 * lane));
+  if (lane < tail_bytes) out8[4 * full_end + lane] = (uint8_t)(win[full_end - st.win_w0] >> (8 * lane));
   if (lane == 0) {
     p.out_bytes[b] = total_bytes;
     p.status[b] = RPP_OK;
@@ -674,7 +741,9 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
     const uint32_t cbase = chunk * chunk_len;
     const uint32_t clen = active ? min(N - cbase, chunk_len) : 0u;
     const uint32_t n = clen / cs;
+    RPP_TSTAMP(4);
     ensure(P >> 5, active);
+    RPP_TSTAMP(5);
     // decode.h:60: 4-bit fs+1 header
     if (active && P + 4 > lim) {
       status = RPP_TRUNCATED_INPUT;
@@ -683,6 +752,7 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
     const uint32_t fsp1 = active ? rbits(P, 4) : 0u;
     P += 4;
     RPP_STAT(6, 1);
+    RPP_TSTAMP(7);
     uint32_t acc = comp ? last1 : last0;
     if (active && fsp1 == 0) {
       // decode.h:79-80: all samples = write(last)
