@@ -29,6 +29,13 @@
 
 #include "ricepp_amd.h"
 
+// Diagnostic builds only: -DRPP_ABLATE=<mask> removes decode phases to time
+// them (outputs are then wrong): 1 flush, 2 extraction, 4 verify rounds,
+// 8 look-back guess.
+#ifndef RPP_ABLATE
+#define RPP_ABLATE 0
+#endif
+
 #ifdef RPP_STATS
 // Diagnostic build only (-DRPP_STATS): loop trip counters, summed over waves.
 __device__ unsigned long long g_rpp_stats[16];
@@ -221,7 +228,7 @@ __device__ __forceinline__ EncRaw enc_load_vec(const uint16_t* in, const EncGeom
   r.prev = in[pi];
   const uint4* q = reinterpret_cast<const uint4*>(g.cnt ? in + (g.m_first - g.comp) : in);
   r.a = q[0];
-  r.c = cs == 2 ? q[1] : r.a;
+  r.c = q[cs - 1];  // cs == 1: a harmless reload of q[0] (a select here went through scratch)
   return r;
 }
 
@@ -491,11 +498,25 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
 // DECODE
 // ===========================================================================
 // Two streams per wavefront: lanes 0-31 decode stream 2*blockIdx.x, lanes
-// 32-63 stream 2*blockIdx.x+1.  A Rice sub-block of ~1000 bits (Poisson
-// sensor data, bs 128) then covers one half-wave of 32 lanes x 32-bit words,
-// so every instruction of the serial sub-block loop serves two streams.  All
-// per-stream state is uniform within a half; cross-lane ops (DPP row shifts,
-// row_bcast15) never cross the half boundary.
+// 32-63 stream 2*blockIdx.x+1.  Every per-stream value is uniform within a
+// half; cross-lane ops (DPP row shifts, row_bcast15) never cross the halves.
+//
+// A Rice sub-block (ricepp/include/ricepp/detail/decode.h:62-71) is parsed in
+// windows of 32 lane segments of SEG bits (SEG = 40 for fs <= 7, 64 above, so
+// one window covers a typical 128-sample sub-block).  The only serial
+// dependency of the parse is where the first code of a segment starts (its
+// entry state 0..fs: remainder bits of the previous code still to skip).
+// Each lane guesses it by running the terminator chain over the 32 bits
+// before its segment from entry 0 (Rice codes self-synchronise: the guess is
+// right ~3 times in 4), then runs the exact chain of its segment from the
+// guess, recording the start of every code.  Guesses are verified against the
+// left neighbour's exit state; mismatching lanes re-run from the corrected
+// entry until the half is consistent (lane 0's entry is exact, so this
+// terminates; typically one round).  Code counts -> prefix sum -> the lane
+// holding the sub-block's last code -> the next header position.  Each lane
+// then turns its recorded code starts into zig-zag deltas (q from the gap,
+// the fs remainder bits from its registers) into an LDS tile; a chunk's tile
+// is prefix-summed, pixel-encoded and stored with vector stores.
 struct DecParams {
   const uint8_t* in;
   const uint64_t* in_off;
@@ -513,7 +534,6 @@ constexpr uint32_t kRingWords = 1024;         // per-stream LDS ring of the comp
 constexpr uint32_t kRingMask = kRingWords - 1;
 constexpr uint32_t kChunkWords = 4 * kHalf;   // refill unit: 16 B per lane of a half
 constexpr uint32_t kAhead = 288;              // words kept resident ahead of the read position
-constexpr uint32_t kPosCap = 512;             // terminator positions of one Rice pass
 
 __device__ __forceinline__ uint32_t half_incl_sum(uint32_t v) {
   v += dpp<kDppRowShr1>(v);
@@ -524,14 +544,74 @@ __device__ __forceinline__ uint32_t half_incl_sum(uint32_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t half_incl_max(uint32_t v) {
+  v = max(v, dpp<kDppRowShr1>(v));
+  v = max(v, dpp<kDppRowShr2>(v));
+  v = max(v, dpp<kDppRowShr4>(v));
+  v = max(v, dpp<kDppRowShr8>(v));
+  v = max(v, dpp<kDppRowBcast15, 0xA>(v));
+  return v;
+}
+
 __device__ __forceinline__ uint32_t half_last(uint32_t v) {
   const uint32_t a = readlane(v, kHalf - 1), b = readlane(v, kWave - 1);
+  return lane_id() >= kHalf ? b : a;
+}
+
+__device__ __forceinline__ uint32_t half_first(uint32_t v) {
+  const uint32_t a = readlane(v, 0), b = readlane(v, kHalf);
   return lane_id() >= kHalf ? b : a;
 }
 
 __device__ __forceinline__ uint32_t half_ballot(bool pred) {
   const uint64_t m = __ballot(pred);
   return lane_id() >= kHalf ? (uint32_t)(m >> 32) : (uint32_t)m;
+}
+
+// Packed 2 x u16 arithmetic (wraps per half-word).
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return as_u32(as_us2(a) + as_us2(b)); }
+
+__device__ __forceinline__ uint32_t half_incl_sum_pk(uint32_t v) {
+  v = pk_add(v, dpp<kDppRowShr1>(v));
+  v = pk_add(v, dpp<kDppRowShr2>(v));
+  v = pk_add(v, dpp<kDppRowShr4>(v));
+  v = pk_add(v, dpp<kDppRowShr8>(v));
+  v = pk_add(v, dpp<kDppRowBcast15, 0xA>(v));
+  return v;
+}
+
+// pixel write (ricepp_cpuspecific_traits.h:69-73) of two packed samples
+__device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t be, uint32_t ulsb) {
+  v = as_u32(as_us2(v) << (us2)(unsigned short)ulsb);
+  return be ? __builtin_amdgcn_perm(v, v, 0x02030001u) : v;
+}
+
+// Orders this wave's LDS accesses without waiting on its global stores
+// (a one-wave workgroup needs no s_barrier; __syncthreads() would also
+// drain vmcnt, i.e. wait for the previous chunk's output stores).
+__device__ __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
+
+// Asynchronous global -> LDS copies (global_load_lds): lane l's 16 (4) bytes
+// land at LDS byte address m0 + 16 l (4 l).  Issued by asm, so the compiler
+// neither waits for them nor counts them: the caller retires them with
+// vm_drain() before the words are read.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t m0) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(m0) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t m0) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(m0) : "memory");
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
 
 // 32-bit word `w` of the stream, zero past the end (bitstream_reader.h:165-166
@@ -553,125 +633,76 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, uint32_t nbytes, 
                     stream_word(in, nbytes, w + 3));
 }
 
-// Terminator chain through one 32-bit word: starting the unary search at bit
-// `entry`, mark every '1' that ends a unary run and skip its fs remainder
-// bits.  Returns the terminator mask; *exit = where the search continues in
-// the next word (0 if it runs off the word while searching).  Branch-free
-// body, wave-uniform trip count: sigma in [32, 45] = left the word after a
-// terminator, 63 = ran off while searching ((0:word) >> 63 == 0 keeps it).
-// Pass entry >= 32 for a lane that has nothing to do.
-__device__ __forceinline__ uint32_t chain_word(uint32_t word, uint32_t entry, uint32_t fs, uint32_t* exit,
-                                               uint32_t* iters = nullptr) {
-  uint32_t T = 0, sigma = entry;
-  const uint64_t w64 = word;
-  while (__any(sigma < 32)) {
-    if (iters) ++*iters;
-    const bool act = sigma < 32;
-    const uint32_t y = (uint32_t)(w64 >> sigma);  // 0 once sigma >= 32
-    const uint32_t t = sigma + (uint32_t)__builtin_ctz(y | 0x80000000u);
-    const bool hit = y != 0;
-    T = hit ? (T | (1u << t)) : T;
-    sigma = hit ? t + fs + 1 : (act ? 63u : sigma);
+// Terminator chain through a lane segment [0, SEG) held in the low SEG bits
+// of X.  The unary search of the first code starts at bit `entry`; every '1'
+// found ends a code, whose fs remainder bits are skipped.  cnt = codes whose
+// terminator lies in the segment; lastc = search start after the last of
+// them; exit = where the search enters the next segment (0 when it runs off
+// the end while searching).  `slow` flags a unary run of >= 32 bits (the
+// search looks 32 bits ahead) or an unfinished chain.
+struct SegChain {
+  uint32_t cnt, exit, lastc;
+  bool slow;
+};
+
+// Segments are 48 bits, so a chain position (< 48 + 14) always shifts a
+// 64-bit register validly; bits at and above SEG are zero, which freezes a
+// finished chain (no terminator -> c = max(c, SEG)).  Fixed, wave-uniform
+// trip counts: a per-step `__any` exit costs ~100 cycles of VALU->SALU
+// latency (measured), more than the step itself.  The search window is 32
+// bits: callers check the segment for a run of 32 zeros (zero_run32).
+constexpr uint32_t kSeg = 48;
+
+template <int SEG>
+__device__ __forceinline__ SegChain seg_chain(uint64_t X, uint32_t entry, uint32_t fsp1, uint32_t nsteps) {
+  uint32_t c = entry, cnt = 0, lastc = 0;
+  for (uint32_t j = 0; j < nsteps; ++j) {
+    const uint32_t t = ffbl((uint32_t)(X >> c));
+    const bool fnd = t != ~0u;
+    const uint32_t cn = c + t + fsp1;
+    cnt += fnd ? 1u : 0u;
+    lastc = fnd ? cn : lastc;
+    c = fnd ? cn : max(c, (uint32_t)SEG);
   }
-  *exit = sigma < 63 ? sigma - 32 : 0u;
-  return T;
+  return SegChain{cnt, c - SEG, lastc, c < (uint32_t)SEG};
 }
 
-// Exit state only (the lookback chain).
-__device__ __forceinline__ uint32_t chain_exit(uint32_t word, uint32_t entry, uint32_t fs) {
-  uint32_t sigma = entry;
-  const uint64_t w64 = word;
-  while (__any(sigma < 32)) {
-    const bool act = sigma < 32;
-    const uint32_t y = (uint32_t)(w64 >> sigma);
-    const uint32_t t = sigma + (uint32_t)__builtin_ctz(y | 0x80000000u);
-    sigma = y != 0 ? t + fs + 1 : (act ? 63u : sigma);
+// exit state only (the look-back guess)
+template <int SEG>
+__device__ __forceinline__ uint32_t seg_exit(uint64_t X, uint32_t entry, uint32_t fsp1, uint32_t nsteps) {
+  uint32_t c = entry;
+  for (uint32_t j = 0; j < nsteps; ++j) {
+    const uint32_t t = ffbl((uint32_t)(X >> c));
+    c = t != ~0u ? c + t + fsp1 : max(c, (uint32_t)SEG);
   }
-  return sigma < 63 ? sigma - 32 : 0u;
+  return c - SEG;
 }
 
-// Exact terminator mask of this lane's 32-bit word.  A lane does not know
-// where the unary search enters its word (that depends on every code to its
-// left), so it runs the terminator chain for every possible entry state
-// 0..fs side by side (independent chains: instruction-level parallelism,
-// no speculation), giving its transfer function entry -> exit.  The first
-// lane of a half has one exact entry (e0).  Entries then resolve left to
-// right: a lane whose exit is the same for every entry (chains merged inside
-// the word, the common case) breaks the dependency, so the resolution takes
-// as many rounds as the longest run of entry-dependent lanes.
-template <int NCH>
-__device__ __forceinline__ uint32_t resolve_word(uint32_t own, uint32_t fs, uint32_t e0, bool first, bool act,
-                                                 uint32_t nit, uint32_t* ex_out) {
-  // sig[e]: next search start of the chain entered at e; >= 32 = left the
-  // word, exit state sig - 32 (a search that runs off the word -> 32, exit 0)
-  uint32_t sig[NCH], T[NCH];
-  const uint64_t w64 = own;
-  const uint32_t fs1 = fs + 1;
-#pragma unroll
-  for (int e = 0; e < NCH; ++e) {
-    const uint32_t se = first ? (e == 0 ? e0 : 32u) : ((uint32_t)e <= fs ? (uint32_t)e : 32u);
-    sig[e] = act ? se : 32u;
-    T[e] = 0;
-  }
-  // stage by stage across the NCH independent chains (keeps them interleaved)
-  for (uint32_t it = 0; it < nit; ++it) {
-    uint32_t y[NCH], tz[NCH];
-#pragma unroll
-    for (int e = 0; e < NCH; ++e) y[e] = (uint32_t)(w64 >> sig[e]);  // 0 once sig >= 32
-#pragma unroll
-    for (int e = 0; e < NCH; ++e) tz[e] = (uint32_t)__builtin_ctz(y[e] | 0x80000000u);
-#pragma unroll
-    for (int e = 0; e < NCH; ++e) {
-      const bool hit = y[e] != 0;
-      T[e] |= (hit ? 1u : 0u) << (sig[e] + tz[e]);
-      sig[e] = hit ? sig[e] + tz[e] + fs1 : max(sig[e], 32u);
-    }
-  }
-  uint64_t F = 0;
-  bool cst = true;
-#pragma unroll
-  for (int e = 0; e < NCH; ++e) {
-    const uint32_t x = sig[e] - 32;
-    F |= (uint64_t)x << (4 * e);
-    cst = cst && (first || (uint32_t)e > fs || x == sig[0] - 32);
-  }
-  // resolve entry states left to right
-  uint32_t entry = 0;
-  bool known = first || !act;
-  for (;;) {
-    const bool out_known = known || cst;
-    const uint32_t out_val = (uint32_t)(F >> (4 * entry)) & 15u;
-    const bool lk = from_left(out_known ? 1u : 0u) != 0;
-    const uint32_t lv = from_left(out_val);
-    entry = (!known && lk) ? lv : entry;
-    known = known || lk;
-    if (!__any(!known)) break;
-  }
-  uint32_t Tt = T[0];
-#pragma unroll
-  for (int e = 1; e < NCH; ++e) Tt = entry == (uint32_t)e ? T[e] : Tt;
-  *ex_out = (uint32_t)(F >> (4 * entry)) & 15u;
-  return Tt;
+// Does the SEG-bit segment X hold 32 consecutive zeros?
+template <int SEG>
+__device__ __forceinline__ bool zero_run32(uint64_t X) {
+  uint64_t z = ~X & ((UINT64_C(1) << SEG) - 1);
+  z &= z >> 1;
+  z &= z >> 2;
+  z &= z >> 4;
+  z &= z >> 8;
+  z &= z >> 16;
+  return z != 0;
 }
 
 __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t ring_s[2][kRingWords];
   __shared__ __attribute__((aligned(16))) uint16_t tile_s[2][kTileSamples];
-  __shared__ uint32_t pos_s[2][kPosCap + 1];  // + one dummy slot
   const uint32_t lane = lane_id();
   const uint32_t h = lane >> 5, hl = lane & (kHalf - 1);
   uint32_t* ring = ring_s[h];
   uint16_t* tile = tile_s[h];
-  uint32_t* posbuf = pos_s[h];
   const uint32_t bs = p.bs, cs = p.cs, be = p.be, ulsb = p.ulsb;
   const uint32_t b = 2 * blockIdx.x + h;
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
-  uint32_t* itp2 = &stat_acc[3];
   unsigned long long tprev_;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
-#else
-  uint32_t* itp2 = nullptr;
 #endif
 
   // ---- per-stream setup (uniform within the half) ----
@@ -699,11 +730,24 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
   const uint32_t chunk_len = cs * bs;
   const uint32_t nsb = b < p.nblocks && status == RPP_OK ? ((N + chunk_len - 1) / chunk_len) * cs : 0u;
 
-  // ---- fill the ring; refills are synchronous but only every ~8 sub-blocks
-  //      (a register-carried prefetch made the compiler wait on every
-  //      iteration for the output stores queued behind it) ----
+  // ---- LDS ring of the stream's words: words [fill_w - kRingWords, fill_w)
+  //      are resident.  Steady state: at the end of an iteration, a chunk of
+  //      256 words lying wholly inside the input is requested by
+  //      global_load_lds (no registers, nothing for the compiler to wait on);
+  //      it is retired (vmcnt(0), by then long complete together with that
+  //      iteration's output stores) at the top of the next iteration's flush,
+  //      and only then counted resident.  ensure() is the synchronous path
+  //      (start-up, the zero-padded tail, long sub-blocks). ----
   uint32_t fill_w = 0;
-  auto refill = [&](bool go) {  // appends 2 chunks (256 words) to this half's ring
+  bool pend = false;  // a requested chunk is in flight for this half
+  auto retire = [&]() {
+    if (__any(pend)) {
+      vm_drain();
+      fill_w = pend ? fill_w + 2 * kChunkWords : fill_w;
+      pend = false;
+    }
+  };
+  auto refill_sync = [&](bool go) {  // appends 256 words (zero past the input) synchronously
     if (go) {
       const uint4 v0 = load_chunk(in, nbytes, fill_w, aligned16);
       const uint4 v1 = load_chunk(in, nbytes, fill_w + kChunkWords, aligned16);
@@ -712,28 +756,55 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
     }
     fill_w = go ? fill_w + 2 * kChunkWords : fill_w;
   };
-  refill(true);
-  refill(true);
-  __syncthreads();
-  // keeps words [w - 1, w + kAhead) of this half's stream resident
-  auto ensure = [&](uint32_t w, bool act) {
-    while (__any(act && fill_w < w + kAhead)) refill(act && fill_w < w + kAhead);
-    __syncthreads();
+  auto request = [&](bool want) {  // asynchronous 256-word chunk for halves that want one
+    want = want && 4u * (fill_w + 2 * kChunkWords) <= nbytes;
+#pragma unroll
+    for (uint32_t hh = 0; hh < 2; ++hh) {
+      if (__any(want && h == hh)) {
+        const uint32_t fw = __builtin_amdgcn_readfirstlane(readlane(fill_w, hh * kHalf));
+        const bool a16 = readlane(aligned16 ? 1u : 0u, hh * kHalf) != 0;
+        // m0 such that lane hh*32 + l lands at ring slot + 16 l (4 l)
+        const uint32_t slot = (uint32_t)(uintptr_t)&ring_s[hh][fw & kRingMask];
+        if (want && h == hh) {
+          const uint8_t* src = in + 4u * fw;
+          if (a16) {
+            glds16(src + 16u * hl, slot - hh * 512u);
+            glds16(src + 512u + 16u * hl, slot + 512u - hh * 512u);
+          } else {
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) glds4(src + 128u * q + 4u * hl, slot + 128u * q - hh * 128u);
+          }
+        }
+      }
+    }
+    pend = want;
   };
-  auto rbits = [&](uint32_t pos, uint32_t width) -> uint32_t {  // width <= 16
-    const uint32_t w = pos >> 5;
-    const uint64_t v = (uint64_t)ring[w & kRingMask] | ((uint64_t)ring[(w + 1) & kRingMask] << 32);
-    return (uint32_t)(v >> (pos & 31u)) & ((1u << width) - 1u);
+  refill_sync(true);
+  refill_sync(true);
+  lds_fence();
+  // keeps words [w - 3, w + kAhead) of this half's stream resident
+  auto ensure = [&](uint32_t w, bool act) {
+    if (__any(act && fill_w < w + kAhead)) {
+      retire();
+      while (__any(act && fill_w < w + kAhead)) refill_sync(act && fill_w < w + kAhead);
+      lds_fence();
+    }
+  };
+  auto word = [&](uint32_t w) -> uint32_t { return ring[w & kRingMask]; };
+  auto peek32 = [&](uint32_t pos) -> uint32_t {
+    return __builtin_amdgcn_alignbit(word((pos >> 5) + 1), word(pos >> 5), pos & 31u);
   };
 
   uint32_t last0 = 0, last1 = 0, P = 16 * cs;
-  if (nsb != 0 || (b < p.nblocks && status == RPP_OK)) {
+  if (b < p.nblocks && status == RPP_OK) {
     if (16 * cs > lim) status = RPP_TRUNCATED_INPUT;
-    last0 = rbits(0, 16);
-    last1 = cs > 1 ? rbits(16, 16) : 0u;
+    last0 = peek32(0) & 0xFFFFu;
+    last1 = cs > 1 ? peek32(16) & 0xFFFFu : 0u;
   }
+  uint32_t rawmask = 0;  // components of the current chunk stored raw
 
   for (uint32_t s = 0;; ++s) {
+    RPP_TSTAMP(4);
     bool active = s < nsb && status == RPP_OK;
     if (!__any(active)) break;
     const uint32_t chunk = cs == 1 ? s : s >> 1;
@@ -741,7 +812,6 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
     const uint32_t cbase = chunk * chunk_len;
     const uint32_t clen = active ? min(N - cbase, chunk_len) : 0u;
     const uint32_t n = clen / cs;
-    RPP_TSTAMP(4);
     ensure(P >> 5, active);
     RPP_TSTAMP(5);
     // decode.h:60: 4-bit fs+1 header
@@ -749,140 +819,253 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
       status = RPP_TRUNCATED_INPUT;
       active = false;
     }
-    const uint32_t fsp1 = active ? rbits(P, 4) : 0u;
-    P += 4;
+    const uint32_t P4 = P + 4;
+    // this lane's Rice window segment [sb, sb + 48) (window = 32 lanes from
+    // P + 4), the 96 bits before it and 16 bits past it; lane 0's look-back
+    // ends with the header
+    uint32_t lk0, lk1, lk2, lo, hiu;
+    auto load_seg = [&](uint32_t sb) {
+      const uint32_t wb = sb >> 5, o = sb & 31u;
+      const uint32_t a0 = word(wb - 3), a1 = word(wb - 2), a2 = word(wb - 1), a3 = word(wb), a4 = word(wb + 1),
+                     a5 = word(wb + 2);
+      lk0 = __builtin_amdgcn_alignbit(a1, a0, o);
+      lk1 = __builtin_amdgcn_alignbit(a2, a1, o);
+      lk2 = __builtin_amdgcn_alignbit(a3, a2, o);
+      lo = __builtin_amdgcn_alignbit(a4, a3, o);
+      hiu = __builtin_amdgcn_alignbit(a5, a4, o);
+    };
+    load_seg(P4 + kSeg * hl);
+    const uint32_t fsp1 = active ? half_first(lk2) >> 28 : 0u;
+    uint32_t E = P4;
     RPP_STAT(6, 1);
     RPP_TSTAMP(7);
-    uint32_t acc = comp ? last1 : last0;
     if (active && fsp1 == 0) {
-      // decode.h:79-80: all samples = write(last)
-      const uint32_t v = px_write(acc, be, ulsb);
-      for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = (uint16_t)v;
+      // decode.h:79-80: every sample = write(last): zero deltas
+      for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = 0;
     }
     if (active && fsp1 == 15) {
       // decode.h:72-77: raw stored values; last = read(last sample)
-      if ((uint64_t)P + 16ull * n > lim) {
+      if ((uint64_t)P4 + 16ull * n > lim) {
         status = RPP_TRUNCATED_INPUT;
         active = false;
       } else {
-        for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = (uint16_t)rbits(P + 16 * k, 16);
-        acc = px_read(rbits(P + 16 * (n - 1), 16), be, ulsb);
-        P += 16 * n;
+        for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = (uint16_t)peek32(P4 + 16 * k);
+        const uint32_t lv = px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb);
+        if (comp) last1 = lv;
+        else last0 = lv;
+        rawmask |= 1u << comp;
+        E = P4 + 16 * n;
       }
     }
-    bool rdo = active && fsp1 != 0 && fsp1 != 15;
+    const bool rice = active && fsp1 != 0 && fsp1 != 15;
+    const uint32_t fs = rice ? fsp1 - 1 : 0u;
+    bool slowh = rice && fs == 0;  // fs 0: serial path below
     RPP_TSTAMP(9);
-    if (__any(rdo)) {
-      // decode.h:62-71: Rice codes, fs = fsp1 - 1
-      const uint32_t fs = rdo ? fsp1 - 1 : 0u;
-      const uint32_t lowmask = (1u << fs) - 1u;
-      // wave-uniform chain shape: entries = max fs + 1, steps = ceil(32 / (min fs + 1))
-      const uint32_t fa = readlane(rdo ? fs : 0u, 0), fb = readlane(rdo ? fs : 0u, kHalf);
-      const bool ra = readlane(rdo ? 1u : 0u, 0) != 0, rb = readlane(rdo ? 1u : 0u, kHalf) != 0;
-      const uint32_t fmax = max(ra ? fa : 0u, rb ? fb : 0u);
-      const uint32_t fmin = min(ra ? fa : 15u, rb ? fb : 15u);
-      const uint32_t nch = fmax + 1;
-      const uint32_t nit = (32 + fmin) / (fmin + 1);
-      uint32_t K = 0;            // codes decoded in earlier passes
-      uint32_t sigma_carry = P;  // search start of the next code
-      uint32_t W0 = P >> 5;      // first word of this pass
-      uint32_t e0 = P & 31u;     // exact entry state of lane 0 of the half
-      while (__any(rdo)) {
-        RPP_STAT(0, 1);
-        if (rdo && 32ull * W0 >= lim) {
-          status = RPP_TRUNCATED_INPUT;
-          rdo = false;
-        }
-        ensure(W0, rdo);
-        RPP_TSTAMP(9);
-        const uint32_t own = ring[(W0 + hl) & kRingMask];
-        // chains for every entry state, then left-to-right resolution
-        uint32_t ex, T;
-        switch (nch) {
-#define RPP_RESOLVE_CASE(k) \
-  case k: T = resolve_word<k>(own, fs, e0, hl == 0, rdo, nit, &ex); break;
-          RPP_RESOLVE_CASE(1) RPP_RESOLVE_CASE(2) RPP_RESOLVE_CASE(3) RPP_RESOLVE_CASE(4)
-          RPP_RESOLVE_CASE(5) RPP_RESOLVE_CASE(6) RPP_RESOLVE_CASE(7) RPP_RESOLVE_CASE(8)
-          RPP_RESOLVE_CASE(9) RPP_RESOLVE_CASE(10) RPP_RESOLVE_CASE(11) RPP_RESOLVE_CASE(12)
-          RPP_RESOLVE_CASE(13)
-          default: T = resolve_word<14>(own, fs, e0, hl == 0, rdo, nit, &ex); break;
-#undef RPP_RESOLVE_CASE
-        }
-        RPP_TSTAMP(10);
-        RPP_TSTAMP(11);
-        const uint32_t c = (uint32_t)__builtin_popcount(T);
-        const uint32_t cincl = half_incl_sum(c);
-        const uint32_t cexcl = cincl - c;
-        const uint32_t ctot = half_last(cincl);
-        const uint32_t need = rdo ? min(ctot, n - K) : 0u;
-        const uint32_t wbit = 32u * (W0 + hl);
-        // materialise the absolute positions of the first `need` terminators
-        {
-          uint32_t TT = T, idx = cexcl;
-          for (uint32_t it = 0; it < nit; ++it) {  // popcount(T) <= nit
-            const bool hit = TT != 0 && idx < need;
-            const uint32_t t = (uint32_t)__builtin_ctz(TT | 0x80000000u);
-            posbuf[hit ? idx : kPosCap] = wbit + t;
-            TT &= TT - 1;
-            ++idx;
+    if (__any(rice && fs != 0)) {
+      // decode.h:62-71: Rice codes, fs = fsp1 - 1 >= 1
+      const uint32_t fa = readlane(rice ? fs : 0u, 0), fb = readlane(rice ? fs : 0u, kHalf);
+      const bool ra = readlane(rice ? 1u : 0u, 0) != 0, rb = readlane(rice ? 1u : 0u, kHalf) != 0;
+      const uint32_t fmin1 = min(ra && fa ? fa : 15u, rb && fb ? fb : 15u) + 1;  // smallest fs + 1 >= 2
+      const uint32_t fs1 = fs + 1;  // >= 1 in every lane (halves not parsing Rice still run the chains)
+      auto rice_fast = [&]<int SEG>() {
+        const uint32_t nsteps = (SEG + fmin1 - 1) / fmin1 + 1;  // codes per segment + 1
+        // q0: first bit of the window; e_in: entry state of its lane 0;
+        // s_in: where the code open at the window start began (its unary run
+        // may span earlier segments)
+        uint32_t q0 = P4, e_in = 0, done = 0, s_in = P4;
+        bool go = rice && fs != 0;
+        while (__any(go)) {
+          RPP_STAT(0, 1);
+          if (__any(q0 != P4)) {  // continuation window: the sub-block is longer than 32 segments
+            if (go && q0 != P4 && q0 >= lim) {  // no input left for the next code
+              status = RPP_TRUNCATED_INPUT;
+              go = false;
+            }
+            ensure(q0 >> 5, go);
+            load_seg(q0 + SEG * hl);
+          }
+          const uint32_t sb = q0 + SEG * hl;
+          const uint64_t X = ((uint64_t)(hiu & ((1u << (SEG - 32)) - 1u)) << 32) | lo;  // the segment
+          const uint64_t XR = ((uint64_t)hiu << 32) | lo;                              // + what follows
+          RPP_TSTAMP(10);
+          // entry guess: chain over the 96 bits before the segment from entry 0
+          const uint32_t e1 = seg_exit<48>(((uint64_t)(lk1 & 0xFFFFu) << 32) | lk0, 0, fs1, (48 + fmin1 - 1) / fmin1 + 1);
+          const uint32_t e2 = seg_exit<48>(((uint64_t)lk2 << 16) | (lk1 >> 16), e1, fs1, (48 + fmin1 - 1) / fmin1 + 1);
+          uint32_t g = hl == 0 ? e_in : ((RPP_ABLATE & 8) ? 0u : e2);
+          SegChain ch = seg_chain<SEG>(X, g, fs1, nsteps);
+          const bool zr = zero_run32<SEG>(X);
+          RPP_TSTAMP(11);
+          const uint32_t need = n - done;
+          uint32_t incl, L;
+          bool fin;
+          // verify entries against the left neighbour's exit; re-run until
+          // consistent (lane 0 is exact: at most kHalf rounds)
+          for (uint32_t round = 0;; ++round) {
+            incl = half_incl_sum(go ? ch.cnt : 0u);
+            const uint32_t fm = half_ballot(go && incl >= need);
+            fin = fm != 0;
+            L = fin ? (uint32_t)__builtin_ctz(fm) : kHalf - 1;
+            const uint32_t lx_ = from_left(ch.exit);  // all lanes active (DPP source)
+            const uint32_t want = hl == 0 ? e_in : lx_;
+            const bool bad = go && hl <= L && want != g;
+            if (!__any(bad) || round > kHalf || (RPP_ABLATE & 4)) break;
+            RPP_STAT(1, 1);
+            g = want;
+            ch = seg_chain<SEG>(X, g, fs1, nsteps);
+          }
+          RPP_TSTAMP(12);
+          const uint32_t excl = incl - (go ? ch.cnt : 0u);
+          // start of the code open at this segment's entry: the last code
+          // start (terminator + fs + 1) of any segment to the left
+          const uint32_t smax = half_incl_max(go && ch.cnt ? sb + ch.lastc : 0u);
+          const uint32_t sleft = from_left(smax);
+          const uint32_t sopen = max(s_in, hl == 0 ? 0u : sleft);
+          // a relevant lane whose chain could not be followed -> serial path
+          const bool sl = half_ballot(go && hl <= L && (ch.slow || zr)) != 0;
+          if (sl) {
+            slowh = slowh || go;
+            go = false;
+          }
+          // zig-zag deltas of this lane's codes (decode.h:66-69): walk the
+          // chain again from the verified entry
+          const uint32_t mine = go ? min(ch.cnt, need > excl ? need - excl : 0u) : 0u;
+          const uint32_t lowmask = (1u << fs) - 1u;
+          uint32_t erel = 0, c = g, sop = sopen;
+          for (uint32_t j = 1; j < ((RPP_ABLATE & 2) ? 0u : nsteps); ++j) {
+            const bool act = j <= mine;
+            const uint32_t t = ffbl((uint32_t)(XR >> c));
+            const uint32_t q = sb + c + t - sop;
+            const uint32_t k = c + t + 1;  // remainder = bits [k, k + fs), k + fs < 64
+            const uint32_t diff = (q << fs) | ((uint32_t)(XR >> k) & lowmask);
+            const uint32_t delta = (diff >> 1) ^ (0u - (diff & 1u));
+            if (act) tile[comp + cs * (done + excl + j - 1)] = (uint16_t)delta;
+            c = act ? k + fs : c;
+            sop = sb + c;
+            erel = act ? c : erel;
+          }
+          RPP_TSTAMP(13);
+          const uint32_t tot = half_last(incl);
+          const uint32_t ea_ = readlane(erel, (int)readlane(L, 0)), eb_ = readlane(erel, (int)(readlane(L, kHalf) + kHalf));
+          const uint32_t lx = half_last(ch.exit);
+          if (go && fin) {
+            E = q0 + SEG * L + (h ? eb_ : ea_);
+            if (E > lim) status = RPP_TRUNCATED_INPUT;
+            go = false;
+          }
+          const uint32_t sl_ = half_last(smax);
+          if (go) {
+            done += tot;
+            e_in = lx;
+            s_in = max(s_in, sl_);
+            q0 += kHalf * SEG;
           }
         }
-        __syncthreads();
-        RPP_TSTAMP(12);
-        // code-parallel extraction: code i of this pass on lane i % 32
-        for (uint32_t r = 0; __any(r < need); r += kHalf) {
-          const uint32_t i = r + hl;
-          const bool valid = i < need;
-          const uint32_t ii = valid ? i : 0u;
-          const uint32_t t = posbuf[ii];
-          const uint32_t sig = ii == 0 ? sigma_carry : posbuf[ii - 1] + fs + 1;
-          const uint32_t rp = t + 1, rw = rp >> 5;
-          const uint64_t v = (uint64_t)ring[rw & kRingMask] | ((uint64_t)ring[(rw + 1) & kRingMask] << 32);
-          const uint32_t rem = (uint32_t)(v >> (rp & 31u)) & lowmask;
-          const uint32_t diff = ((t - sig) << fs) | rem;
-          const uint32_t delta = valid ? (diff >> 1) ^ (0u - (diff & 1u)) : 0u;
-          const uint32_t incl = half_incl_sum(delta);
-          if (valid) tile[comp + cs * (K + i)] = (uint16_t)px_write(acc + incl, be, ulsb);
-          acc += half_last(incl);
-        }
-        RPP_TSTAMP(13);
-        const uint32_t ex_last = half_last(ex);
-        const bool fin = rdo && K + ctot >= n;
-        const uint32_t E = posbuf[fin ? n - 1 - K : 0u] + fs + 1;
-        const uint32_t lastpos = posbuf[ctot ? ctot - 1 : 0u] + fs + 1;
-        __syncthreads();
-        if (fin) {
-          if (E > lim) status = RPP_TRUNCATED_INPUT;
-          P = E;
-          rdo = false;
-        }
-        if (rdo) {
-          sigma_carry = ctot ? lastpos : sigma_carry;
-          K += ctot;
-          e0 = ex_last;
-          W0 += kHalf;
-        }
-      }
+      };
+      rice_fast.template operator()<kSeg>();
     }
     RPP_TSTAMP(14);
-    if (active && status == RPP_OK) {
-      if (comp) last1 = acc & 0xFFFFu;
-      else last0 = acc & 0xFFFFu;
-    }
-    __syncthreads();
-    // ---- chunk complete: flush this half's tile ----
-    if (active && status == RPP_OK && comp == cs - 1) {
-      uint16_t* dst = out + cbase;
-      if (((uintptr_t)dst & 15) == 0 && (clen & 7) == 0) {
-        for (uint32_t i = hl; i < clen / 8; i += kHalf)
-          reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(tile)[i];
-      } else {
-        for (uint32_t i = hl; i < clen; i += kHalf) dst[i] = tile[i];
+    if (__any(slowh)) {
+      // serial path (lane 0 of the half): fs 0, unary runs >= 32 bits,
+      // corrupt streams.  Resumable across ring refills.
+      RPP_STAT(2, 1);
+      uint32_t pos = P4, k = 0, qacc = 0;
+      bool sgo = slowh;
+      while (__any(sgo)) {
+        const uint32_t pb = half_first(pos);
+        ensure(pb >> 5, sgo);
+        if (sgo && hl == 0) {
+          const uint32_t resident = ((pb >> 5) + kAhead - 2) * 32u;
+          while (k < n) {
+            if (pos + 64 > resident) break;
+            const uint32_t w = peek32(pos);
+            if (w == 0) {
+              if (pos + 32 >= lim) {  // the terminator would lie past the input
+                status = RPP_TRUNCATED_INPUT;
+                break;
+              }
+              qacc += 32;
+              pos += 32;
+              continue;
+            }
+            const uint32_t t = ffbl(w);
+            qacc += t;
+            pos += t + 1;
+            const uint32_t rem = fs ? peek32(pos) & ((1u << fs) - 1u) : 0u;
+            pos += fs;
+            const uint32_t diff = (qacc << fs) | rem;
+            qacc = 0;
+            tile[comp + cs * k] = (uint16_t)((diff >> 1) ^ (0u - (diff & 1u)));
+            ++k;
+          }
+        }
+        status = (int32_t)half_first((uint32_t)status);
+        sgo = sgo && status == RPP_OK && half_first(k) < n;
+      }
+      if (slowh && status == RPP_OK) {
+        E = half_first(pos);
+        if (E > lim) status = RPP_TRUNCATED_INPUT;
       }
     }
-    __syncthreads();
+    if (active && status == RPP_OK) P = E;
+    retire();
+    lds_fence();
+    // ---- chunk complete: prefix sums (decode.h:68), pixel encode, store.
+    //      Each lane takes 4 consecutive tile entries (cs 1: 4 samples; cs 2:
+    //      2 interleaved (c0, c1) pairs, summed as packed u16). ----
+    if (!(RPP_ABLATE & 1) && __any(active && status == RPP_OK && comp == cs - 1)) {
+      const bool fl = active && status == RPP_OK && comp == cs - 1;
+      const uint32_t rawm = cs == 1 ? ((rawmask & 1u) ? 0xFFFFFFFFu : 0u)
+                                    : ((rawmask & 1u) ? 0x0000FFFFu : 0u) | ((rawmask & 2u) ? 0xFFFF0000u : 0u);
+      uint32_t acc = cs == 1 ? last0 : (last0 | (last1 << 16));
+      uint16_t* dst = out + cbase;
+      const bool vec = ((uintptr_t)dst & 7) == 0;
+      for (uint32_t r0 = 0; __any(fl && r0 < clen); r0 += 4 * kHalf) {
+        const uint32_t e = r0 + 4 * hl;  // first tile entry of this lane
+        const uint2 dv = fl && e < clen ? *reinterpret_cast<const uint2*>(&tile[e]) : make_uint2(0, 0);
+        const uint32_t nv = fl && e < clen ? min(clen - e, 4u) : 0u;
+        const uint32_t A = nv > 1 ? dv.x : (nv ? dv.x & 0xFFFFu : 0u);
+        const uint32_t B = nv > 3 ? dv.y : (nv > 2 ? dv.y & 0xFFFFu : 0u);
+        uint32_t oa, ob;
+        if (cs == 1) {
+          const uint32_t s0 = A & 0xFFFFu, s1 = s0 + (A >> 16), s2 = s1 + (B & 0xFFFFu), s3 = s2 + (B >> 16);
+          const uint32_t inc = half_incl_sum(s3);
+          const uint32_t base = acc + inc - s3;
+          oa = ((base + s0) & 0xFFFFu) | ((base + s1) << 16);
+          ob = ((base + s2) & 0xFFFFu) | ((base + s3) << 16);
+          acc += half_last(inc);
+        } else {
+          const uint32_t t = pk_add(A, B);
+          const uint32_t inc = half_incl_sum_pk(t);
+          const uint32_t base = pk_add(acc, inc);
+          const uint32_t bx = as_u32(as_us2(base) - as_us2(t));
+          oa = pk_add(bx, A);
+          ob = pk_add(bx, t);
+          acc = pk_add(acc, half_last(inc));
+        }
+        oa = (px_write2(oa, be, ulsb) & ~rawm) | (A & rawm);
+        ob = (px_write2(ob, be, ulsb) & ~rawm) | (B & rawm);
+        if (nv == 4 && vec) {
+          *reinterpret_cast<uint2*>(dst + e) = make_uint2(oa, ob);
+        } else if (nv) {
+          dst[e] = (uint16_t)oa;
+          if (nv > 1) dst[e + 1] = (uint16_t)(oa >> 16);
+          if (nv > 2) dst[e + 2] = (uint16_t)ob;
+          if (nv > 3) dst[e + 3] = (uint16_t)(ob >> 16);
+        }
+      }
+      if (fl) {
+        if (!(rawmask & 1u)) last0 = acc & 0xFFFFu;
+        if (cs > 1 && !(rawmask & 2u)) last1 = acc >> 16;
+        rawmask = 0;
+      }
+      lds_fence();
+    }
+    // request the next chunk once the look-ahead drops below 510 words (it
+    // overwrites words [fill_w - 1024, fill_w - 768), all below P - 256)
+    request(active && status == RPP_OK && !pend && fill_w <= (P >> 5) + 510);
+    RPP_TSTAMP(15);
   }
-  RPP_TSTAMP(15);
+  retire();
   if (b < p.nblocks && hl == 0) p.status[b] = status;
 #ifdef RPP_STATS
   if (lane == 0)

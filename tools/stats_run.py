@@ -26,8 +26,8 @@ pipe.decode()
 torch.cuda.synchronize()
 pipe.check(x)
 L.rpp_stats_fetch(st.ctypes.data, 1)
-names = ["passes", "verify_rounds", "-", "chain_iters", "t_flush+looptop", "t_ensure",
-         "subblocks", "t_header", "-", "t_modes+ensureW0", "t_chains", "t_verify", "t_materialize", "t_extract", "t_end", "t_flush"]
+names = ["windows", "verify_rounds", "slow_subblocks", "-", "t_looptop", "t_ensure",
+         "subblocks", "t_header", "-", "t_modes", "t_ensure+load", "t_chains", "t_verify", "t_extract", "t_end+slow", "t_flush"]
 sb = float(st[6])
 for i, nm in enumerate(names):
     print(f"{nm:20s} total={int(st[i]):12d}  per_subblock={st[i] / sb:8.3f}")
