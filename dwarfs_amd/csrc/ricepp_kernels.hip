@@ -27,6 +27,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <mutex>
+
 #include "ricepp_amd.h"
 
 // Diagnostic builds only: -DRPP_ABLATE=<mask> removes decode phases to time
@@ -497,26 +500,31 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
 // ===========================================================================
 // DECODE
 // ===========================================================================
-// Two streams per wavefront: lanes 0-31 decode stream 2*blockIdx.x, lanes
-// 32-63 stream 2*blockIdx.x+1.  Every per-stream value is uniform within a
-// half; cross-lane ops (DPP row shifts, row_bcast15) never cross the halves.
+// Two streams per wavefront: lanes 0-31 decode one stream, lanes 32-63 the
+// next.  Every per-stream value is uniform within a half; cross-lane ops (DPP
+// row shifts, row_bcast15) never cross the halves.  A workgroup holds up to
+// kDecMaxWaves such waves plus one shared copy of the transfer tables below.
 //
-// A Rice sub-block (ricepp/include/ricepp/detail/decode.h:62-71) is parsed in
-// windows of 32 lane segments of SEG bits (SEG = 40 for fs <= 7, 64 above, so
-// one window covers a typical 128-sample sub-block).  The only serial
-// dependency of the parse is where the first code of a segment starts (its
-// entry state 0..fs: remainder bits of the previous code still to skip).
-// Each lane guesses it by running the terminator chain over the 32 bits
-// before its segment from entry 0 (Rice codes self-synchronise: the guess is
-// right ~3 times in 4), then runs the exact chain of its segment from the
-// guess, recording the start of every code.  Guesses are verified against the
-// left neighbour's exit state; mismatching lanes re-run from the corrected
-// entry until the half is consistent (lane 0's entry is exact, so this
-// terminates; typically one round).  Code counts -> prefix sum -> the lane
-// holding the sub-block's last code -> the next header position.  Each lane
-// then turns its recorded code starts into zig-zag deltas (q from the gap,
-// the fs remainder bits from its registers) into an LDS tile; a chunk's tile
-// is prefix-summed, pixel-encoded and stored with vector stores.
+// A Rice sub-block (ricepp/include/ricepp/detail/decode.h:62-71) has no
+// index: code i+1 starts where code i ends, so the parse is a finite-state
+// machine whose state at any bit boundary is "remainder bits still to skip
+// before the next unary search" (sigma, 0..fs).  Per 8-bit unit and fs the
+// machine's transfer function (sigma -> sigma', and which bits of the byte
+// are code terminators) is a table lookup (g_map_table, 16 B per (fs, byte)).
+// A sub-block is parsed in windows of 32 lane segments of 48 bits starting at
+// the 4-bit header:
+//   1. each lane composes the maps of its 6 bytes into one segment map;
+//   2. a 5-level DPP scan composes the segment maps along the half (function
+//      composition of 8-entry byte maps is two v_perm_b32), so every lane
+//      knows its exact entry state -- no speculation, no re-runs;
+//   3. the entry state selects each byte's terminator bits -> a 48-bit
+//      terminator mask; popcounts -> DPP prefix sums -> code indices and the
+//      lane holding the sub-block's last code (its end is the next header);
+//   4. each lane turns its terminators into zig-zag deltas (q = gap from the
+//      previous code's end, remainder from its registers) into an LDS tile;
+//      a chunk's tile is prefix-summed, pixel-encoded and stored.
+// fs >= 8 uses 16-entry maps (sigma up to 13), composed by two v_perm_b32
+// per dword plus a byte select.
 struct DecParams {
   const uint8_t* in;
   const uint64_t* in_off;
@@ -527,13 +535,68 @@ struct DecParams {
   int32_t* status;
   uint32_t nblocks;
   uint32_t bs, cs, be, ulsb;
+  uint32_t waves;  // waves per workgroup
 };
 
+// ---- transfer tables (built at compile time) ----
+// Entry (fs, byte): dwords {map 0-3, map 4-7, term 0-3, term 4-7}: byte s of
+// `map` is the state after the byte when entering it in state s (0..7), byte
+// s of `term` the bits of the byte that end a code (the '1' closing a unary
+// run) on that path.  Entering in state s >= 8 (fs >= 8 only) skips the byte:
+// state s - 8, no terminator.
+constexpr uint32_t kMapFs = 14;  // fs 0..13 (fs + 1 = 1..14 is a Rice header)
+constexpr uint32_t kMapEntries = kMapFs * 256;
+
+struct MapTable {
+  uint32_t w[kMapEntries * 4];
+};
+
+constexpr MapTable make_map_table() {
+  MapTable t{};
+  for (uint32_t fs = 0; fs < kMapFs; ++fs) {
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t m[2] = {0, 0}, tm[2] = {0, 0};
+      for (uint32_t s = 0; s < 8; ++s) {
+        uint32_t c = s, mask = 0, ex = 0;
+        for (;;) {
+          const uint32_t rest = b >> c;
+          if (rest == 0) {  // the unary search runs into the next byte
+            ex = 0;
+            break;
+          }
+          const uint32_t tp = c + (uint32_t)__builtin_ctz(rest);
+          mask |= 1u << tp;
+          c = tp + 1 + fs;  // skip the terminator and fs remainder bits
+          if (c >= 8) {
+            ex = c - 8;
+            break;
+          }
+        }
+        m[s >> 2] |= ex << (8 * (s & 3));
+        tm[s >> 2] |= mask << (8 * (s & 3));
+      }
+      const uint32_t e = (fs * 256 + b) * 4;
+      t.w[e] = m[0];
+      t.w[e + 1] = m[1];
+      t.w[e + 2] = tm[0];
+      t.w[e + 3] = tm[1];
+    }
+  }
+  return t;
+}
+
+__device__ const MapTable g_map_table = make_map_table();
+
 constexpr uint32_t kHalf = 32;                // lanes per stream
+constexpr uint32_t kSegBits = 48;             // bits per lane segment (6 table bytes)
+constexpr uint32_t kWinBits = kHalf * kSegBits;  // bits per window
 constexpr uint32_t kRingWords = 1024;         // per-stream LDS ring of the compressed stream (4 KiB)
 constexpr uint32_t kRingMask = kRingWords - 1;
 constexpr uint32_t kChunkWords = 4 * kHalf;   // refill unit: 16 B per lane of a half
 constexpr uint32_t kAhead = 288;              // words kept resident ahead of the read position
+constexpr uint32_t kDecMaxWaves = 8;          // waves per workgroup (one table copy each)
+constexpr uint32_t kWaveLdsWords = 2 * kRingWords + kTileSamples;  // 2 rings + 2 tiles of u16
+constexpr uint32_t kTabBytes = kMapEntries * 16;
 
 __device__ __forceinline__ uint32_t half_incl_sum(uint32_t v) {
   v += dpp<kDppRowShr1>(v);
@@ -563,11 +626,6 @@ __device__ __forceinline__ uint32_t half_first(uint32_t v) {
   return lane_id() >= kHalf ? b : a;
 }
 
-__device__ __forceinline__ uint32_t half_ballot(bool pred) {
-  const uint64_t m = __ballot(pred);
-  return lane_id() >= kHalf ? (uint32_t)(m >> 32) : (uint32_t)m;
-}
-
 // Packed 2 x u16 arithmetic (wraps per half-word).
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return as_u32(as_us2(a) + as_us2(b)); }
 
@@ -586,9 +644,55 @@ __device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t be, uint32_t 
   return be ? __builtin_amdgcn_perm(v, v, 0x02030001u) : v;
 }
 
+// ---- state maps ----
+// An 8-entry map (states 0..7) is 8 bytes; byte s = image of s.  g after f
+// (apply f first): byte s of the result = g[f[s]] = v_perm_b32(g.hi, g.lo, f).
+constexpr uint32_t kId0 = 0x03020100u, kId1 = 0x07060504u, kId2 = 0x0B0A0908u, kId3 = 0x0F0E0D0Cu;
+constexpr uint32_t kSelByte0 = 0x0C0C0C00u;  // v_perm selector: byte 0 = index, bytes 1-3 = 0
+
+struct Map8 {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ Map8 comp8(Map8 g, Map8 f) {
+  return Map8{__builtin_amdgcn_perm(g.hi, g.lo, f.lo), __builtin_amdgcn_perm(g.hi, g.lo, f.hi)};
+}
+template <int Ctrl, int RowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp_keep(uint32_t old, uint32_t v) {
+  // lanes without a source in range keep `old`
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, Ctrl, RowMask, 0xF, false);
+}
+template <int Ctrl, int RowMask = 0xF>
+__device__ __forceinline__ Map8 scan_step8(Map8 m) {
+  const Map8 d{dpp_keep<Ctrl, RowMask>(kId0, m.lo), dpp_keep<Ctrl, RowMask>(kId1, m.hi)};
+  return comp8(m, d);
+}
+
+// 16-entry maps (states 0..15) for fs >= 8.
+struct Map16 {
+  uint32_t w[4];
+};
+// bytes of g selected by the 4 byte indices (0..15) in idx
+__device__ __forceinline__ uint32_t sel16(const Map16& g, uint32_t idx) {
+  const uint32_t i7 = idx & 0x07070707u;
+  const uint32_t lo = __builtin_amdgcn_perm(g.w[1], g.w[0], i7);
+  const uint32_t hi = __builtin_amdgcn_perm(g.w[3], g.w[2], i7);
+  const uint32_t m = idx & 0x08080808u;
+  const uint32_t mask = (m << 5) - (m >> 3);  // 0xFF in bytes with index >= 8
+  return (hi & mask) | (lo & ~mask);
+}
+__device__ __forceinline__ Map16 comp16(const Map16& g, const Map16& f) {
+  return Map16{{sel16(g, f.w[0]), sel16(g, f.w[1]), sel16(g, f.w[2]), sel16(g, f.w[3])}};
+}
+template <int Ctrl, int RowMask = 0xF>
+__device__ __forceinline__ Map16 scan_step16(const Map16& m) {
+  const Map16 d{{dpp_keep<Ctrl, RowMask>(kId0, m.w[0]), dpp_keep<Ctrl, RowMask>(kId1, m.w[1]),
+                 dpp_keep<Ctrl, RowMask>(kId2, m.w[2]), dpp_keep<Ctrl, RowMask>(kId3, m.w[3])}};
+  return comp16(m, d);
+}
+
 // Orders this wave's LDS accesses without waiting on its global stores
-// (a one-wave workgroup needs no s_barrier; __syncthreads() would also
-// drain vmcnt, i.e. wait for the previous chunk's output stores).
+// (LDS operations of one wave complete in order; a full __syncthreads()
+// would also drain vmcnt, i.e. wait for the previous chunk's output stores).
 __device__ __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
 
 // Asynchronous global -> LDS copies (global_load_lds): lane l's 16 (4) bytes
@@ -606,13 +710,6 @@ __device__ __forceinline__ void glds4(const void* gsrc, uint32_t m0) {
                : "=&s"(keep) : "v"(gsrc), "s"(m0) : "memory");
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0
-__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
-  uint32_t r;
-  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
 
 // 32-bit word `w` of the stream, zero past the end (bitstream_reader.h:165-166
 // zero-pads the last packet; reading beyond it is checked separately).
@@ -633,72 +730,23 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, uint32_t nbytes, 
                     stream_word(in, nbytes, w + 3));
 }
 
-// Terminator chain through a lane segment [0, SEG) held in the low SEG bits
-// of X.  The unary search of the first code starts at bit `entry`; every '1'
-// found ends a code, whose fs remainder bits are skipped.  cnt = codes whose
-// terminator lies in the segment; lastc = search start after the last of
-// them; exit = where the search enters the next segment (0 when it runs off
-// the end while searching).  `slow` flags a unary run of >= 32 bits (the
-// search looks 32 bits ahead) or an unfinished chain.
-struct SegChain {
-  uint32_t cnt, exit, lastc;
-  bool slow;
-};
-
-// Segments are 48 bits, so a chain position (< 48 + 14) always shifts a
-// 64-bit register validly; bits at and above SEG are zero, which freezes a
-// finished chain (no terminator -> c = max(c, SEG)).  Fixed, wave-uniform
-// trip counts: a per-step `__any` exit costs ~100 cycles of VALU->SALU
-// latency (measured), more than the step itself.  The search window is 32
-// bits: callers check the segment for a run of 32 zeros (zero_run32).
-constexpr uint32_t kSeg = 48;
-
-template <int SEG>
-__device__ __forceinline__ SegChain seg_chain(uint64_t X, uint32_t entry, uint32_t fsp1, uint32_t nsteps) {
-  uint32_t c = entry, cnt = 0, lastc = 0;
-  for (uint32_t j = 0; j < nsteps; ++j) {
-    const uint32_t t = ffbl((uint32_t)(X >> c));
-    const bool fnd = t != ~0u;
-    const uint32_t cn = c + t + fsp1;
-    cnt += fnd ? 1u : 0u;
-    lastc = fnd ? cn : lastc;
-    c = fnd ? cn : max(c, (uint32_t)SEG);
+__global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
+  // ---- the transfer tables, one copy per workgroup ----
+  {
+    const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
+    for (uint32_t i = threadIdx.x; i < kMapEntries; i += blockDim.x) dsm[i] = gt[i];
   }
-  return SegChain{cnt, c - SEG, lastc, c < (uint32_t)SEG};
-}
-
-// exit state only (the look-back guess)
-template <int SEG>
-__device__ __forceinline__ uint32_t seg_exit(uint64_t X, uint32_t entry, uint32_t fsp1, uint32_t nsteps) {
-  uint32_t c = entry;
-  for (uint32_t j = 0; j < nsteps; ++j) {
-    const uint32_t t = ffbl((uint32_t)(X >> c));
-    c = t != ~0u ? c + t + fsp1 : max(c, (uint32_t)SEG);
-  }
-  return c - SEG;
-}
-
-// Does the SEG-bit segment X hold 32 consecutive zeros?
-template <int SEG>
-__device__ __forceinline__ bool zero_run32(uint64_t X) {
-  uint64_t z = ~X & ((UINT64_C(1) << SEG) - 1);
-  z &= z >> 1;
-  z &= z >> 2;
-  z &= z >> 4;
-  z &= z >> 8;
-  z &= z >> 16;
-  return z != 0;
-}
-
-__global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
-  __shared__ __attribute__((aligned(16))) uint32_t ring_s[2][kRingWords];
-  __shared__ __attribute__((aligned(16))) uint16_t tile_s[2][kTileSamples];
+  __syncthreads();
+  const uint4* tab = dsm;
   const uint32_t lane = lane_id();
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t h = lane >> 5, hl = lane & (kHalf - 1);
-  uint32_t* ring = ring_s[h];
-  uint16_t* tile = tile_s[h];
+  uint32_t* ring_w = reinterpret_cast<uint32_t*>(dsm + kMapEntries) + wv * kWaveLdsWords;  // this wave's rings
+  uint32_t* ring = ring_w + h * kRingWords;
+  uint16_t* tile = reinterpret_cast<uint16_t*>(ring_w + 2 * kRingWords) + h * kTileSamples;
   const uint32_t bs = p.bs, cs = p.cs, be = p.be, ulsb = p.ulsb;
-  const uint32_t b = 2 * blockIdx.x + h;
+  const uint32_t b = 2 * (blockIdx.x * p.waves + wv) + h;
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
   unsigned long long tprev_;
@@ -735,9 +783,9 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
   //      256 words lying wholly inside the input is requested by
   //      global_load_lds (no registers, nothing for the compiler to wait on);
   //      it is retired (vmcnt(0), by then long complete together with that
-  //      iteration's output stores) at the top of the next iteration's flush,
-  //      and only then counted resident.  ensure() is the synchronous path
-  //      (start-up, the zero-padded tail, long sub-blocks). ----
+  //      iteration's output stores) before the next flush, and only then
+  //      counted resident.  ensure() is the synchronous path (start-up, the
+  //      zero-padded tail, long sub-blocks). ----
   uint32_t fill_w = 0;
   bool pend = false;  // a requested chunk is in flight for this half
   auto retire = [&]() {
@@ -764,7 +812,8 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
         const uint32_t fw = __builtin_amdgcn_readfirstlane(readlane(fill_w, hh * kHalf));
         const bool a16 = readlane(aligned16 ? 1u : 0u, hh * kHalf) != 0;
         // m0 such that lane hh*32 + l lands at ring slot + 16 l (4 l)
-        const uint32_t slot = (uint32_t)(uintptr_t)&ring_s[hh][fw & kRingMask];
+        const uint32_t slot =
+            __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring_w[hh * kRingWords + (fw & kRingMask)]);
         if (want && h == hh) {
           const uint8_t* src = in + 4u * fw;
           if (a16) {
@@ -819,23 +868,18 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
       status = RPP_TRUNCATED_INPUT;
       active = false;
     }
-    const uint32_t P4 = P + 4;
-    // this lane's Rice window segment [sb, sb + 48) (window = 32 lanes from
-    // P + 4), the 96 bits before it and 16 bits past it; lane 0's look-back
-    // ends with the header
-    uint32_t lk0, lk1, lk2, lo, hiu;
-    auto load_seg = [&](uint32_t sb) {
+    // this lane's 64 bits from bit sb of the stream (its 48-bit segment of
+    // the window and what follows it)
+    uint32_t xl, xh;
+    auto load_x = [&](uint32_t sb) {
       const uint32_t wb = sb >> 5, o = sb & 31u;
-      const uint32_t a0 = word(wb - 3), a1 = word(wb - 2), a2 = word(wb - 1), a3 = word(wb), a4 = word(wb + 1),
-                     a5 = word(wb + 2);
-      lk0 = __builtin_amdgcn_alignbit(a1, a0, o);
-      lk1 = __builtin_amdgcn_alignbit(a2, a1, o);
-      lk2 = __builtin_amdgcn_alignbit(a3, a2, o);
-      lo = __builtin_amdgcn_alignbit(a4, a3, o);
-      hiu = __builtin_amdgcn_alignbit(a5, a4, o);
+      const uint32_t a0 = word(wb), a1 = word(wb + 1), a2 = word(wb + 2);
+      xl = __builtin_amdgcn_alignbit(a1, a0, o);
+      xh = __builtin_amdgcn_alignbit(a2, a1, o);
     };
-    load_seg(P4 + kSeg * hl);
-    const uint32_t fsp1 = active ? half_first(lk2) >> 28 : 0u;
+    load_x(P + kSegBits * hl);
+    const uint32_t fsp1 = active ? half_first(xl) & 15u : 0u;
+    const uint32_t P4 = P + 4;
     uint32_t E = P4;
     RPP_STAT(6, 1);
     RPP_TSTAMP(7);
@@ -858,154 +902,147 @@ __global__ __launch_bounds__(kWave) void rpp_decode_kernel(DecParams p) {
       }
     }
     const bool rice = active && fsp1 != 0 && fsp1 != 15;
-    const uint32_t fs = rice ? fsp1 - 1 : 0u;
-    bool slowh = rice && fs == 0;  // fs 0: serial path below
     RPP_TSTAMP(9);
-    if (__any(rice && fs != 0)) {
-      // decode.h:62-71: Rice codes, fs = fsp1 - 1 >= 1
-      const uint32_t fa = readlane(rice ? fs : 0u, 0), fb = readlane(rice ? fs : 0u, kHalf);
-      const bool ra = readlane(rice ? 1u : 0u, 0) != 0, rb = readlane(rice ? 1u : 0u, kHalf) != 0;
-      const uint32_t fmin1 = min(ra && fa ? fa : 15u, rb && fb ? fb : 15u) + 1;  // smallest fs + 1 >= 2
-      const uint32_t fs1 = fs + 1;  // >= 1 in every lane (halves not parsing Rice still run the chains)
-      auto rice_fast = [&]<int SEG>() {
-        const uint32_t nsteps = (SEG + fmin1 - 1) / fmin1 + 1;  // codes per segment + 1
-        // q0: first bit of the window; e_in: entry state of its lane 0;
-        // s_in: where the code open at the window start began (its unary run
-        // may span earlier segments)
-        uint32_t q0 = P4, e_in = 0, done = 0, s_in = P4;
-        bool go = rice && fs != 0;
-        while (__any(go)) {
-          RPP_STAT(0, 1);
-          if (__any(q0 != P4)) {  // continuation window: the sub-block is longer than 32 segments
-            if (go && q0 != P4 && q0 >= lim) {  // no input left for the next code
-              status = RPP_TRUNCATED_INPUT;
-              go = false;
-            }
-            ensure(q0 >> 5, go);
-            load_seg(q0 + SEG * hl);
-          }
-          const uint32_t sb = q0 + SEG * hl;
-          const uint64_t X = ((uint64_t)(hiu & ((1u << (SEG - 32)) - 1u)) << 32) | lo;  // the segment
-          const uint64_t XR = ((uint64_t)hiu << 32) | lo;                              // + what follows
-          RPP_TSTAMP(10);
-          // entry guess: chain over the 96 bits before the segment from entry 0
-          const uint32_t e1 = seg_exit<48>(((uint64_t)(lk1 & 0xFFFFu) << 32) | lk0, 0, fs1, (48 + fmin1 - 1) / fmin1 + 1);
-          const uint32_t e2 = seg_exit<48>(((uint64_t)lk2 << 16) | (lk1 >> 16), e1, fs1, (48 + fmin1 - 1) / fmin1 + 1);
-          uint32_t g = hl == 0 ? e_in : ((RPP_ABLATE & 8) ? 0u : e2);
-          SegChain ch = seg_chain<SEG>(X, g, fs1, nsteps);
-          const bool zr = zero_run32<SEG>(X);
-          RPP_TSTAMP(11);
-          const uint32_t need = n - done;
-          uint32_t incl, L;
-          bool fin;
-          // verify entries against the left neighbour's exit; re-run until
-          // consistent (lane 0 is exact: at most kHalf rounds)
-          for (uint32_t round = 0;; ++round) {
-            incl = half_incl_sum(go ? ch.cnt : 0u);
-            const uint32_t fm = half_ballot(go && incl >= need);
-            fin = fm != 0;
-            L = fin ? (uint32_t)__builtin_ctz(fm) : kHalf - 1;
-            const uint32_t lx_ = from_left(ch.exit);  // all lanes active (DPP source)
-            const uint32_t want = hl == 0 ? e_in : lx_;
-            const bool bad = go && hl <= L && want != g;
-            if (!__any(bad) || round > kHalf || (RPP_ABLATE & 4)) break;
-            RPP_STAT(1, 1);
-            g = want;
-            ch = seg_chain<SEG>(X, g, fs1, nsteps);
-          }
-          RPP_TSTAMP(12);
-          const uint32_t excl = incl - (go ? ch.cnt : 0u);
-          // start of the code open at this segment's entry: the last code
-          // start (terminator + fs + 1) of any segment to the left
-          const uint32_t smax = half_incl_max(go && ch.cnt ? sb + ch.lastc : 0u);
-          const uint32_t sleft = from_left(smax);
-          const uint32_t sopen = max(s_in, hl == 0 ? 0u : sleft);
-          // a relevant lane whose chain could not be followed -> serial path
-          const bool sl = half_ballot(go && hl <= L && (ch.slow || zr)) != 0;
-          if (sl) {
-            slowh = slowh || go;
+    if (__any(rice)) {
+      // decode.h:62-71: n Rice codes with fs = fsp1 - 1
+      const uint32_t fs = rice ? fsp1 - 1 : 0u;
+      const uint32_t k = fs + 1;
+      const uint32_t fmask = (1u << fs) - 1u;
+      const bool wide = fs >= 8;
+      const uint4* tb = tab + 256u * fs;
+      // q0: first bit of the window; s0: state at q0 (4 = skip the header);
+      // s_in: end of the last code before the window; done: codes before it
+      uint32_t q0 = P, s0 = 4, s_in = P4, done = 0;
+      bool go = rice;
+      while (__any(go)) {
+        RPP_STAT(0, 1);
+        if (__any(q0 != P)) {  // continuation window: the sub-block is longer than kWinBits
+          if (go && q0 != P && q0 >= lim) {  // the open unary search would read past the input
+            status = RPP_TRUNCATED_INPUT;
             go = false;
           }
-          // zig-zag deltas of this lane's codes (decode.h:66-69): walk the
-          // chain again from the verified entry
-          const uint32_t mine = go ? min(ch.cnt, need > excl ? need - excl : 0u) : 0u;
-          const uint32_t lowmask = (1u << fs) - 1u;
-          uint32_t erel = 0, c = g, sop = sopen;
-          for (uint32_t j = 1; j < ((RPP_ABLATE & 2) ? 0u : nsteps); ++j) {
-            const bool act = j <= mine;
-            const uint32_t t = ffbl((uint32_t)(XR >> c));
-            const uint32_t q = sb + c + t - sop;
-            const uint32_t k = c + t + 1;  // remainder = bits [k, k + fs), k + fs < 64
-            const uint32_t diff = (q << fs) | ((uint32_t)(XR >> k) & lowmask);
-            const uint32_t delta = (diff >> 1) ^ (0u - (diff & 1u));
-            if (act) tile[comp + cs * (done + excl + j - 1)] = (uint16_t)delta;
-            c = act ? k + fs : c;
-            sop = sb + c;
-            erel = act ? c : erel;
+          ensure(q0 >> 5, go);
+          load_x(q0 + kSegBits * hl);
+        }
+        const uint32_t sb = q0 + kSegBits * hl;
+        // ---- 1. byte transfer functions ----
+        uint4 e[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) e[j] = tb[__builtin_amdgcn_ubfe(j < 4 ? xl : xh, 8 * (j & 3), 8)];
+        RPP_TSTAMP(10);
+        uint32_t tml = 0, tmh = 0, xexit = 0;
+        if (__any(go && !wide)) {
+          // ---- 2. segment map, scan along the half, entry state ----
+          const Map8 m01 = comp8(Map8{e[1].x, e[1].y}, Map8{e[0].x, e[0].y});
+          const Map8 m23 = comp8(Map8{e[3].x, e[3].y}, Map8{e[2].x, e[2].y});
+          const Map8 m45 = comp8(Map8{e[5].x, e[5].y}, Map8{e[4].x, e[4].y});
+          Map8 M = comp8(m45, comp8(m23, m01));
+          M = scan_step8<kDppRowShr1>(M);
+          M = scan_step8<kDppRowShr2>(M);
+          M = scan_step8<kDppRowShr4>(M);
+          M = scan_step8<kDppRowShr8>(M);
+          M = scan_step8<kDppRowBcast15, 0xA>(M);
+          Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
+          if (hl == 0) X = Map8{kId0, kId1};
+          // ---- 3. terminators of this lane's segment ----
+          uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
+          uint32_t t[6];
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            t[j] = __builtin_amdgcn_perm(e[j].w, e[j].z, sel);
+            sel = __builtin_amdgcn_perm(e[j].y, e[j].x, sel) | kSelByte0;
           }
-          RPP_TSTAMP(13);
-          const uint32_t tot = half_last(incl);
-          const uint32_t ea_ = readlane(erel, (int)readlane(L, 0)), eb_ = readlane(erel, (int)(readlane(L, kHalf) + kHalf));
-          const uint32_t lx = half_last(ch.exit);
-          if (go && fin) {
-            E = q0 + SEG * L + (h ? eb_ : ea_);
-            if (E > lim) status = RPP_TRUNCATED_INPUT;
-            go = false;
-          }
-          const uint32_t sl_ = half_last(smax);
-          if (go) {
-            done += tot;
-            e_in = lx;
-            s_in = max(s_in, sl_);
-            q0 += kHalf * SEG;
+          if (!wide) {
+            tml = t[0] | (t[1] << 8) | (t[2] << 16) | (t[3] << 24);
+            tmh = t[4] | (t[5] << 8);
+            xexit = sel & 0xFFu;
           }
         }
-      };
-      rice_fast.template operator()<kSeg>();
+        if (__any(go && wide)) {
+          Map16 bm[6];
+#pragma unroll
+          for (int j = 0; j < 6; ++j) bm[j] = Map16{{e[j].x, e[j].y, kId0, kId1}};
+          Map16 M = comp16(bm[5], comp16(bm[4], comp16(comp16(bm[3], bm[2]), comp16(bm[1], bm[0]))));
+          M = scan_step16<kDppRowShr1>(M);
+          M = scan_step16<kDppRowShr2>(M);
+          M = scan_step16<kDppRowShr4>(M);
+          M = scan_step16<kDppRowShr8>(M);
+          M = scan_step16<kDppRowBcast15, 0xA>(M);
+          Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
+                   dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
+          if (hl == 0) X = Map16{{kId0, kId1, kId2, kId3}};
+          uint32_t st = sel16(X, s0) & 0xFFu;
+          uint32_t t[6];
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            const uint32_t sel = st | kSelByte0;
+            const bool skip = st >= 8;
+            t[j] = skip ? 0u : __builtin_amdgcn_perm(e[j].w, e[j].z, sel);
+            st = skip ? st - 8 : __builtin_amdgcn_perm(e[j].y, e[j].x, sel);
+          }
+          if (wide) {
+            tml = t[0] | (t[1] << 8) | (t[2] << 16) | (t[3] << 24);
+            tmh = t[4] | (t[5] << 8);
+            xexit = st;
+          }
+        }
+        RPP_TSTAMP(11);
+        // ---- 4. code counts -> indices; the lane holding code n-1 ----
+        const uint32_t cnt = go ? __builtin_popcount(tml) + __builtin_popcount(tmh) : 0u;
+        const uint32_t incl = half_incl_sum(cnt);
+        const uint32_t excl = incl - cnt;
+        const uint32_t need = n - done;
+        const uint64_t finm = __ballot(go && incl >= need);
+        const uint32_t L0 = (uint32_t)finm ? (uint32_t)__builtin_ctz((uint32_t)finm) : 0u;
+        const uint32_t L1 = (uint32_t)(finm >> 32) ? (uint32_t)__builtin_ctz((uint32_t)(finm >> 32)) : 0u;
+        const bool fin = (h ? (uint32_t)(finm >> 32) : (uint32_t)finm) != 0;
+        // end of the last code of each lane -> start of the code open at a
+        // lane's entry (its unary run may span earlier segments)
+        const uint32_t lastt = tmh ? 63u - (uint32_t)__builtin_clz(tmh) : 31u - (uint32_t)__builtin_clz(tml | 1u);
+        const uint32_t lend = cnt ? sb + lastt + k : 0u;
+        const uint32_t smax = half_incl_max(lend);
+        const uint32_t sleft = from_left(smax);
+        uint32_t prev = max(s_in, hl == 0 ? 0u : sleft);
+        // ---- 5. zig-zag deltas of this lane's codes (decode.h:66-69) ----
+        const uint32_t mine = go && need > excl ? min(cnt, need - excl) : 0u;
+        const uint32_t mmax = half_incl_max(mine);
+        const uint32_t trips = max(readlane(mmax, kHalf - 1), readlane(mmax, kWave - 1));
+        const uint64_t X64 = ((uint64_t)xh << 32) | xl;
+        uint64_t tm = ((uint64_t)tmh << 32) | tml;
+        uint16_t* tdst = tile + comp + cs * (done + excl);
+        uint32_t ecand = 0;
+        for (uint32_t j = 0; j < ((RPP_ABLATE & 2) ? 0u : trips); ++j) {
+          const bool act = j < mine;
+          const uint32_t t = (uint32_t)__builtin_ctzll(tm | (UINT64_C(1) << kSegBits));
+          tm &= tm - 1;
+          const uint32_t tg = sb + t;
+          const uint32_t q = tg - prev;
+          const uint32_t rem = (uint32_t)(X64 >> (t + 1)) & fmask;
+          const uint32_t diff = (q << fs) | rem;
+          const uint32_t delta = (diff >> 1) ^ (0u - (diff & 1u));
+          if (act) tdst[cs * j] = (uint16_t)delta;
+          prev = tg + k;
+          ecand = act && excl + j + 1 == need ? prev : ecand;
+        }
+        RPP_TSTAMP(12);
+        const uint32_t tot = half_last(incl);
+        const uint32_t ea = readlane(ecand, (int)L0), eb = readlane(ecand, (int)(L1 + kHalf));
+        if (go && fin) {
+          E = h ? eb : ea;
+          if (E > lim) status = RPP_TRUNCATED_INPUT;
+          go = false;
+        }
+        const uint32_t wexit = half_last(xexit);
+        const uint32_t slast = half_last(smax);
+        if (go) {
+          done += tot;
+          s0 = wexit;
+          s_in = max(s_in, slast);
+          q0 += kWinBits;
+        }
+      }
     }
     RPP_TSTAMP(14);
-    if (__any(slowh)) {
-      // serial path (lane 0 of the half): fs 0, unary runs >= 32 bits,
-      // corrupt streams.  Resumable across ring refills.
-      RPP_STAT(2, 1);
-      uint32_t pos = P4, k = 0, qacc = 0;
-      bool sgo = slowh;
-      while (__any(sgo)) {
-        const uint32_t pb = half_first(pos);
-        ensure(pb >> 5, sgo);
-        if (sgo && hl == 0) {
-          const uint32_t resident = ((pb >> 5) + kAhead - 2) * 32u;
-          while (k < n) {
-            if (pos + 64 > resident) break;
-            const uint32_t w = peek32(pos);
-            if (w == 0) {
-              if (pos + 32 >= lim) {  // the terminator would lie past the input
-                status = RPP_TRUNCATED_INPUT;
-                break;
-              }
-              qacc += 32;
-              pos += 32;
-              continue;
-            }
-            const uint32_t t = ffbl(w);
-            qacc += t;
-            pos += t + 1;
-            const uint32_t rem = fs ? peek32(pos) & ((1u << fs) - 1u) : 0u;
-            pos += fs;
-            const uint32_t diff = (qacc << fs) | rem;
-            qacc = 0;
-            tile[comp + cs * k] = (uint16_t)((diff >> 1) ^ (0u - (diff & 1u)));
-            ++k;
-          }
-        }
-        status = (int32_t)half_first((uint32_t)status);
-        sgo = sgo && status == RPP_OK && half_first(k) < n;
-      }
-      if (slowh && status == RPP_OK) {
-        E = half_first(pos);
-        if (E > lim) status = RPP_TRUNCATED_INPUT;
-      }
-    }
     if (active && status == RPP_OK) P = E;
     retire();
     lds_fence();
@@ -1136,10 +1173,23 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   if (!d_in || !d_in_offsets || !d_in_bytes || !d_out || !d_out_offsets || !d_n_samples || !d_status)
     return RPP_INVALID_ARGUMENT;
   if (cfg->component_stream_count * cfg->block_size > (uint32_t)kTileSamples) return RPP_UNSUPPORTED_CONFIG;
+  // two streams per wave; up to kDecMaxWaves waves share one copy of the
+  // transfer tables, fewer when the batch cannot fill the 256 CUs anyway
+  const uint32_t nwaves = (nblocks + 1) / 2;
+  const uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nwaves + 255) / 256));
+  const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
+  static std::once_flag attr_once;
+  static hipError_t attr_err = hipSuccess;
+  std::call_once(attr_once, [] {
+    attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&rpp_decode_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4));
+  });
+  if (attr_err != hipSuccess) return RPP_HIP_ERROR;
   DecParams p{d_in, d_in_offsets, d_in_bytes, d_out, d_out_offsets, d_n_samples, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count};
-  hipLaunchKernelGGL(rpp_decode_kernel, dim3((nblocks + 1) / 2), dim3(kWave), 0, (hipStream_t)stream, p);
+              cfg->unused_lsb_count, W};
+  hipLaunchKernelGGL(rpp_decode_kernel, dim3((nwaves + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
