@@ -500,24 +500,23 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
 // ===========================================================================
 // DECODE
 // ===========================================================================
-// Two streams per wavefront: lanes 0-31 decode one stream, lanes 32-63 the
-// next.  Every per-stream value is uniform within a half; cross-lane ops (DPP
-// row shifts, row_bcast15) never cross the halves.  A workgroup holds up to
-// kDecMaxWaves such waves plus one shared copy of the transfer tables below.
+// One stream per wavefront; a workgroup holds up to kDecMaxWaves waves plus
+// one shared copy of the transfer tables below.  Per-stream state is
+// wave-uniform (scalar registers, uniform branches).
 //
 // A Rice sub-block (ricepp/include/ricepp/detail/decode.h:62-71) has no
 // index: code i+1 starts where code i ends, so the parse is a finite-state
 // machine whose state at any bit boundary is "remainder bits still to skip
 // before the next unary search" (sigma, 0..fs).  Per 8-bit unit and fs the
 // machine's transfer function (sigma -> sigma', and which bits of the byte
-// are code terminators) is a table lookup (g_map_table, 16 B per (fs, byte)).
-// A sub-block is parsed in windows of 32 lane segments of 48 bits starting at
-// the 4-bit header:
-//   1. each lane composes the maps of its 6 bytes into one segment map;
-//   2. a 5-level DPP scan composes the segment maps along the half (function
+// end a code) is a table lookup (g_map_table, 16 B per (fs, byte)).  A
+// sub-block is parsed in windows of 64 lane segments of 24 bits starting at
+// its 4-bit header:
+//   1. each lane composes the maps of its 3 bytes into one segment map;
+//   2. a 6-level DPP scan composes the segment maps along the wave (function
 //      composition of 8-entry byte maps is two v_perm_b32), so every lane
 //      knows its exact entry state -- no speculation, no re-runs;
-//   3. the entry state selects each byte's terminator bits -> a 48-bit
+//   3. the entry state selects each byte's terminator bits -> a 24-bit
 //      terminator mask; popcounts -> DPP prefix sums -> code indices and the
 //      lane holding the sub-block's last code (its end is the next header);
 //   4. each lane turns its terminators into zig-zag deltas (q = gap from the
@@ -535,7 +534,7 @@ struct DecParams {
   int32_t* status;
   uint32_t nblocks;
   uint32_t bs, cs, be, ulsb;
-  uint32_t waves;  // waves per workgroup
+  uint32_t waves;  // waves (streams) per workgroup
 };
 
 // ---- transfer tables (built at compile time) ----
@@ -587,54 +586,29 @@ constexpr MapTable make_map_table() {
 
 __device__ const MapTable g_map_table = make_map_table();
 
-constexpr uint32_t kHalf = 32;                // lanes per stream
-constexpr uint32_t kSegBits = 48;             // bits per lane segment (6 table bytes)
-constexpr uint32_t kWinBits = kHalf * kSegBits;  // bits per window
-constexpr uint32_t kRingWords = 1024;         // per-stream LDS ring of the compressed stream (4 KiB)
+constexpr uint32_t kSegBits = 24;                // bits per lane segment (3 table bytes)
+constexpr uint32_t kWinBits = kWave * kSegBits;  // bits per window
+constexpr uint32_t kRingWords = 1024;            // per-stream LDS ring of the compressed stream (4 KiB)
 constexpr uint32_t kRingMask = kRingWords - 1;
-constexpr uint32_t kChunkWords = 4 * kHalf;   // refill unit: 16 B per lane of a half
-constexpr uint32_t kAhead = 288;              // words kept resident ahead of the read position
-constexpr uint32_t kDecMaxWaves = 8;          // waves per workgroup (one table copy each)
-constexpr uint32_t kWaveLdsWords = 2 * kRingWords + kTileSamples;  // 2 rings + 2 tiles of u16
+constexpr uint32_t kChunkWords = 4 * kWave;      // refill unit: 16 B per lane
+constexpr uint32_t kAhead = 288;                 // words kept resident ahead of the read position
+constexpr uint32_t kDecMaxWaves = 16;            // waves per workgroup (one table copy each)
+constexpr uint32_t kTileSlots = kTileSamples + 8;  // + a dump slot for masked-off lanes
+constexpr uint32_t kWaveLdsWords = kRingWords + kTileSlots / 2;
 constexpr uint32_t kTabBytes = kMapEntries * 16;
 
-__device__ __forceinline__ uint32_t half_incl_sum(uint32_t v) {
-  v += dpp<kDppRowShr1>(v);
-  v += dpp<kDppRowShr2>(v);
-  v += dpp<kDppRowShr4>(v);
-  v += dpp<kDppRowShr8>(v);
-  v += dpp<kDppRowBcast15, 0xA>(v);
-  return v;
-}
-
-__device__ __forceinline__ uint32_t half_incl_max(uint32_t v) {
-  v = max(v, dpp<kDppRowShr1>(v));
-  v = max(v, dpp<kDppRowShr2>(v));
-  v = max(v, dpp<kDppRowShr4>(v));
-  v = max(v, dpp<kDppRowShr8>(v));
-  v = max(v, dpp<kDppRowBcast15, 0xA>(v));
-  return v;
-}
-
-__device__ __forceinline__ uint32_t half_last(uint32_t v) {
-  const uint32_t a = readlane(v, kHalf - 1), b = readlane(v, kWave - 1);
-  return lane_id() >= kHalf ? b : a;
-}
-
-__device__ __forceinline__ uint32_t half_first(uint32_t v) {
-  const uint32_t a = readlane(v, 0), b = readlane(v, kHalf);
-  return lane_id() >= kHalf ? b : a;
-}
+__device__ __forceinline__ uint32_t wave_last(uint32_t v) { return readlane(v, kWave - 1); }
 
 // Packed 2 x u16 arithmetic (wraps per half-word).
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return as_u32(as_us2(a) + as_us2(b)); }
 
-__device__ __forceinline__ uint32_t half_incl_sum_pk(uint32_t v) {
+__device__ __forceinline__ uint32_t wave_incl_sum_pk(uint32_t v) {
   v = pk_add(v, dpp<kDppRowShr1>(v));
   v = pk_add(v, dpp<kDppRowShr2>(v));
   v = pk_add(v, dpp<kDppRowShr4>(v));
   v = pk_add(v, dpp<kDppRowShr8>(v));
   v = pk_add(v, dpp<kDppRowBcast15, 0xA>(v));
+  v = pk_add(v, dpp<kDppRowBcast31, 0xC>(v));
   return v;
 }
 
@@ -711,6 +685,13 @@ __device__ __forceinline__ void glds4(const void* gsrc, uint32_t m0) {
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // 32-bit word `w` of the stream, zero past the end (bitstream_reader.h:165-166
 // zero-pads the last packet; reading beyond it is checked separately).
 __device__ __forceinline__ uint32_t stream_word(const uint8_t* in, uint32_t nbytes, uint32_t w) {
@@ -720,14 +701,6 @@ __device__ __forceinline__ uint32_t stream_word(const uint8_t* in, uint32_t nbyt
   uint32_t v = 0;
   for (uint32_t k = 0; k < nbytes - byte0; ++k) v |= (uint32_t)in[byte0 + k] << (8 * k);
   return v;
-}
-
-// This lane's 4 words of the 128-word chunk starting at word `w0`.
-__device__ __forceinline__ uint4 load_chunk(const uint8_t* in, uint32_t nbytes, uint32_t w0, bool aligned16) {
-  const uint32_t w = w0 + 4 * (lane_id() & (kHalf - 1));
-  if (aligned16 && 4 * w + 16 <= nbytes) return *reinterpret_cast<const uint4*>(in + 4 * w);
-  return make_uint4(stream_word(in, nbytes, w), stream_word(in, nbytes, w + 1), stream_word(in, nbytes, w + 2),
-                    stream_word(in, nbytes, w + 3));
 }
 
 __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecParams p) {
@@ -741,24 +714,23 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint4* tab = dsm;
   const uint32_t lane = lane_id();
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint32_t h = lane >> 5, hl = lane & (kHalf - 1);
-  uint32_t* ring_w = reinterpret_cast<uint32_t*>(dsm + kMapEntries) + wv * kWaveLdsWords;  // this wave's rings
-  uint32_t* ring = ring_w + h * kRingWords;
-  uint16_t* tile = reinterpret_cast<uint16_t*>(ring_w + 2 * kRingWords) + h * kTileSamples;
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + kMapEntries) + wv * kWaveLdsWords;
+  uint16_t* tile = reinterpret_cast<uint16_t*>(ring + kRingWords);
   const uint32_t bs = p.bs, cs = p.cs, be = p.be, ulsb = p.ulsb;
-  const uint32_t b = 2 * (blockIdx.x * p.waves + wv) + h;
+  const uint32_t b = blockIdx.x * p.waves + wv;
+  if (b >= p.nblocks) return;  // no barrier below this point
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
   unsigned long long tprev_;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
 #endif
 
-  // ---- per-stream setup (uniform within the half) ----
+  // ---- per-stream setup (wave-uniform) ----
   int32_t status = RPP_OK;
   uint32_t N = 0, nbytes = 0;
   const uint8_t* in = p.in;
   uint16_t* out = p.out;
-  if (b < p.nblocks) {
+  {
     const uint64_t n64 = p.n_samples[b];
     const uint64_t ioff = p.in_off[b];
     const uint64_t nb64 = p.in_bytes[b];
@@ -776,7 +748,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   // (bitstream_reader.h:149-183), so it only throws past this point.
   const uint32_t lim = 64u * ((nbytes + 7u) >> 3);
   const uint32_t chunk_len = cs * bs;
-  const uint32_t nsb = b < p.nblocks && status == RPP_OK ? ((N + chunk_len - 1) / chunk_len) * cs : 0u;
+  const uint32_t nsb = status == RPP_OK ? ((N + chunk_len - 1) / chunk_len) * cs : 0u;
 
   // ---- LDS ring of the stream's words: words [fill_w - kRingWords, fill_w)
   //      are resident.  Steady state: at the end of an iteration, a chunk of
@@ -787,55 +759,47 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   //      counted resident.  ensure() is the synchronous path (start-up, the
   //      zero-padded tail, long sub-blocks). ----
   uint32_t fill_w = 0;
-  bool pend = false;  // a requested chunk is in flight for this half
+  bool pend = false;  // a requested chunk is in flight
   auto retire = [&]() {
-    if (__any(pend)) {
+    if (pend) {
       vm_drain();
-      fill_w = pend ? fill_w + 2 * kChunkWords : fill_w;
+      fill_w += kChunkWords;
       pend = false;
     }
   };
-  auto refill_sync = [&](bool go) {  // appends 256 words (zero past the input) synchronously
-    if (go) {
-      const uint4 v0 = load_chunk(in, nbytes, fill_w, aligned16);
-      const uint4 v1 = load_chunk(in, nbytes, fill_w + kChunkWords, aligned16);
-      *reinterpret_cast<uint4*>(&ring[(fill_w + 4 * hl) & kRingMask]) = v0;
-      *reinterpret_cast<uint4*>(&ring[(fill_w + kChunkWords + 4 * hl) & kRingMask]) = v1;
+  auto refill_sync = [&]() {  // appends 256 words (zero past the input) synchronously
+    const uint32_t w = fill_w + 4 * lane;
+    uint4 v;
+    if (aligned16 && 4 * w + 16 <= nbytes) {
+      v = *reinterpret_cast<const uint4*>(in + 4 * w);
+    } else {
+      v = make_uint4(stream_word(in, nbytes, w), stream_word(in, nbytes, w + 1), stream_word(in, nbytes, w + 2),
+                     stream_word(in, nbytes, w + 3));
     }
-    fill_w = go ? fill_w + 2 * kChunkWords : fill_w;
+    *reinterpret_cast<uint4*>(&ring[w & kRingMask]) = v;
+    fill_w += kChunkWords;
   };
-  auto request = [&](bool want) {  // asynchronous 256-word chunk for halves that want one
-    want = want && 4u * (fill_w + 2 * kChunkWords) <= nbytes;
+  auto request = [&]() {  // asynchronous 256-word chunk (only wholly inside the input)
+    if (4u * (fill_w + kChunkWords) > nbytes) return;
+    // m0 such that lane l lands at ring slot + 16 l (4 l)
+    const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[fill_w & kRingMask]);
+    const uint8_t* src = in + 4u * fill_w;
+    if (aligned16) {
+      glds16(src + 16u * lane, slot);
+    } else {
 #pragma unroll
-    for (uint32_t hh = 0; hh < 2; ++hh) {
-      if (__any(want && h == hh)) {
-        const uint32_t fw = __builtin_amdgcn_readfirstlane(readlane(fill_w, hh * kHalf));
-        const bool a16 = readlane(aligned16 ? 1u : 0u, hh * kHalf) != 0;
-        // m0 such that lane hh*32 + l lands at ring slot + 16 l (4 l)
-        const uint32_t slot =
-            __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring_w[hh * kRingWords + (fw & kRingMask)]);
-        if (want && h == hh) {
-          const uint8_t* src = in + 4u * fw;
-          if (a16) {
-            glds16(src + 16u * hl, slot - hh * 512u);
-            glds16(src + 512u + 16u * hl, slot + 512u - hh * 512u);
-          } else {
-#pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) glds4(src + 128u * q + 4u * hl, slot + 128u * q - hh * 128u);
-          }
-        }
-      }
+      for (uint32_t q = 0; q < 4; ++q) glds4(src + 256u * q + 4u * lane, slot + 256u * q);
     }
-    pend = want;
+    pend = true;
   };
-  refill_sync(true);
-  refill_sync(true);
+  refill_sync();
+  refill_sync();
   lds_fence();
-  // keeps words [w - 3, w + kAhead) of this half's stream resident
-  auto ensure = [&](uint32_t w, bool act) {
-    if (__any(act && fill_w < w + kAhead)) {
+  // keeps words [w - 3, w + kAhead) of the stream resident
+  auto ensure = [&](uint32_t w) {
+    if (fill_w < w + kAhead) {
       retire();
-      while (__any(act && fill_w < w + kAhead)) refill_sync(act && fill_w < w + kAhead);
+      while (fill_w < w + kAhead) refill_sync();
       lds_fence();
     }
   };
@@ -845,30 +809,29 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   };
 
   uint32_t last0 = 0, last1 = 0, P = 16 * cs;
-  if (b < p.nblocks && status == RPP_OK) {
+  if (status == RPP_OK) {
     if (16 * cs > lim) status = RPP_TRUNCATED_INPUT;
-    last0 = peek32(0) & 0xFFFFu;
-    last1 = cs > 1 ? peek32(16) & 0xFFFFu : 0u;
+    last0 = __builtin_amdgcn_readfirstlane(peek32(0) & 0xFFFFu);
+    last1 = cs > 1 ? __builtin_amdgcn_readfirstlane(peek32(16) & 0xFFFFu) : 0u;
   }
   uint32_t rawmask = 0;  // components of the current chunk stored raw
+  constexpr uint32_t kDump = kTileSamples;  // tile slot written by masked-off lanes
 
-  for (uint32_t s = 0;; ++s) {
+  for (uint32_t s = 0; s < nsb && status == RPP_OK; ++s) {
     RPP_TSTAMP(4);
-    bool active = s < nsb && status == RPP_OK;
-    if (!__any(active)) break;
     const uint32_t chunk = cs == 1 ? s : s >> 1;
     const uint32_t comp = s - chunk * cs;
     const uint32_t cbase = chunk * chunk_len;
-    const uint32_t clen = active ? min(N - cbase, chunk_len) : 0u;
+    const uint32_t clen = min(N - cbase, chunk_len);
     const uint32_t n = clen / cs;
-    ensure(P >> 5, active);
+    ensure(P >> 5);
     RPP_TSTAMP(5);
     // decode.h:60: 4-bit fs+1 header
-    if (active && P + 4 > lim) {
+    if (P + 4 > lim) {
       status = RPP_TRUNCATED_INPUT;
-      active = false;
+      break;
     }
-    // this lane's 64 bits from bit sb of the stream (its 48-bit segment of
+    // this lane's 64 bits from bit sb of the stream (its 24-bit segment of
     // the window and what follows it)
     uint32_t xl, xh;
     auto load_x = [&](uint32_t sb) {
@@ -877,233 +840,188 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       xl = __builtin_amdgcn_alignbit(a1, a0, o);
       xh = __builtin_amdgcn_alignbit(a2, a1, o);
     };
-    load_x(P + kSegBits * hl);
-    const uint32_t fsp1 = active ? half_first(xl) & 15u : 0u;
+    load_x(P + kSegBits * lane);
+    const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
     const uint32_t P4 = P + 4;
     uint32_t E = P4;
     RPP_STAT(6, 1);
     RPP_TSTAMP(7);
-    if (active && fsp1 == 0) {
+    if (fsp1 == 0) {
       // decode.h:79-80: every sample = write(last): zero deltas
-      for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = 0;
-    }
-    if (active && fsp1 == 15) {
+      for (uint32_t k = lane; k < n; k += kWave) tile[comp + cs * k] = 0;
+    } else if (fsp1 == 15) {
       // decode.h:72-77: raw stored values; last = read(last sample)
       if ((uint64_t)P4 + 16ull * n > lim) {
         status = RPP_TRUNCATED_INPUT;
-        active = false;
-      } else {
-        for (uint32_t k = hl; k < n; k += kHalf) tile[comp + cs * k] = (uint16_t)peek32(P4 + 16 * k);
-        const uint32_t lv = px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb);
-        if (comp) last1 = lv;
-        else last0 = lv;
-        rawmask |= 1u << comp;
-        E = P4 + 16 * n;
+        break;
       }
-    }
-    const bool rice = active && fsp1 != 0 && fsp1 != 15;
-    RPP_TSTAMP(9);
-    if (__any(rice)) {
+      for (uint32_t k = lane; k < n; k += kWave) tile[comp + cs * k] = (uint16_t)peek32(P4 + 16 * k);
+      const uint32_t lv =
+          __builtin_amdgcn_readfirstlane(px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb));
+      if (comp) last1 = lv;
+      else last0 = lv;
+      rawmask |= 1u << comp;
+      E = P4 + 16 * n;
+    } else {
       // decode.h:62-71: n Rice codes with fs = fsp1 - 1
-      const uint32_t fs = rice ? fsp1 - 1 : 0u;
-      const uint32_t k = fs + 1;
+      const uint32_t fs = fsp1 - 1;
+      const uint32_t k = fsp1;
       const uint32_t fmask = (1u << fs) - 1u;
-      const bool wide = fs >= 8;
       const uint4* tb = tab + 256u * fs;
       // q0: first bit of the window; s0: state at q0 (4 = skip the header);
       // s_in: end of the last code before the window; done: codes before it
       uint32_t q0 = P, s0 = 4, s_in = P4, done = 0;
-      bool go = rice;
-      while (__any(go)) {
+      for (;;) {
         RPP_STAT(0, 1);
-        if (__any(q0 != P)) {  // continuation window: the sub-block is longer than kWinBits
-          if (go && q0 != P && q0 >= lim) {  // the open unary search would read past the input
-            status = RPP_TRUNCATED_INPUT;
-            go = false;
-          }
-          ensure(q0 >> 5, go);
-          load_x(q0 + kSegBits * hl);
-        }
-        const uint32_t sb = q0 + kSegBits * hl;
+        const uint32_t sb = q0 + kSegBits * lane;
         // ---- 1. byte transfer functions ----
-        uint4 e[6];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) e[j] = tb[__builtin_amdgcn_ubfe(j < 4 ? xl : xh, 8 * (j & 3), 8)];
+        const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
+                    e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
         RPP_TSTAMP(10);
-        uint32_t tml = 0, tmh = 0, xexit = 0;
-        if (__any(go && !wide)) {
-          // ---- 2. segment map, scan along the half, entry state ----
-          const Map8 m01 = comp8(Map8{e[1].x, e[1].y}, Map8{e[0].x, e[0].y});
-          const Map8 m23 = comp8(Map8{e[3].x, e[3].y}, Map8{e[2].x, e[2].y});
-          const Map8 m45 = comp8(Map8{e[5].x, e[5].y}, Map8{e[4].x, e[4].y});
-          Map8 M = comp8(m45, comp8(m23, m01));
+        uint32_t tm, xexit;
+        if (fs < 8) {
+          // ---- 2. segment map, scan along the wave, entry state ----
+          Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
           M = scan_step8<kDppRowShr1>(M);
           M = scan_step8<kDppRowShr2>(M);
           M = scan_step8<kDppRowShr4>(M);
           M = scan_step8<kDppRowShr8>(M);
           M = scan_step8<kDppRowBcast15, 0xA>(M);
-          Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
-          if (hl == 0) X = Map8{kId0, kId1};
+          M = scan_step8<kDppRowBcast31, 0xC>(M);
+          const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
           // ---- 3. terminators of this lane's segment ----
           uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
-          uint32_t t[6];
-#pragma unroll
-          for (int j = 0; j < 6; ++j) {
-            t[j] = __builtin_amdgcn_perm(e[j].w, e[j].z, sel);
-            sel = __builtin_amdgcn_perm(e[j].y, e[j].x, sel) | kSelByte0;
-          }
-          if (!wide) {
-            tml = t[0] | (t[1] << 8) | (t[2] << 16) | (t[3] << 24);
-            tmh = t[4] | (t[5] << 8);
-            xexit = sel & 0xFFu;
-          }
-        }
-        if (__any(go && wide)) {
-          Map16 bm[6];
-#pragma unroll
-          for (int j = 0; j < 6; ++j) bm[j] = Map16{{e[j].x, e[j].y, kId0, kId1}};
-          Map16 M = comp16(bm[5], comp16(bm[4], comp16(comp16(bm[3], bm[2]), comp16(bm[1], bm[0]))));
+          const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+          sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+          const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+          sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+          const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+          xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
+          tm = t0 | (t1 << 8) | (t2 << 16);
+        } else {
+          const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
+          Map16 M = comp16(b2, comp16(b1, b0));
           M = scan_step16<kDppRowShr1>(M);
           M = scan_step16<kDppRowShr2>(M);
           M = scan_step16<kDppRowShr4>(M);
           M = scan_step16<kDppRowShr8>(M);
           M = scan_step16<kDppRowBcast15, 0xA>(M);
-          Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
-                   dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
-          if (hl == 0) X = Map16{{kId0, kId1, kId2, kId3}};
+          M = scan_step16<kDppRowBcast31, 0xC>(M);
+          const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
+                         dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
           uint32_t st = sel16(X, s0) & 0xFFu;
-          uint32_t t[6];
+          uint32_t t[3];
+          const uint4 ee[3] = {e0, e1, e2};
 #pragma unroll
-          for (int j = 0; j < 6; ++j) {
+          for (int j = 0; j < 3; ++j) {
             const uint32_t sel = st | kSelByte0;
             const bool skip = st >= 8;
-            t[j] = skip ? 0u : __builtin_amdgcn_perm(e[j].w, e[j].z, sel);
-            st = skip ? st - 8 : __builtin_amdgcn_perm(e[j].y, e[j].x, sel);
+            t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
+            st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
           }
-          if (wide) {
-            tml = t[0] | (t[1] << 8) | (t[2] << 16) | (t[3] << 24);
-            tmh = t[4] | (t[5] << 8);
-            xexit = st;
-          }
+          tm = t[0] | (t[1] << 8) | (t[2] << 16);
+          xexit = st;
         }
         RPP_TSTAMP(11);
         // ---- 4. code counts -> indices; the lane holding code n-1 ----
-        const uint32_t cnt = go ? __builtin_popcount(tml) + __builtin_popcount(tmh) : 0u;
-        const uint32_t incl = half_incl_sum(cnt);
+        const uint32_t cnt = __builtin_popcount(tm);
+        const uint32_t incl = wave_incl_sum(cnt);
         const uint32_t excl = incl - cnt;
         const uint32_t need = n - done;
-        const uint64_t finm = __ballot(go && incl >= need);
-        const uint32_t L0 = (uint32_t)finm ? (uint32_t)__builtin_ctz((uint32_t)finm) : 0u;
-        const uint32_t L1 = (uint32_t)(finm >> 32) ? (uint32_t)__builtin_ctz((uint32_t)(finm >> 32)) : 0u;
-        const bool fin = (h ? (uint32_t)(finm >> 32) : (uint32_t)finm) != 0;
+        const uint64_t finm = __ballot(incl >= need);
         // end of the last code of each lane -> start of the code open at a
         // lane's entry (its unary run may span earlier segments)
-        const uint32_t lastt = tmh ? 63u - (uint32_t)__builtin_clz(tmh) : 31u - (uint32_t)__builtin_clz(tml | 1u);
-        const uint32_t lend = cnt ? sb + lastt + k : 0u;
-        const uint32_t smax = half_incl_max(lend);
-        const uint32_t sleft = from_left(smax);
-        uint32_t prev = max(s_in, hl == 0 ? 0u : sleft);
+        const uint32_t lend = cnt ? sb + (31u - (uint32_t)__builtin_clz(tm)) + k : 0u;
+        const uint32_t smax = wave_incl_max(lend);
+        uint32_t prev = max(s_in, from_left(smax));
         // ---- 5. zig-zag deltas of this lane's codes (decode.h:66-69) ----
-        const uint32_t mine = go && need > excl ? min(cnt, need - excl) : 0u;
-        const uint32_t mmax = half_incl_max(mine);
-        const uint32_t trips = max(readlane(mmax, kHalf - 1), readlane(mmax, kWave - 1));
-        const uint64_t X64 = ((uint64_t)xh << 32) | xl;
-        uint64_t tm = ((uint64_t)tmh << 32) | tml;
-        uint16_t* tdst = tile + comp + cs * (done + excl);
+        const uint32_t mine = need > excl ? min(cnt, need - excl) : 0u;
+        const uint32_t trips = wave_last(wave_incl_max(mine));
+        const uint32_t rsel = need - 1 - excl;  // index of code n-1 within this lane
+        const uint32_t tbase = comp + cs * (done + excl);
         uint32_t ecand = 0;
         for (uint32_t j = 0; j < ((RPP_ABLATE & 2) ? 0u : trips); ++j) {
-          const bool act = j < mine;
-          const uint32_t t = (uint32_t)__builtin_ctzll(tm | (UINT64_C(1) << kSegBits));
+          const uint32_t t = ffbl(tm);
           tm &= tm - 1;
           const uint32_t tg = sb + t;
           const uint32_t q = tg - prev;
-          const uint32_t rem = (uint32_t)(X64 >> (t + 1)) & fmask;
+          const uint32_t rem = __builtin_amdgcn_alignbit(xh, xl, t + 1) & fmask;
           const uint32_t diff = (q << fs) | rem;
           const uint32_t delta = (diff >> 1) ^ (0u - (diff & 1u));
-          if (act) tdst[cs * j] = (uint16_t)delta;
+          tile[j < mine ? tbase + cs * j : kDump] = (uint16_t)delta;
           prev = tg + k;
-          ecand = act && excl + j + 1 == need ? prev : ecand;
+          ecand = j == rsel ? prev : ecand;
         }
         RPP_TSTAMP(12);
-        const uint32_t tot = half_last(incl);
-        const uint32_t ea = readlane(ecand, (int)L0), eb = readlane(ecand, (int)(L1 + kHalf));
-        if (go && fin) {
-          E = h ? eb : ea;
+        if (finm) {
+          E = readlane(ecand, (int)__builtin_ctzll(finm));
           if (E > lim) status = RPP_TRUNCATED_INPUT;
-          go = false;
+          break;
         }
-        const uint32_t wexit = half_last(xexit);
-        const uint32_t slast = half_last(smax);
-        if (go) {
-          done += tot;
-          s0 = wexit;
-          s_in = max(s_in, slast);
-          q0 += kWinBits;
+        // continuation window: the sub-block is longer than kWinBits
+        done += wave_last(incl);
+        s0 = wave_last(xexit);
+        s_in = max(s_in, wave_last(smax));
+        q0 += kWinBits;
+        if (q0 >= lim) {  // the open unary search would read past the input
+          status = RPP_TRUNCATED_INPUT;
+          break;
         }
+        ensure(q0 >> 5);
+        load_x(q0 + kSegBits * lane);
       }
+      if (status != RPP_OK) break;
     }
     RPP_TSTAMP(14);
-    if (active && status == RPP_OK) P = E;
+    P = E;
     retire();
     lds_fence();
     // ---- chunk complete: prefix sums (decode.h:68), pixel encode, store.
-    //      Each lane takes 4 consecutive tile entries (cs 1: 4 samples; cs 2:
-    //      2 interleaved (c0, c1) pairs, summed as packed u16). ----
-    if (!(RPP_ABLATE & 1) && __any(active && status == RPP_OK && comp == cs - 1)) {
-      const bool fl = active && status == RPP_OK && comp == cs - 1;
+    //      Each lane takes 2 consecutive tile entries (cs 1: 2 samples; cs 2:
+    //      one (c0, c1) pair, summed as packed u16). ----
+    if (!(RPP_ABLATE & 1) && comp == cs - 1) {
       const uint32_t rawm = cs == 1 ? ((rawmask & 1u) ? 0xFFFFFFFFu : 0u)
                                     : ((rawmask & 1u) ? 0x0000FFFFu : 0u) | ((rawmask & 2u) ? 0xFFFF0000u : 0u);
       uint32_t acc = cs == 1 ? last0 : (last0 | (last1 << 16));
       uint16_t* dst = out + cbase;
-      const bool vec = ((uintptr_t)dst & 7) == 0;
-      for (uint32_t r0 = 0; __any(fl && r0 < clen); r0 += 4 * kHalf) {
-        const uint32_t e = r0 + 4 * hl;  // first tile entry of this lane
-        const uint2 dv = fl && e < clen ? *reinterpret_cast<const uint2*>(&tile[e]) : make_uint2(0, 0);
-        const uint32_t nv = fl && e < clen ? min(clen - e, 4u) : 0u;
-        const uint32_t A = nv > 1 ? dv.x : (nv ? dv.x & 0xFFFFu : 0u);
-        const uint32_t B = nv > 3 ? dv.y : (nv > 2 ? dv.y & 0xFFFFu : 0u);
-        uint32_t oa, ob;
+      const bool vec = ((uintptr_t)dst & 3) == 0;
+      for (uint32_t r0 = 0; r0 < clen; r0 += 2 * kWave) {
+        const uint32_t e = r0 + 2 * lane;  // first tile entry of this lane
+        const uint32_t nv = e < clen ? min(clen - e, 2u) : 0u;
+        const uint32_t dv = nv ? *reinterpret_cast<const uint32_t*>(&tile[e]) : 0u;
+        const uint32_t A = nv > 1 ? dv : (dv & 0xFFFFu);
+        uint32_t o;
         if (cs == 1) {
-          const uint32_t s0 = A & 0xFFFFu, s1 = s0 + (A >> 16), s2 = s1 + (B & 0xFFFFu), s3 = s2 + (B >> 16);
-          const uint32_t inc = half_incl_sum(s3);
-          const uint32_t base = acc + inc - s3;
-          oa = ((base + s0) & 0xFFFFu) | ((base + s1) << 16);
-          ob = ((base + s2) & 0xFFFFu) | ((base + s3) << 16);
-          acc += half_last(inc);
+          const uint32_t s0 = A & 0xFFFFu, s1 = s0 + (A >> 16);
+          const uint32_t inc = wave_incl_sum(s1);
+          const uint32_t base = acc + inc - s1;
+          o = ((base + s0) & 0xFFFFu) | ((base + s1) << 16);
+          acc += wave_last(inc);
         } else {
-          const uint32_t t = pk_add(A, B);
-          const uint32_t inc = half_incl_sum_pk(t);
-          const uint32_t base = pk_add(acc, inc);
-          const uint32_t bx = as_u32(as_us2(base) - as_us2(t));
-          oa = pk_add(bx, A);
-          ob = pk_add(bx, t);
-          acc = pk_add(acc, half_last(inc));
+          const uint32_t inc = wave_incl_sum_pk(A);
+          o = pk_add(acc, inc);
+          acc = pk_add(acc, wave_last(inc));
         }
-        oa = (px_write2(oa, be, ulsb) & ~rawm) | (A & rawm);
-        ob = (px_write2(ob, be, ulsb) & ~rawm) | (B & rawm);
-        if (nv == 4 && vec) {
-          *reinterpret_cast<uint2*>(dst + e) = make_uint2(oa, ob);
+        o = (px_write2(o, be, ulsb) & ~rawm) | (A & rawm);
+        if (nv == 2 && vec) {
+          *reinterpret_cast<uint32_t*>(dst + e) = o;
         } else if (nv) {
-          dst[e] = (uint16_t)oa;
-          if (nv > 1) dst[e + 1] = (uint16_t)(oa >> 16);
-          if (nv > 2) dst[e + 2] = (uint16_t)ob;
-          if (nv > 3) dst[e + 3] = (uint16_t)(ob >> 16);
+          dst[e] = (uint16_t)o;
+          if (nv > 1) dst[e + 1] = (uint16_t)(o >> 16);
         }
       }
-      if (fl) {
-        if (!(rawmask & 1u)) last0 = acc & 0xFFFFu;
-        if (cs > 1 && !(rawmask & 2u)) last1 = acc >> 16;
-        rawmask = 0;
-      }
+      if (!(rawmask & 1u)) last0 = acc & 0xFFFFu;
+      if (cs > 1 && !(rawmask & 2u)) last1 = acc >> 16;
+      rawmask = 0;
       lds_fence();
     }
-    // request the next chunk once the look-ahead drops below 510 words (it
+    // request the next chunk once the look-ahead drops below 766 words (it
     // overwrites words [fill_w - 1024, fill_w - 768), all below P - 256)
-    request(active && status == RPP_OK && !pend && fill_w <= (P >> 5) + 510);
+    if (!pend && fill_w <= (P >> 5) + 766) request();
     RPP_TSTAMP(15);
   }
   retire();
-  if (b < p.nblocks && hl == 0) p.status[b] = status;
+  if (lane == 0) p.status[b] = status;
 #ifdef RPP_STATS
   if (lane == 0)
     for (int i = 0; i < 16; ++i) atomicAdd(&g_rpp_stats[i], (unsigned long long)stat_acc[i]);
@@ -1173,10 +1091,9 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   if (!d_in || !d_in_offsets || !d_in_bytes || !d_out || !d_out_offsets || !d_n_samples || !d_status)
     return RPP_INVALID_ARGUMENT;
   if (cfg->component_stream_count * cfg->block_size > (uint32_t)kTileSamples) return RPP_UNSUPPORTED_CONFIG;
-  // two streams per wave; up to kDecMaxWaves waves share one copy of the
+  // one stream per wave; up to kDecMaxWaves waves share one copy of the
   // transfer tables, fewer when the batch cannot fill the 256 CUs anyway
-  const uint32_t nwaves = (nblocks + 1) / 2;
-  const uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nwaves + 255) / 256));
+  const uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
   static std::once_flag attr_once;
   static hipError_t attr_err = hipSuccess;
@@ -1189,7 +1106,7 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   DecParams p{d_in, d_in_offsets, d_in_bytes, d_out, d_out_offsets, d_n_samples, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count, W};
-  hipLaunchKernelGGL(rpp_decode_kernel, dim3((nwaves + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(rpp_decode_kernel, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 

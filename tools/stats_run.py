@@ -26,8 +26,9 @@ pipe.decode()
 torch.cuda.synchronize()
 pipe.check(x)
 L.rpp_stats_fetch(st.ctypes.data, 1)
-names = ["windows", "verify_rounds", "slow_subblocks", "-", "t_looptop", "t_ensure",
-         "subblocks", "t_header", "-", "t_modes", "t_ensure+load", "t_chains", "t_verify", "t_extract", "t_end+slow", "t_flush"]
+names = ["windows", "-", "-", "-", "t_looptop", "t_ensure",
+         "subblocks", "t_load+header", "-", "t_zero/raw", "t_lookup", "t_maps+terms", "t_count+extract", "-",
+         "t_winend", "t_flush+request"]
 sb = float(st[6])
 for i, nm in enumerate(names):
     print(f"{nm:20s} total={int(st[i]):12d}  per_subblock={st[i] / sb:8.3f}")
