@@ -33,8 +33,8 @@
 #include "ricepp_amd.h"
 
 // Diagnostic builds only: -DRPP_ABLATE=<mask> removes decode phases to time
-// them (outputs are then wrong): 1 flush, 2 extraction, 4 verify rounds,
-// 8 look-back guess.
+// them (outputs are then wrong): 1 flush, 2 extraction, 4 async ring refill,
+// 8 output stores.
 #ifndef RPP_ABLATE
 #define RPP_ABLATE 0
 #endif
@@ -59,8 +59,6 @@ __device__ unsigned long long g_rpp_stats[16];
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWinWords = 512;   // encode LDS output window (2 KiB)
-constexpr int kTileSamples = 1024;  // decode LDS chunk tile (cs*bs <= 1024)
 
 // ---------------------------------------------------------------------------
 // pixel traits (ricepp/ricepp_cpuspecific_traits.h:63-75)
@@ -593,8 +591,9 @@ constexpr uint32_t kRingMask = kRingWords - 1;
 constexpr uint32_t kChunkWords = 4 * kWave;      // refill unit: 16 B per lane
 constexpr uint32_t kAhead = 288;                 // words kept resident ahead of the read position
 constexpr uint32_t kDecMaxWaves = 16;            // waves per workgroup (one table copy each)
-constexpr uint32_t kTileSlots = kTileSamples + 8;  // + a dump slot for masked-off lanes
-constexpr uint32_t kWaveLdsWords = kRingWords + kTileSlots / 2;
+constexpr uint32_t kListDump = 512;            // list slot written by masked-off lanes
+constexpr uint32_t kListWords = kListDump + 8;  // terminator positions of one sub-block (bs <= 512)
+constexpr uint32_t kWaveLdsWords = kRingWords + kListWords;
 constexpr uint32_t kTabBytes = kMapEntries * 16;
 
 __device__ __forceinline__ uint32_t wave_last(uint32_t v) { return readlane(v, kWave - 1); }
@@ -703,6 +702,7 @@ __device__ __forceinline__ uint32_t stream_word(const uint8_t* in, uint32_t nbyt
   return v;
 }
 
+template <uint32_t CS>
 __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
   // ---- the transfer tables, one copy per workgroup ----
@@ -715,8 +715,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint32_t lane = lane_id();
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + kMapEntries) + wv * kWaveLdsWords;
-  uint16_t* tile = reinterpret_cast<uint16_t*>(ring + kRingWords);
-  const uint32_t bs = p.bs, cs = p.cs, be = p.be, ulsb = p.ulsb;
+  uint32_t* list = ring + kRingWords;  // terminator positions of the current sub-block
+  const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
   const uint32_t b = blockIdx.x * p.waves + wv;
   if (b >= p.nblocks) return;  // no barrier below this point
 #ifdef RPP_STATS
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
     const uint64_t n64 = p.n_samples[b];
     const uint64_t ioff = p.in_off[b];
     const uint64_t nb64 = p.in_bytes[b];
-    if (n64 % cs != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ioff & 3u) || nb64 >= (UINT64_C(1) << 29)) {
+    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ioff & 3u) || nb64 >= (UINT64_C(1) << 29)) {
       status = RPP_INVALID_ARGUMENT;
     } else {
       N = (uint32_t)n64;
@@ -747,17 +747,16 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   // last readable bit + 1: the reader pulls whole 8-byte packets
   // (bitstream_reader.h:149-183), so it only throws past this point.
   const uint32_t lim = 64u * ((nbytes + 7u) >> 3);
-  const uint32_t chunk_len = cs * bs;
-  const uint32_t nsb = status == RPP_OK ? ((N + chunk_len - 1) / chunk_len) * cs : 0u;
+  const uint32_t chunk_len = CS * bs;
+  const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
 
   // ---- LDS ring of the stream's words: words [fill_w - kRingWords, fill_w)
   //      are resident.  Steady state: at the end of an iteration, a chunk of
   //      256 words lying wholly inside the input is requested by
   //      global_load_lds (no registers, nothing for the compiler to wait on);
-  //      it is retired (vmcnt(0), by then long complete together with that
-  //      iteration's output stores) before the next flush, and only then
-  //      counted resident.  ensure() is the synchronous path (start-up, the
-  //      zero-padded tail, long sub-blocks). ----
+  //      it is retired (vmcnt(0), by then long complete) a few iterations
+  //      later, and only then counted resident.  ensure() is the synchronous
+  //      path (start-up, the zero-padded tail, long sub-blocks). ----
   uint32_t fill_w = 0;
   bool pend = false;  // a requested chunk is in flight
   auto retire = [&]() {
@@ -795,7 +794,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   refill_sync();
   refill_sync();
   lds_fence();
-  // keeps words [w - 3, w + kAhead) of the stream resident
+  // keeps words [w, w + kAhead) of the stream resident
   auto ensure = [&](uint32_t w) {
     if (fill_w < w + kAhead) {
       retire();
@@ -808,217 +807,203 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
     return __builtin_amdgcn_alignbit(word((pos >> 5) + 1), word(pos >> 5), pos & 31u);
   };
 
-  uint32_t last0 = 0, last1 = 0, P = 16 * cs;
+  // codec.h:69-74,81-86: the 16-bit initial value of each component
+  uint32_t last[CS];
+  uint32_t P = 16 * CS;
   if (status == RPP_OK) {
-    if (16 * cs > lim) status = RPP_TRUNCATED_INPUT;
-    last0 = __builtin_amdgcn_readfirstlane(peek32(0) & 0xFFFFu);
-    last1 = cs > 1 ? __builtin_amdgcn_readfirstlane(peek32(16) & 0xFFFFu) : 0u;
+    if (16 * CS > lim) status = RPP_TRUNCATED_INPUT;
+#pragma unroll
+    for (uint32_t c = 0; c < CS; ++c) last[c] = __builtin_amdgcn_readfirstlane(peek32(16 * c) & 0xFFFFu);
   }
-  uint32_t rawmask = 0;  // components of the current chunk stored raw
-  constexpr uint32_t kDump = kTileSamples;  // tile slot written by masked-off lanes
 
-  for (uint32_t s = 0; s < nsb && status == RPP_OK; ++s) {
-    RPP_TSTAMP(4);
-    const uint32_t chunk = cs == 1 ? s : s >> 1;
-    const uint32_t comp = s - chunk * cs;
+  for (uint32_t chunk = 0; chunk < nchunks && status == RPP_OK; ++chunk) {
     const uint32_t cbase = chunk * chunk_len;
-    const uint32_t clen = min(N - cbase, chunk_len);
-    const uint32_t n = clen / cs;
-    ensure(P >> 5);
-    RPP_TSTAMP(5);
-    // decode.h:60: 4-bit fs+1 header
-    if (P + 4 > lim) {
-      status = RPP_TRUNCATED_INPUT;
-      break;
-    }
-    // this lane's 64 bits from bit sb of the stream (its 24-bit segment of
-    // the window and what follows it)
-    uint32_t xl, xh;
-    auto load_x = [&](uint32_t sb) {
-      const uint32_t wb = sb >> 5, o = sb & 31u;
-      const uint32_t a0 = word(wb), a1 = word(wb + 1), a2 = word(wb + 2);
-      xl = __builtin_amdgcn_alignbit(a1, a0, o);
-      xh = __builtin_amdgcn_alignbit(a2, a1, o);
-    };
-    load_x(P + kSegBits * lane);
-    const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
-    const uint32_t P4 = P + 4;
-    uint32_t E = P4;
-    RPP_STAT(6, 1);
-    RPP_TSTAMP(7);
-    if (fsp1 == 0) {
-      // decode.h:79-80: every sample = write(last): zero deltas
-      for (uint32_t k = lane; k < n; k += kWave) tile[comp + cs * k] = 0;
-    } else if (fsp1 == 15) {
-      // decode.h:72-77: raw stored values; last = read(last sample)
-      if ((uint64_t)P4 + 16ull * n > lim) {
+    const uint32_t n = min(N - cbase, chunk_len) / CS;  // samples per component sub-block
+#pragma unroll
+    for (uint32_t comp = 0; comp < CS; ++comp) {
+      RPP_TSTAMP(4);
+      ensure(P >> 5);
+      // decode.h:60: 4-bit fs+1 header
+      if (P + 4 > lim) {
         status = RPP_TRUNCATED_INPUT;
         break;
       }
-      for (uint32_t k = lane; k < n; k += kWave) tile[comp + cs * k] = (uint16_t)peek32(P4 + 16 * k);
-      const uint32_t lv =
-          __builtin_amdgcn_readfirstlane(px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb));
-      if (comp) last1 = lv;
-      else last0 = lv;
-      rawmask |= 1u << comp;
-      E = P4 + 16 * n;
-    } else {
-      // decode.h:62-71: n Rice codes with fs = fsp1 - 1
-      const uint32_t fs = fsp1 - 1;
-      const uint32_t k = fsp1;
-      const uint32_t fmask = (1u << fs) - 1u;
-      const uint4* tb = tab + 256u * fs;
-      // q0: first bit of the window; s0: state at q0 (4 = skip the header);
-      // s_in: end of the last code before the window; done: codes before it
-      uint32_t q0 = P, s0 = 4, s_in = P4, done = 0;
-      for (;;) {
-        RPP_STAT(0, 1);
-        const uint32_t sb = q0 + kSegBits * lane;
-        // ---- 1. byte transfer functions ----
-        const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
-                    e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
-        RPP_TSTAMP(10);
-        uint32_t tm, xexit;
-        if (fs < 8) {
-          // ---- 2. segment map, scan along the wave, entry state ----
-          Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
-          M = scan_step8<kDppRowShr1>(M);
-          M = scan_step8<kDppRowShr2>(M);
-          M = scan_step8<kDppRowShr4>(M);
-          M = scan_step8<kDppRowShr8>(M);
-          M = scan_step8<kDppRowBcast15, 0xA>(M);
-          M = scan_step8<kDppRowBcast31, 0xC>(M);
-          const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
-          // ---- 3. terminators of this lane's segment ----
-          uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
-          const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-          sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
-          const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
-          sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
-          const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
-          xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
-          tm = t0 | (t1 << 8) | (t2 << 16);
+      // this lane's 64 bits from bit sb of the stream (its 24-bit segment of
+      // the window and what follows it)
+      uint32_t xl, xh;
+      auto load_x = [&](uint32_t sb) {
+        const uint32_t wb = sb >> 5, o = sb & 31u;
+        const uint32_t a0 = word(wb), a1 = word(wb + 1), a2 = word(wb + 2);
+        xl = __builtin_amdgcn_alignbit(a1, a0, o);
+        xh = __builtin_amdgcn_alignbit(a2, a1, o);
+      };
+      load_x(P + kSegBits * lane);
+      const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
+      const uint32_t P4 = P + 4;
+      uint16_t* dst = out + cbase + comp;  // sample i of this sub-block at dst[CS * i]
+      // stores samples i0, i0 + 1 (i0 even) of the sub-block, those below m
+      auto put2 = [&](uint32_t i0, uint32_t v0, uint32_t v1, uint32_t m) {
+        if (CS == 1 && i0 + 1 < m && (((uintptr_t)(dst + i0)) & 3u) == 0) {
+          *reinterpret_cast<uint32_t*>(dst + i0) = (v0 & 0xFFFFu) | (v1 << 16);
         } else {
-          const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
-          Map16 M = comp16(b2, comp16(b1, b0));
-          M = scan_step16<kDppRowShr1>(M);
-          M = scan_step16<kDppRowShr2>(M);
-          M = scan_step16<kDppRowShr4>(M);
-          M = scan_step16<kDppRowShr8>(M);
-          M = scan_step16<kDppRowBcast15, 0xA>(M);
-          M = scan_step16<kDppRowBcast31, 0xC>(M);
-          const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
-                         dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
-          uint32_t st = sel16(X, s0) & 0xFFu;
-          uint32_t t[3];
-          const uint4 ee[3] = {e0, e1, e2};
-#pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const uint32_t sel = st | kSelByte0;
-            const bool skip = st >= 8;
-            t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
-            st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
-          }
-          tm = t[0] | (t[1] << 8) | (t[2] << 16);
-          xexit = st;
+          if (i0 < m) dst[CS * i0] = (uint16_t)v0;
+          if (i0 + 1 < m) dst[CS * (i0 + 1)] = (uint16_t)v1;
         }
-        RPP_TSTAMP(11);
-        // ---- 4. code counts -> indices; the lane holding code n-1 ----
-        const uint32_t cnt = __builtin_popcount(tm);
-        const uint32_t incl = wave_incl_sum(cnt);
-        const uint32_t excl = incl - cnt;
-        const uint32_t need = n - done;
-        const uint64_t finm = __ballot(incl >= need);
-        // end of the last code of each lane -> start of the code open at a
-        // lane's entry (its unary run may span earlier segments)
-        const uint32_t lend = cnt ? sb + (31u - (uint32_t)__builtin_clz(tm)) + k : 0u;
-        const uint32_t smax = wave_incl_max(lend);
-        uint32_t prev = max(s_in, from_left(smax));
-        // ---- 5. zig-zag deltas of this lane's codes (decode.h:66-69) ----
-        const uint32_t mine = need > excl ? min(cnt, need - excl) : 0u;
-        const uint32_t trips = wave_last(wave_incl_max(mine));
-        const uint32_t rsel = need - 1 - excl;  // index of code n-1 within this lane
-        const uint32_t tbase = comp + cs * (done + excl);
-        uint32_t ecand = 0;
-        for (uint32_t j = 0; j < ((RPP_ABLATE & 2) ? 0u : trips); ++j) {
-          const uint32_t t = ffbl(tm);
-          tm &= tm - 1;
-          const uint32_t tg = sb + t;
-          const uint32_t q = tg - prev;
-          const uint32_t rem = __builtin_amdgcn_alignbit(xh, xl, t + 1) & fmask;
-          const uint32_t diff = (q << fs) | rem;
-          const uint32_t delta = (diff >> 1) ^ (0u - (diff & 1u));
-          tile[j < mine ? tbase + cs * j : kDump] = (uint16_t)delta;
-          prev = tg + k;
-          ecand = j == rsel ? prev : ecand;
-        }
-        RPP_TSTAMP(12);
-        if (finm) {
-          E = readlane(ecand, (int)__builtin_ctzll(finm));
-          if (E > lim) status = RPP_TRUNCATED_INPUT;
-          break;
-        }
-        // continuation window: the sub-block is longer than kWinBits
-        done += wave_last(incl);
-        s0 = wave_last(xexit);
-        s_in = max(s_in, wave_last(smax));
-        q0 += kWinBits;
-        if (q0 >= lim) {  // the open unary search would read past the input
+      };
+      RPP_STAT(6, 1);
+      RPP_TSTAMP(5);
+      if (fsp1 == 0) {
+        // decode.h:79-80: every sample = write(last)
+        const uint32_t v = px_write(last[comp], be, ulsb);
+        for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) put2(i0, v, v, n);
+        P = P4;
+      } else if (fsp1 == 15) {
+        // decode.h:72-77: raw stored values; last = read(last sample)
+        if ((uint64_t)P4 + 16ull * n > lim) {
           status = RPP_TRUNCATED_INPUT;
           break;
         }
-        ensure(q0 >> 5);
-        load_x(q0 + kSegBits * lane);
-      }
-      if (status != RPP_OK) break;
-    }
-    RPP_TSTAMP(14);
-    P = E;
-    retire();
-    lds_fence();
-    // ---- chunk complete: prefix sums (decode.h:68), pixel encode, store.
-    //      Each lane takes 2 consecutive tile entries (cs 1: 2 samples; cs 2:
-    //      one (c0, c1) pair, summed as packed u16). ----
-    if (!(RPP_ABLATE & 1) && comp == cs - 1) {
-      const uint32_t rawm = cs == 1 ? ((rawmask & 1u) ? 0xFFFFFFFFu : 0u)
-                                    : ((rawmask & 1u) ? 0x0000FFFFu : 0u) | ((rawmask & 2u) ? 0xFFFF0000u : 0u);
-      uint32_t acc = cs == 1 ? last0 : (last0 | (last1 << 16));
-      uint16_t* dst = out + cbase;
-      const bool vec = ((uintptr_t)dst & 3) == 0;
-      for (uint32_t r0 = 0; r0 < clen; r0 += 2 * kWave) {
-        const uint32_t e = r0 + 2 * lane;  // first tile entry of this lane
-        const uint32_t nv = e < clen ? min(clen - e, 2u) : 0u;
-        const uint32_t dv = nv ? *reinterpret_cast<const uint32_t*>(&tile[e]) : 0u;
-        const uint32_t A = nv > 1 ? dv : (dv & 0xFFFFu);
-        uint32_t o;
-        if (cs == 1) {
-          const uint32_t s0 = A & 0xFFFFu, s1 = s0 + (A >> 16);
-          const uint32_t inc = wave_incl_sum(s1);
-          const uint32_t base = acc + inc - s1;
-          o = ((base + s0) & 0xFFFFu) | ((base + s1) << 16);
-          acc += wave_last(inc);
-        } else {
-          const uint32_t inc = wave_incl_sum_pk(A);
-          o = pk_add(acc, inc);
-          acc = pk_add(acc, wave_last(inc));
+        for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) {
+          const uint32_t w = peek32(P4 + 16 * i0);
+          put2(i0, w, w >> 16, n);
         }
-        o = (px_write2(o, be, ulsb) & ~rawm) | (A & rawm);
-        if (nv == 2 && vec) {
-          *reinterpret_cast<uint32_t*>(dst + e) = o;
-        } else if (nv) {
-          dst[e] = (uint16_t)o;
-          if (nv > 1) dst[e + 1] = (uint16_t)(o >> 16);
+        last[comp] = __builtin_amdgcn_readfirstlane(px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb));
+        P = P4 + 16 * n;
+      } else {
+        // decode.h:62-71: n Rice codes with fs = fsp1 - 1
+        const uint32_t fs = fsp1 - 1;
+        const uint32_t k = fsp1;
+        const uint32_t fmask = (1u << fs) - 1u;
+        const uint4* tb = tab + 256u * fs;
+        // ---- codes [xdone, m) -> zig-zag deltas (decode.h:66-69) -> values,
+        //      2 per lane (m even or m == n) ----
+        uint32_t acc = last[comp], start = P4, xdone = 0;  // start: first bit of code xdone's unary run
+        auto extract = [&](uint32_t m) {
+          for (; xdone < m; xdone += 2 * kWave) {
+            const uint32_t i0 = xdone + 2 * lane;
+            const uint2 tt = i0 < m ? *reinterpret_cast<const uint2*>(&list[i0]) : make_uint2(0, 0);
+            const uint32_t t0 = tt.x, t1 = i0 + 1 < m ? tt.y : t0;
+            const uint32_t lft = from_left(t1 + k);  // end of code i0 - 1
+            const uint32_t st0 = lane == 0 ? start : lft;
+            const uint32_t r0 = peek32(t0 + 1) & fmask, r1 = peek32(t1 + 1) & fmask;
+            const uint32_t df0 = ((t0 - st0) << fs) | r0, df1 = ((t1 - t0 - k) << fs) | r1;
+            const uint32_t d0 = i0 < m ? (df0 >> 1) ^ (0u - (df0 & 1u)) : 0u;
+            const uint32_t d1 = i0 + 1 < m ? (df1 >> 1) ^ (0u - (df1 & 1u)) : 0u;
+            const uint32_t s1 = d0 + d1;
+            const uint32_t inc = wave_incl_sum(s1);
+            const uint32_t base = acc + inc - s1;
+            put2(i0, px_write(base + d0, be, ulsb), px_write(base + s1, be, ulsb), m);
+            acc += wave_last(inc);
+            start = wave_last(t1) + k;
+          }
+          xdone = m;
+          start = __builtin_amdgcn_readfirstlane(list[m - 1]) + k;
+        };
+        // ---- parse: the terminator position of code i -> list[i] ----
+        // q0: first bit of the window; s0: state at q0 (4 = skip the header);
+        // done: codes before the window
+        uint32_t q0 = P, s0 = 4, done = 0;
+        for (;;) {
+          RPP_STAT(0, 1);
+          const uint32_t sb = q0 + kSegBits * lane;
+          // 1. byte transfer functions
+          const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
+                      e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+          RPP_TSTAMP(10);
+          uint32_t tm, xexit;
+          if (fs < 8) {
+            // 2. segment map, scan along the wave, entry state
+            Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
+            M = scan_step8<kDppRowShr1>(M);
+            M = scan_step8<kDppRowShr2>(M);
+            M = scan_step8<kDppRowShr4>(M);
+            M = scan_step8<kDppRowShr8>(M);
+            M = scan_step8<kDppRowBcast15, 0xA>(M);
+            M = scan_step8<kDppRowBcast31, 0xC>(M);
+            const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
+            // 3. terminators of this lane's segment
+            uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
+            const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+            sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+            const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+            sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+            const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+            xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
+            tm = t0 | (t1 << 8) | (t2 << 16);
+          } else {
+            const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
+            Map16 M = comp16(b2, comp16(b1, b0));
+            M = scan_step16<kDppRowShr1>(M);
+            M = scan_step16<kDppRowShr2>(M);
+            M = scan_step16<kDppRowShr4>(M);
+            M = scan_step16<kDppRowShr8>(M);
+            M = scan_step16<kDppRowBcast15, 0xA>(M);
+            M = scan_step16<kDppRowBcast31, 0xC>(M);
+            const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
+                           dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
+            uint32_t st = sel16(X, s0) & 0xFFu;
+            uint32_t t[3];
+            const uint4 ee[3] = {e0, e1, e2};
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const uint32_t sel = st | kSelByte0;
+              const bool skip = st >= 8;
+              t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
+              st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
+            }
+            tm = t[0] | (t[1] << 8) | (t[2] << 16);
+            xexit = st;
+          }
+          RPP_TSTAMP(11);
+          // 4. code indices: terminators -> list[done + excl + j]
+          const uint32_t cnt = __builtin_popcount(tm);
+          const uint32_t incl = wave_incl_sum(cnt);
+          const uint32_t excl = incl - cnt;
+          const uint32_t need = n - done;
+          const uint32_t mine = need > excl ? min(cnt, need - excl) : 0u;
+          uint32_t* lp = list + done + excl;
+          for (uint32_t j = 0; __any(j < mine); ++j) {
+            const uint32_t t = ffbl(tm);
+            tm &= tm - 1;
+            *(j < mine ? lp + j : list + kListDump) = sb + t;
+          }
+          RPP_TSTAMP(12);
+          if (__ballot(incl >= need)) break;
+          // continuation window: the sub-block is longer than kWinBits;
+          // turn the codes found so far into samples first (the ring only
+          // keeps the recent windows resident)
+          done += wave_last(incl);
+          if ((done & ~1u) > xdone) {
+            lds_fence();
+            extract(done & ~1u);
+          }
+          s0 = wave_last(xexit);
+          q0 += kWinBits;
+          if (q0 >= lim) {  // the open unary search would read past the input
+            status = RPP_TRUNCATED_INPUT;
+            break;
+          }
+          ensure(q0 >> 5);
+          load_x(q0 + kSegBits * lane);
+        }
+        if (status != RPP_OK) break;
+        lds_fence();
+        extract(n);
+        last[comp] = acc & 0xFFFFu;
+        // the next sub-block starts after code n-1's remainder
+        P = __builtin_amdgcn_readfirstlane(list[n - 1]) + k;
+        if (P > lim) {
+          status = RPP_TRUNCATED_INPUT;
+          break;
         }
       }
-      if (!(rawmask & 1u)) last0 = acc & 0xFFFFu;
-      if (cs > 1 && !(rawmask & 2u)) last1 = acc >> 16;
-      rawmask = 0;
-      lds_fence();
+      RPP_TSTAMP(14);
+      // request the next chunk once the look-ahead drops below 766 words (it
+      // overwrites words [fill_w - 1024, fill_w - 768), all below P >> 5)
+      if (pend && fill_w < (P >> 5) + kAhead + 128) retire();
+      if (!(RPP_ABLATE & 4) && !pend && fill_w <= (P >> 5) + 766) request();
+      RPP_TSTAMP(15);
     }
-    // request the next chunk once the look-ahead drops below 766 words (it
-    // overwrites words [fill_w - 1024, fill_w - 768), all below P - 256)
-    if (!pend && fill_w <= (P >> 5) + 766) request();
-    RPP_TSTAMP(15);
   }
   retire();
   if (lane == 0) p.status[b] = status;
@@ -1090,7 +1075,6 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   if (nblocks == 0) return RPP_OK;
   if (!d_in || !d_in_offsets || !d_in_bytes || !d_out || !d_out_offsets || !d_n_samples || !d_status)
     return RPP_INVALID_ARGUMENT;
-  if (cfg->component_stream_count * cfg->block_size > (uint32_t)kTileSamples) return RPP_UNSUPPORTED_CONFIG;
   // one stream per wave; up to kDecMaxWaves waves share one copy of the
   // transfer tables, fewer when the batch cannot fill the 256 CUs anyway
   const uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
@@ -1098,15 +1082,21 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   static std::once_flag attr_once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(attr_once, [] {
-    attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&rpp_decode_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)(kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4));
+    const int mx = (int)(kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4);
+    attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&rpp_decode_kernel<1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    if (attr_err == hipSuccess)
+      attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&rpp_decode_kernel<2>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   });
   if (attr_err != hipSuccess) return RPP_HIP_ERROR;
   DecParams p{d_in, d_in_offsets, d_in_bytes, d_out, d_out_offsets, d_n_samples, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count, W};
-  hipLaunchKernelGGL(rpp_decode_kernel, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
+  if (cfg->component_stream_count == 1)
+    hipLaunchKernelGGL(rpp_decode_kernel<1>, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(rpp_decode_kernel<2>, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
