@@ -591,9 +591,10 @@ constexpr uint32_t kRingMask = kRingWords - 1;
 constexpr uint32_t kChunkWords = 4 * kWave;      // refill unit: 16 B per lane
 constexpr uint32_t kAhead = 288;                 // words kept resident ahead of the read position
 constexpr uint32_t kDecMaxWaves = 16;            // waves per workgroup (one table copy each)
+constexpr uint32_t kRingPad = 64;               // ring words 0..63 mirrored after the ring end
 constexpr uint32_t kListDump = 512;            // list slot written by masked-off lanes
 constexpr uint32_t kListWords = kListDump + 8;  // terminator positions of one sub-block (bs <= 512)
-constexpr uint32_t kWaveLdsWords = kRingWords + kListWords;
+constexpr uint32_t kWaveLdsWords = kRingWords + kRingPad + kListWords;
 constexpr uint32_t kTabBytes = kMapEntries * 16;
 
 __device__ __forceinline__ uint32_t wave_last(uint32_t v) { return readlane(v, kWave - 1); }
@@ -611,10 +612,11 @@ __device__ __forceinline__ uint32_t wave_incl_sum_pk(uint32_t v) {
   return v;
 }
 
-// pixel write (ricepp_cpuspecific_traits.h:69-73) of two packed samples
-__device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t be, uint32_t ulsb) {
+// pixel write (ricepp_cpuspecific_traits.h:69-73) of two packed samples;
+// sel = v_perm selector that byte-swaps each half (big endian) or not
+__device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t sel, uint32_t ulsb) {
   v = as_u32(as_us2(v) << (us2)(unsigned short)ulsb);
-  return be ? __builtin_amdgcn_perm(v, v, 0x02030001u) : v;
+  return __builtin_amdgcn_perm(v, v, sel);
 }
 
 // ---- state maps ----
@@ -715,8 +717,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint32_t lane = lane_id();
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + kMapEntries) + wv * kWaveLdsWords;
-  uint32_t* list = ring + kRingWords;  // terminator positions of the current sub-block
+  uint32_t* list = ring + kRingWords + kRingPad;  // terminator positions of the current sub-block
   const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
+  const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
   const uint32_t b = blockIdx.x * p.waves + wv;
   if (b >= p.nblocks) return;  // no barrier below this point
 #ifdef RPP_STATS
@@ -776,6 +779,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
                      stream_word(in, nbytes, w + 3));
     }
     *reinterpret_cast<uint4*>(&ring[w & kRingMask]) = v;
+    if ((w & kRingMask) < kRingPad) *reinterpret_cast<uint4*>(&ring[kRingWords + (w & kRingMask)]) = v;
     fill_w += kChunkWords;
   };
   auto request = [&]() {  // asynchronous 256-word chunk (only wholly inside the input)
@@ -789,6 +793,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q) glds4(src + 256u * q + 4u * lane, slot + 256u * q);
     }
+    if ((fill_w & kRingMask) == 0)  // the mirror of words 0..63
+      glds4(src + 4u * lane, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[kRingWords]));
     pend = true;
   };
   refill_sync();
@@ -802,9 +808,11 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       lds_fence();
     }
   };
-  auto word = [&](uint32_t w) -> uint32_t { return ring[w & kRingMask]; };
+  // words w, w + 1, w + 2 are contiguous in LDS thanks to the mirror
+  auto wptr = [&](uint32_t w) -> const uint32_t* { return ring + (w & kRingMask); };
   auto peek32 = [&](uint32_t pos) -> uint32_t {
-    return __builtin_amdgcn_alignbit(word((pos >> 5) + 1), word(pos >> 5), pos & 31u);
+    const uint32_t* q = wptr(pos >> 5);
+    return __builtin_amdgcn_alignbit(q[1], q[0], pos & 31u);
   };
 
   // codec.h:69-74,81-86: the 16-bit initial value of each component
@@ -832,8 +840,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // the window and what follows it)
       uint32_t xl, xh;
       auto load_x = [&](uint32_t sb) {
-        const uint32_t wb = sb >> 5, o = sb & 31u;
-        const uint32_t a0 = word(wb), a1 = word(wb + 1), a2 = word(wb + 2);
+        const uint32_t* q = wptr(sb >> 5);
+        const uint32_t o = sb & 31u;
+        const uint32_t a0 = q[0], a1 = q[1], a2 = q[2];
         xl = __builtin_amdgcn_alignbit(a1, a0, o);
         xh = __builtin_amdgcn_alignbit(a2, a1, o);
       };
@@ -841,21 +850,23 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
       const uint32_t P4 = P + 4;
       uint16_t* dst = out + cbase + comp;  // sample i of this sub-block at dst[CS * i]
-      // stores samples i0, i0 + 1 (i0 even) of the sub-block, those below m
-      auto put2 = [&](uint32_t i0, uint32_t v0, uint32_t v1, uint32_t m) {
-        if (CS == 1 && i0 + 1 < m && (((uintptr_t)(dst + i0)) & 3u) == 0) {
-          *reinterpret_cast<uint32_t*>(dst + i0) = (v0 & 0xFFFFu) | (v1 << 16);
+      const bool dw = CS == 1 && (((uintptr_t)dst) & 3u) == 0;
+      // stores the packed stored-order samples i0 (low), i0 + 1 (high) of the
+      // sub-block (i0 even)
+      auto put2 = [&](uint32_t i0, uint32_t o, bool ok0, bool ok1) {
+        if (dw && ok1) {
+          *reinterpret_cast<uint32_t*>(dst + i0) = o;
         } else {
-          if (i0 < m) dst[CS * i0] = (uint16_t)v0;
-          if (i0 + 1 < m) dst[CS * (i0 + 1)] = (uint16_t)v1;
+          if (ok0) dst[CS * i0] = (uint16_t)o;
+          if (ok1) dst[CS * (i0 + 1)] = (uint16_t)(o >> 16);
         }
       };
       RPP_STAT(6, 1);
       RPP_TSTAMP(5);
       if (fsp1 == 0) {
         // decode.h:79-80: every sample = write(last)
-        const uint32_t v = px_write(last[comp], be, ulsb);
-        for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) put2(i0, v, v, n);
+        const uint32_t v = px_write(last[comp], be, ulsb) * 0x10001u;
+        for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) put2(i0, v, true, i0 + 1 < n);
         P = P4;
       } else if (fsp1 == 15) {
         // decode.h:72-77: raw stored values; last = read(last sample)
@@ -864,8 +875,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           break;
         }
         for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) {
-          const uint32_t w = peek32(P4 + 16 * i0);
-          put2(i0, w, w >> 16, n);
+          put2(i0, peek32(P4 + 16 * i0), true, i0 + 1 < n);
         }
         last[comp] = __builtin_amdgcn_readfirstlane(px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb));
         P = P4 + 16 * n;
@@ -881,18 +891,18 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         auto extract = [&](uint32_t m) {
           for (; xdone < m; xdone += 2 * kWave) {
             const uint32_t i0 = xdone + 2 * lane;
-            const uint2 tt = i0 < m ? *reinterpret_cast<const uint2*>(&list[i0]) : make_uint2(0, 0);
-            const uint32_t t0 = tt.x, t1 = i0 + 1 < m ? tt.y : t0;
+            const bool ok0 = i0 < m, ok1 = i0 + 1 < m;
+            const uint2 tt = *reinterpret_cast<const uint2*>(&list[min(i0, kListDump - 2)]);
+            const uint32_t t0 = tt.x, t1 = ok1 ? tt.y : t0;
             const uint32_t lft = from_left(t1 + k);  // end of code i0 - 1
             const uint32_t st0 = lane == 0 ? start : lft;
             const uint32_t r0 = peek32(t0 + 1) & fmask, r1 = peek32(t1 + 1) & fmask;
             const uint32_t df0 = ((t0 - st0) << fs) | r0, df1 = ((t1 - t0 - k) << fs) | r1;
-            const uint32_t d0 = i0 < m ? (df0 >> 1) ^ (0u - (df0 & 1u)) : 0u;
-            const uint32_t d1 = i0 + 1 < m ? (df1 >> 1) ^ (0u - (df1 & 1u)) : 0u;
-            const uint32_t s1 = d0 + d1;
-            const uint32_t inc = wave_incl_sum(s1);
-            const uint32_t base = acc + inc - s1;
-            put2(i0, px_write(base + d0, be, ulsb), px_write(base + s1, be, ulsb), m);
+            const uint32_t d0 = ok0 ? (df0 >> 1) ^ (0u - (df0 & 1u)) : 0u;
+            const uint32_t d1 = ok1 ? (df1 >> 1) ^ (0u - (df1 & 1u)) : 0u;
+            const uint32_t inc = wave_incl_sum(d0 + d1);
+            const uint32_t v1 = acc + inc;  // value of sample i0 + 1 (mod 2^16)
+            put2(i0, px_write2(((v1 - d1) & 0xFFFFu) | (v1 << 16), selbe, ulsb), ok0, ok1);
             acc += wave_last(inc);
             start = wave_last(t1) + k;
           }
