@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <stdlib.h>
 
 #include "ricepp_amd.h"
 
@@ -885,6 +886,74 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t k = fsp1;
         const uint32_t fmask = (1u << fs) - 1u;
         const uint4* tb = tab + 256u * fs;
+        bool fast = false;
+        if (fs >= 5 && fs < 8 && n == 2 * kWave) {
+          // ---- fast path (the common case): a full 128-code sub-block with
+          //      fs 5..7 that lies in the first window.  Straight-line code:
+          //      at most 4 terminators per 24-bit segment (codes are >= 6
+          //      bits), every lane owns exactly 2 codes. ----
+          const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
+                      e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+          Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
+          M = scan_step8<kDppRowShr1>(M);
+          M = scan_step8<kDppRowShr2>(M);
+          M = scan_step8<kDppRowShr4>(M);
+          M = scan_step8<kDppRowShr8>(M);
+          M = scan_step8<kDppRowBcast15, 0xA>(M);
+          M = scan_step8<kDppRowBcast31, 0xC>(M);
+          const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
+          // state 4 at the window start: skip the header
+          uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 4u | kSelByte0) | kSelByte0;
+          const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+          sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+          const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+          sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+          const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+          uint32_t tm = a0 | (a1 << 8) | (a2 << 16);
+          const uint32_t cnt = __builtin_popcount(tm);
+          const uint32_t incl = wave_incl_sum(cnt);
+          const uint64_t finm = __ballot(incl >= n);
+          if (finm) {
+            fast = true;
+            const uint32_t excl = incl - cnt;
+            const uint32_t mine = n > excl ? min(cnt, n - excl) : 0u;
+            const uint32_t sb = P + kSegBits * lane;
+            const uint32_t rsel = n - 1 - excl;  // code n-1, in the lane holding it
+            uint32_t* lp = list + excl;
+            uint32_t ecand = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+              const uint32_t tg = sb + ffbl(tm);
+              tm &= tm - 1;
+              *(j < mine ? lp + j : list + kListDump) = tg;
+              ecand = j == rsel ? tg : ecand;
+            }
+            lds_fence();
+            // codes 2c, 2c+1 on lane c -> zig-zag deltas -> values
+            const uint2 tt = *reinterpret_cast<const uint2*>(&list[2 * lane]);
+            const uint32_t lft = dpp_keep<kDppWaveShr1>(P4 - k, tt.y);  // terminator of code 2c-1
+            const uint32_t r0 = peek32(tt.x + 1) & fmask, r1 = peek32(tt.y + 1) & fmask;
+            const uint32_t df0 = ((tt.x - lft - k) << fs) | r0, df1 = ((tt.y - tt.x - k) << fs) | r1;
+            const uint32_t d0 = (df0 >> 1) ^ (0u - (df0 & 1u)), d1 = (df1 >> 1) ^ (0u - (df1 & 1u));
+            const uint32_t inc = wave_incl_sum(d0 + d1);
+            const uint32_t v1 = last[comp] + inc;  // value of sample 2c + 1 (mod 2^16)
+            const uint32_t o = px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb);
+            if (dw) {
+              *reinterpret_cast<uint32_t*>(dst + 2 * lane) = o;
+            } else {
+              dst[CS * 2 * lane] = (uint16_t)o;
+              dst[CS * (2 * lane + 1)] = (uint16_t)(o >> 16);
+            }
+            last[comp] = (last[comp] + wave_last(inc)) & 0xFFFFu;
+            // the next sub-block starts after code n-1's remainder
+            P = readlane(ecand, (int)__builtin_ctzll(finm)) + k;
+            if (P > lim) {
+              status = RPP_TRUNCATED_INPUT;
+              break;
+            }
+          }
+        }
+        if (!fast) {
         // ---- codes [xdone, m) -> zig-zag deltas (decode.h:66-69) -> values,
         //      2 per lane (m even or m == n) ----
         uint32_t acc = last[comp], start = P4, xdone = 0;  // start: first bit of code xdone's unary run
@@ -1006,6 +1075,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           status = RPP_TRUNCATED_INPUT;
           break;
         }
+        }
       }
       RPP_TSTAMP(14);
       // request the next chunk once the look-ahead drops below 766 words (it
@@ -1087,7 +1157,8 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
     return RPP_INVALID_ARGUMENT;
   // one stream per wave; up to kDecMaxWaves waves share one copy of the
   // transfer tables, fewer when the batch cannot fill the 256 CUs anyway
-  const uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
+  uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
+  if (const char* e = getenv("RICEPP_DEC_WAVES")) W = std::min<uint32_t>(kDecMaxWaves, std::max(1, atoi(e)));  // diagnostics
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
   static std::once_flag attr_once;
   static hipError_t attr_err = hipSuccess;
