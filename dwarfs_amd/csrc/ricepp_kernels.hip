@@ -817,83 +817,206 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   };
 
   // codec.h:69-74,81-86: the 16-bit initial value of each component
-  uint32_t last[CS];
+  uint32_t last0 = 0, last1 = 0;
   uint32_t P = 16 * CS;
   if (status == RPP_OK) {
     if (16 * CS > lim) status = RPP_TRUNCATED_INPUT;
-#pragma unroll
-    for (uint32_t c = 0; c < CS; ++c) last[c] = __builtin_amdgcn_readfirstlane(peek32(16 * c) & 0xFFFFu);
+    last0 = __builtin_amdgcn_readfirstlane(peek32(0) & 0xFFFFu);
+    if (CS > 1) last1 = __builtin_amdgcn_readfirstlane(peek32(16) & 0xFFFFu);
   }
+  // this lane's 64 bits from bit sb of the stream (its 24-bit segment of a
+  // window and what follows it)
+  auto load_x = [&](uint32_t sb, uint32_t& xl, uint32_t& xh) {
+    const uint32_t* q = wptr(sb >> 5);
+    const uint32_t o = sb & 31u;
+    const uint32_t a0 = q[0], a1 = q[1], a2 = q[2];
+    xl = __builtin_amdgcn_alignbit(a1, a0, o);
+    xh = __builtin_amdgcn_alignbit(a2, a1, o);
+  };
+  // keep the look-ahead: retire the pending chunk once it is needed soon;
+  // request the next once the look-ahead drops below 766 words (it
+  // overwrites words [fill_w - 1024, fill_w - 768), all below P >> 5)
+  auto ring_keep = [&]() {
+    if (pend && fill_w < (P >> 5) + kAhead + 128) retire();
+    if (!(RPP_ABLATE & 4) && !pend && fill_w <= (P >> 5) + 766) request();
+  };
+  const uint32_t nsb = nchunks * CS;
+  // sub-blocks the fast loop may take: those of full 128-sample chunks
+  const uint32_t nsb_fast = bs == 2 * kWave ? (N / chunk_len) * CS : 0u;
+  const bool dw = CS == 1 && (((uintptr_t)out) & 3u) == 0;  // 2-sample stores are dword aligned
 
-  for (uint32_t chunk = 0; chunk < nchunks && status == RPP_OK; ++chunk) {
-    const uint32_t cbase = chunk * chunk_len;
-    const uint32_t n = min(N - cbase, chunk_len) / CS;  // samples per component sub-block
+  for (uint32_t s = 0; s < nsb && status == RPP_OK; ++s) {
+    // ---- fast loop (the common case): Rice sub-blocks of 128 codes with fs
+    //      5..7 that lie in one window, ring already resident.  Straight-line
+    //      code: at most 4 terminators per 24-bit segment (codes are >= 6
+    //      bits), every lane owns exactly 2 codes.  Anything else leaves the
+    //      loop and takes the general path below for that sub-block. ----
+    for (; s < nsb_fast; ++s) {
+      if (fill_w < (P >> 5) + kAhead || P + 4 > lim) break;
+      const uint32_t comp = s % CS;
+      uint16_t* dst = out + (s / CS) * chunk_len + comp;
+      uint32_t xl, xh;
+      load_x(P + kSegBits * lane, xl, xh);
+      const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
+      if (fsp1 - 6u > 2u) break;
+      const uint32_t fs = fsp1 - 1, k = fsp1, fmask = (1u << fs) - 1u;
+      const uint32_t n = 2 * kWave, P4 = P + 4;
+      const uint4* tb = tab + 256u * fs;
+      const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
+                  e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+      Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
+      M = scan_step8<kDppRowShr1>(M);
+      M = scan_step8<kDppRowShr2>(M);
+      M = scan_step8<kDppRowShr4>(M);
+      M = scan_step8<kDppRowShr8>(M);
+      M = scan_step8<kDppRowBcast15, 0xA>(M);
+      M = scan_step8<kDppRowBcast31, 0xC>(M);
+      const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
+      // state 4 at the window start: skip the header
+      uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 4u | kSelByte0) | kSelByte0;
+      const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+      sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+      const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+      sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+      const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+      uint32_t tm = a0 | (a1 << 8) | (a2 << 16);
+      const uint32_t cnt = __builtin_popcount(tm);
+      const uint32_t incl = wave_incl_sum(cnt);
+      const uint64_t finm = __ballot(incl >= n);
+      if (!finm) break;
+      const uint32_t excl = incl - cnt;
+      const uint32_t mine = n > excl ? min(cnt, n - excl) : 0u;
+      const uint32_t sb = P + kSegBits * lane;
+      const uint32_t rsel = n - 1 - excl;  // code n-1, in the lane holding it
+      uint32_t* lp = list + excl;
+      uint32_t ecand = 0;
 #pragma unroll
-    for (uint32_t comp = 0; comp < CS; ++comp) {
-      RPP_TSTAMP(4);
-      ensure(P >> 5);
-      // decode.h:60: 4-bit fs+1 header
-      if (P + 4 > lim) {
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t tg = sb + ffbl(tm);
+        tm &= tm - 1;
+        *(j < mine ? lp + j : list + kListDump) = tg;
+        ecand = j == rsel ? tg : ecand;
+      }
+      lds_fence();
+      // codes 2c, 2c+1 on lane c -> zig-zag deltas (decode.h:66-69) -> values
+      const uint2 tt = *reinterpret_cast<const uint2*>(&list[2 * lane]);
+      const uint32_t lft = dpp_keep<kDppWaveShr1>(P4 - k, tt.y);  // terminator of code 2c-1
+      const uint32_t r0 = peek32(tt.x + 1) & fmask, r1 = peek32(tt.y + 1) & fmask;
+      const uint32_t df0 = ((tt.x - lft - k) << fs) | r0, df1 = ((tt.y - tt.x - k) << fs) | r1;
+      const uint32_t d0 = (df0 >> 1) ^ (0u - (df0 & 1u)), d1 = (df1 >> 1) ^ (0u - (df1 & 1u));
+      const uint32_t inc = wave_incl_sum(d0 + d1);
+      const uint32_t lastc = comp ? last1 : last0;
+      const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (mod 2^16)
+      const uint32_t o = px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb);
+      if (dw) {
+        *reinterpret_cast<uint32_t*>(dst + 2 * lane) = o;
+      } else {
+        dst[CS * 2 * lane] = (uint16_t)o;
+        dst[CS * (2 * lane + 1)] = (uint16_t)(o >> 16);
+      }
+      const uint32_t lnew = (lastc + wave_last(inc)) & 0xFFFFu;
+      if (comp) last1 = lnew;
+      else last0 = lnew;
+      // the next sub-block starts after code n-1's remainder
+      P = readlane(ecand, (int)__builtin_ctzll(finm)) + k;
+      if (P > lim) {
         status = RPP_TRUNCATED_INPUT;
         break;
       }
-      // this lane's 64 bits from bit sb of the stream (its 24-bit segment of
-      // the window and what follows it)
-      uint32_t xl, xh;
-      auto load_x = [&](uint32_t sb) {
-        const uint32_t* q = wptr(sb >> 5);
-        const uint32_t o = sb & 31u;
-        const uint32_t a0 = q[0], a1 = q[1], a2 = q[2];
-        xl = __builtin_amdgcn_alignbit(a1, a0, o);
-        xh = __builtin_amdgcn_alignbit(a2, a1, o);
-      };
-      load_x(P + kSegBits * lane);
-      const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
-      const uint32_t P4 = P + 4;
-      uint16_t* dst = out + cbase + comp;  // sample i of this sub-block at dst[CS * i]
-      const bool dw = CS == 1 && (((uintptr_t)dst) & 3u) == 0;
-      // stores the packed stored-order samples i0 (low), i0 + 1 (high) of the
-      // sub-block (i0 even)
-      auto put2 = [&](uint32_t i0, uint32_t o, bool ok0, bool ok1) {
-        if (dw && ok1) {
-          *reinterpret_cast<uint32_t*>(dst + i0) = o;
-        } else {
-          if (ok0) dst[CS * i0] = (uint16_t)o;
-          if (ok1) dst[CS * (i0 + 1)] = (uint16_t)(o >> 16);
-        }
-      };
-      RPP_STAT(6, 1);
-      RPP_TSTAMP(5);
-      if (fsp1 == 0) {
-        // decode.h:79-80: every sample = write(last)
-        const uint32_t v = px_write(last[comp], be, ulsb) * 0x10001u;
-        for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) put2(i0, v, true, i0 + 1 < n);
-        P = P4;
-      } else if (fsp1 == 15) {
-        // decode.h:72-77: raw stored values; last = read(last sample)
-        if ((uint64_t)P4 + 16ull * n > lim) {
-          status = RPP_TRUNCATED_INPUT;
-          break;
-        }
-        for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) {
-          put2(i0, peek32(P4 + 16 * i0), true, i0 + 1 < n);
-        }
-        last[comp] = __builtin_amdgcn_readfirstlane(px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb));
-        P = P4 + 16 * n;
+      ring_keep();
+    }
+    if (s >= nsb || status != RPP_OK) break;
+    // ---- general path: one sub-block of any kind ----
+    const uint32_t comp = s % CS;
+    const uint32_t cbase = (s / CS) * chunk_len;
+    const uint32_t n = min(N - cbase, chunk_len) / CS;  // samples per component sub-block
+    RPP_TSTAMP(4);
+    ensure(P >> 5);
+    // decode.h:60: 4-bit fs+1 header
+    if (P + 4 > lim) {
+      status = RPP_TRUNCATED_INPUT;
+      break;
+    }
+    uint32_t xl, xh;
+    load_x(P + kSegBits * lane, xl, xh);
+    const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
+    const uint32_t P4 = P + 4;
+    uint16_t* dst = out + cbase + comp;  // sample i of this sub-block at dst[CS * i]
+    const bool dw = CS == 1 && (((uintptr_t)dst) & 3u) == 0;
+    // stores the packed stored-order samples i0 (low), i0 + 1 (high) of the
+    // sub-block (i0 even)
+    auto put2 = [&](uint32_t i0, uint32_t o, bool ok0, bool ok1) {
+      if (dw && ok1) {
+        *reinterpret_cast<uint32_t*>(dst + i0) = o;
       } else {
-        // decode.h:62-71: n Rice codes with fs = fsp1 - 1
-        const uint32_t fs = fsp1 - 1;
-        const uint32_t k = fsp1;
-        const uint32_t fmask = (1u << fs) - 1u;
-        const uint4* tb = tab + 256u * fs;
-        bool fast = false;
-        if (fs >= 5 && fs < 8 && n == 2 * kWave) {
-          // ---- fast path (the common case): a full 128-code sub-block with
-          //      fs 5..7 that lies in the first window.  Straight-line code:
-          //      at most 4 terminators per 24-bit segment (codes are >= 6
-          //      bits), every lane owns exactly 2 codes. ----
-          const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
-                      e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+        if (ok0) dst[CS * i0] = (uint16_t)o;
+        if (ok1) dst[CS * (i0 + 1)] = (uint16_t)(o >> 16);
+      }
+    };
+    RPP_STAT(6, 1);
+    RPP_TSTAMP(5);
+    if (fsp1 == 0) {
+      // decode.h:79-80: every sample = write(last)
+      const uint32_t v = px_write(comp ? last1 : last0, be, ulsb) * 0x10001u;
+      for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) put2(i0, v, true, i0 + 1 < n);
+      P = P4;
+    } else if (fsp1 == 15) {
+      // decode.h:72-77: raw stored values; last = read(last sample)
+      if ((uint64_t)P4 + 16ull * n > lim) {
+        status = RPP_TRUNCATED_INPUT;
+        break;
+      }
+      for (uint32_t i0 = 2 * lane; i0 < n; i0 += 2 * kWave) {
+        put2(i0, peek32(P4 + 16 * i0), true, i0 + 1 < n);
+      }
+      const uint32_t lv = __builtin_amdgcn_readfirstlane(px_read(peek32(P4 + 16 * (n - 1)) & 0xFFFFu, be, ulsb));
+      if (comp) last1 = lv;
+      else last0 = lv;
+      P = P4 + 16 * n;
+    } else {
+      // decode.h:62-71: n Rice codes with fs = fsp1 - 1
+      const uint32_t fs = fsp1 - 1;
+      const uint32_t k = fsp1;
+      const uint32_t fmask = (1u << fs) - 1u;
+      const uint4* tb = tab + 256u * fs;
+      // ---- codes [xdone, m) -> zig-zag deltas (decode.h:66-69) -> values,
+      //      2 per lane (m even or m == n) ----
+      uint32_t acc = comp ? last1 : last0, start = P4, xdone = 0;  // start: first bit of code xdone's unary run
+      auto extract = [&](uint32_t m) {
+        for (; xdone < m; xdone += 2 * kWave) {
+          const uint32_t i0 = xdone + 2 * lane;
+          const bool ok0 = i0 < m, ok1 = i0 + 1 < m;
+          const uint2 tt = *reinterpret_cast<const uint2*>(&list[min(i0, kListDump - 2)]);
+          const uint32_t t0 = tt.x, t1 = ok1 ? tt.y : t0;
+          const uint32_t lft = from_left(t1 + k);  // end of code i0 - 1
+          const uint32_t st0 = lane == 0 ? start : lft;
+          const uint32_t r0 = peek32(t0 + 1) & fmask, r1 = peek32(t1 + 1) & fmask;
+          const uint32_t df0 = ((t0 - st0) << fs) | r0, df1 = ((t1 - t0 - k) << fs) | r1;
+          const uint32_t d0 = ok0 ? (df0 >> 1) ^ (0u - (df0 & 1u)) : 0u;
+          const uint32_t d1 = ok1 ? (df1 >> 1) ^ (0u - (df1 & 1u)) : 0u;
+          const uint32_t inc = wave_incl_sum(d0 + d1);
+          const uint32_t v1 = acc + inc;  // value of sample i0 + 1 (mod 2^16)
+          put2(i0, px_write2(((v1 - d1) & 0xFFFFu) | (v1 << 16), selbe, ulsb), ok0, ok1);
+          acc += wave_last(inc);
+          start = wave_last(t1) + k;
+        }
+        xdone = m;
+        start = __builtin_amdgcn_readfirstlane(list[m - 1]) + k;
+      };
+      // ---- parse: the terminator position of code i -> list[i] ----
+      // q0: first bit of the window; s0: state at q0 (4 = skip the header);
+      // done: codes before the window
+      uint32_t q0 = P, s0 = 4, done = 0;
+      for (;;) {
+        RPP_STAT(0, 1);
+        const uint32_t sb = q0 + kSegBits * lane;
+        // 1. byte transfer functions
+        const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
+                    e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+        RPP_TSTAMP(10);
+        uint32_t tm, xexit;
+        if (fs < 8) {
+          // 2. segment map, scan along the wave, entry state
           Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
           M = scan_step8<kDppRowShr1>(M);
           M = scan_step8<kDppRowShr2>(M);
@@ -902,188 +1025,85 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           M = scan_step8<kDppRowBcast15, 0xA>(M);
           M = scan_step8<kDppRowBcast31, 0xC>(M);
           const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
-          // state 4 at the window start: skip the header
-          uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 4u | kSelByte0) | kSelByte0;
-          const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+          // 3. terminators of this lane's segment
+          uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
+          const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
           sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
-          const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+          const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
           sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
-          const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
-          uint32_t tm = a0 | (a1 << 8) | (a2 << 16);
-          const uint32_t cnt = __builtin_popcount(tm);
-          const uint32_t incl = wave_incl_sum(cnt);
-          const uint64_t finm = __ballot(incl >= n);
-          if (finm) {
-            fast = true;
-            const uint32_t excl = incl - cnt;
-            const uint32_t mine = n > excl ? min(cnt, n - excl) : 0u;
-            const uint32_t sb = P + kSegBits * lane;
-            const uint32_t rsel = n - 1 - excl;  // code n-1, in the lane holding it
-            uint32_t* lp = list + excl;
-            uint32_t ecand = 0;
+          const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+          xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
+          tm = t0 | (t1 << 8) | (t2 << 16);
+        } else {
+          const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
+          Map16 M = comp16(b2, comp16(b1, b0));
+          M = scan_step16<kDppRowShr1>(M);
+          M = scan_step16<kDppRowShr2>(M);
+          M = scan_step16<kDppRowShr4>(M);
+          M = scan_step16<kDppRowShr8>(M);
+          M = scan_step16<kDppRowBcast15, 0xA>(M);
+          M = scan_step16<kDppRowBcast31, 0xC>(M);
+          const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
+                         dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
+          uint32_t st = sel16(X, s0) & 0xFFu;
+          uint32_t t[3];
+          const uint4 ee[3] = {e0, e1, e2};
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-              const uint32_t tg = sb + ffbl(tm);
-              tm &= tm - 1;
-              *(j < mine ? lp + j : list + kListDump) = tg;
-              ecand = j == rsel ? tg : ecand;
-            }
-            lds_fence();
-            // codes 2c, 2c+1 on lane c -> zig-zag deltas -> values
-            const uint2 tt = *reinterpret_cast<const uint2*>(&list[2 * lane]);
-            const uint32_t lft = dpp_keep<kDppWaveShr1>(P4 - k, tt.y);  // terminator of code 2c-1
-            const uint32_t r0 = peek32(tt.x + 1) & fmask, r1 = peek32(tt.y + 1) & fmask;
-            const uint32_t df0 = ((tt.x - lft - k) << fs) | r0, df1 = ((tt.y - tt.x - k) << fs) | r1;
-            const uint32_t d0 = (df0 >> 1) ^ (0u - (df0 & 1u)), d1 = (df1 >> 1) ^ (0u - (df1 & 1u));
-            const uint32_t inc = wave_incl_sum(d0 + d1);
-            const uint32_t v1 = last[comp] + inc;  // value of sample 2c + 1 (mod 2^16)
-            const uint32_t o = px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb);
-            if (dw) {
-              *reinterpret_cast<uint32_t*>(dst + 2 * lane) = o;
-            } else {
-              dst[CS * 2 * lane] = (uint16_t)o;
-              dst[CS * (2 * lane + 1)] = (uint16_t)(o >> 16);
-            }
-            last[comp] = (last[comp] + wave_last(inc)) & 0xFFFFu;
-            // the next sub-block starts after code n-1's remainder
-            P = readlane(ecand, (int)__builtin_ctzll(finm)) + k;
-            if (P > lim) {
-              status = RPP_TRUNCATED_INPUT;
-              break;
-            }
+          for (int j = 0; j < 3; ++j) {
+            const uint32_t sel = st | kSelByte0;
+            const bool skip = st >= 8;
+            t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
+            st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
           }
+          tm = t[0] | (t[1] << 8) | (t[2] << 16);
+          xexit = st;
         }
-        if (!fast) {
-        // ---- codes [xdone, m) -> zig-zag deltas (decode.h:66-69) -> values,
-        //      2 per lane (m even or m == n) ----
-        uint32_t acc = last[comp], start = P4, xdone = 0;  // start: first bit of code xdone's unary run
-        auto extract = [&](uint32_t m) {
-          for (; xdone < m; xdone += 2 * kWave) {
-            const uint32_t i0 = xdone + 2 * lane;
-            const bool ok0 = i0 < m, ok1 = i0 + 1 < m;
-            const uint2 tt = *reinterpret_cast<const uint2*>(&list[min(i0, kListDump - 2)]);
-            const uint32_t t0 = tt.x, t1 = ok1 ? tt.y : t0;
-            const uint32_t lft = from_left(t1 + k);  // end of code i0 - 1
-            const uint32_t st0 = lane == 0 ? start : lft;
-            const uint32_t r0 = peek32(t0 + 1) & fmask, r1 = peek32(t1 + 1) & fmask;
-            const uint32_t df0 = ((t0 - st0) << fs) | r0, df1 = ((t1 - t0 - k) << fs) | r1;
-            const uint32_t d0 = ok0 ? (df0 >> 1) ^ (0u - (df0 & 1u)) : 0u;
-            const uint32_t d1 = ok1 ? (df1 >> 1) ^ (0u - (df1 & 1u)) : 0u;
-            const uint32_t inc = wave_incl_sum(d0 + d1);
-            const uint32_t v1 = acc + inc;  // value of sample i0 + 1 (mod 2^16)
-            put2(i0, px_write2(((v1 - d1) & 0xFFFFu) | (v1 << 16), selbe, ulsb), ok0, ok1);
-            acc += wave_last(inc);
-            start = wave_last(t1) + k;
-          }
-          xdone = m;
-          start = __builtin_amdgcn_readfirstlane(list[m - 1]) + k;
-        };
-        // ---- parse: the terminator position of code i -> list[i] ----
-        // q0: first bit of the window; s0: state at q0 (4 = skip the header);
-        // done: codes before the window
-        uint32_t q0 = P, s0 = 4, done = 0;
-        for (;;) {
-          RPP_STAT(0, 1);
-          const uint32_t sb = q0 + kSegBits * lane;
-          // 1. byte transfer functions
-          const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
-                      e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
-          RPP_TSTAMP(10);
-          uint32_t tm, xexit;
-          if (fs < 8) {
-            // 2. segment map, scan along the wave, entry state
-            Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
-            M = scan_step8<kDppRowShr1>(M);
-            M = scan_step8<kDppRowShr2>(M);
-            M = scan_step8<kDppRowShr4>(M);
-            M = scan_step8<kDppRowShr8>(M);
-            M = scan_step8<kDppRowBcast15, 0xA>(M);
-            M = scan_step8<kDppRowBcast31, 0xC>(M);
-            const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
-            // 3. terminators of this lane's segment
-            uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
-            const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-            sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
-            const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
-            sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
-            const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
-            xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
-            tm = t0 | (t1 << 8) | (t2 << 16);
-          } else {
-            const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
-            Map16 M = comp16(b2, comp16(b1, b0));
-            M = scan_step16<kDppRowShr1>(M);
-            M = scan_step16<kDppRowShr2>(M);
-            M = scan_step16<kDppRowShr4>(M);
-            M = scan_step16<kDppRowShr8>(M);
-            M = scan_step16<kDppRowBcast15, 0xA>(M);
-            M = scan_step16<kDppRowBcast31, 0xC>(M);
-            const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
-                           dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
-            uint32_t st = sel16(X, s0) & 0xFFu;
-            uint32_t t[3];
-            const uint4 ee[3] = {e0, e1, e2};
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              const uint32_t sel = st | kSelByte0;
-              const bool skip = st >= 8;
-              t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
-              st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
-            }
-            tm = t[0] | (t[1] << 8) | (t[2] << 16);
-            xexit = st;
-          }
-          RPP_TSTAMP(11);
-          // 4. code indices: terminators -> list[done + excl + j]
-          const uint32_t cnt = __builtin_popcount(tm);
-          const uint32_t incl = wave_incl_sum(cnt);
-          const uint32_t excl = incl - cnt;
-          const uint32_t need = n - done;
-          const uint32_t mine = need > excl ? min(cnt, need - excl) : 0u;
-          uint32_t* lp = list + done + excl;
-          for (uint32_t j = 0; __any(j < mine); ++j) {
-            const uint32_t t = ffbl(tm);
-            tm &= tm - 1;
-            *(j < mine ? lp + j : list + kListDump) = sb + t;
-          }
-          RPP_TSTAMP(12);
-          if (__ballot(incl >= need)) break;
-          // continuation window: the sub-block is longer than kWinBits;
-          // turn the codes found so far into samples first (the ring only
-          // keeps the recent windows resident)
-          done += wave_last(incl);
-          if ((done & ~1u) > xdone) {
-            lds_fence();
-            extract(done & ~1u);
-          }
-          s0 = wave_last(xexit);
-          q0 += kWinBits;
-          if (q0 >= lim) {  // the open unary search would read past the input
-            status = RPP_TRUNCATED_INPUT;
-            break;
-          }
-          ensure(q0 >> 5);
-          load_x(q0 + kSegBits * lane);
+        RPP_TSTAMP(11);
+        // 4. code indices: terminators -> list[done + excl + j]
+        const uint32_t cnt = __builtin_popcount(tm);
+        const uint32_t incl = wave_incl_sum(cnt);
+        const uint32_t excl = incl - cnt;
+        const uint32_t need = n - done;
+        const uint32_t mine = need > excl ? min(cnt, need - excl) : 0u;
+        uint32_t* lp = list + done + excl;
+        for (uint32_t j = 0; __any(j < mine); ++j) {
+          const uint32_t t = ffbl(tm);
+          tm &= tm - 1;
+          *(j < mine ? lp + j : list + kListDump) = sb + t;
         }
-        if (status != RPP_OK) break;
-        lds_fence();
-        extract(n);
-        last[comp] = acc & 0xFFFFu;
-        // the next sub-block starts after code n-1's remainder
-        P = __builtin_amdgcn_readfirstlane(list[n - 1]) + k;
-        if (P > lim) {
+        RPP_TSTAMP(12);
+        if (__ballot(incl >= need)) break;
+        // continuation window: the sub-block is longer than kWinBits;
+        // turn the codes found so far into samples first (the ring only
+        // keeps the recent windows resident)
+        done += wave_last(incl);
+        if ((done & ~1u) > xdone) {
+          lds_fence();
+          extract(done & ~1u);
+        }
+        s0 = wave_last(xexit);
+        q0 += kWinBits;
+        if (q0 >= lim) {  // the open unary search would read past the input
           status = RPP_TRUNCATED_INPUT;
           break;
         }
-        }
+        ensure(q0 >> 5);
+        load_x(q0 + kSegBits * lane, xl, xh);
       }
-      RPP_TSTAMP(14);
-      // request the next chunk once the look-ahead drops below 766 words (it
-      // overwrites words [fill_w - 1024, fill_w - 768), all below P >> 5)
-      if (pend && fill_w < (P >> 5) + kAhead + 128) retire();
-      if (!(RPP_ABLATE & 4) && !pend && fill_w <= (P >> 5) + 766) request();
-      RPP_TSTAMP(15);
+      if (status != RPP_OK) break;
+      lds_fence();
+      extract(n);
+      if (comp) last1 = acc & 0xFFFFu;
+      else last0 = acc & 0xFFFFu;
+      // the next sub-block starts after code n-1's remainder
+      P = __builtin_amdgcn_readfirstlane(list[n - 1]) + k;
+      if (P > lim) {
+        status = RPP_TRUNCATED_INPUT;
+        break;
+      }
     }
+    RPP_TSTAMP(14);
+    ring_keep();
   }
   retire();
   if (lane == 0) p.status[b] = status;
