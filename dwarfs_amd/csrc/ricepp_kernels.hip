@@ -888,21 +888,23 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       const uint32_t mine = n > excl ? min(cnt, n - excl) : 0u;
       const uint32_t sb = P + kSegBits * lane;
       const uint32_t rsel = n - 1 - excl;  // code n-1, in the lane holding it
-      uint32_t* lp = list + excl;
+      // (terminator position, remainder) of code i -> list pair i
+      uint2* lp = reinterpret_cast<uint2*>(list) + excl;
       uint32_t ecand = 0;
 #pragma unroll
       for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t tg = sb + ffbl(tm);
+        const uint32_t t = ffbl(tm);
         tm &= tm - 1;
-        *(j < mine ? lp + j : list + kListDump) = tg;
+        const uint32_t tg = sb + t;
+        const uint32_t rem = __builtin_amdgcn_alignbit(xh, xl, t + 1) & fmask;
+        *(j < mine ? lp + j : reinterpret_cast<uint2*>(list) + kListDump / 2) = make_uint2(tg, rem);
         ecand = j == rsel ? tg : ecand;
       }
       lds_fence();
       // codes 2c, 2c+1 on lane c -> zig-zag deltas (decode.h:66-69) -> values
-      const uint2 tt = *reinterpret_cast<const uint2*>(&list[2 * lane]);
-      const uint32_t lft = dpp_keep<kDppWaveShr1>(P4 - k, tt.y);  // terminator of code 2c-1
-      const uint32_t r0 = peek32(tt.x + 1) & fmask, r1 = peek32(tt.y + 1) & fmask;
-      const uint32_t df0 = ((tt.x - lft - k) << fs) | r0, df1 = ((tt.y - tt.x - k) << fs) | r1;
+      const uint4 tt = reinterpret_cast<const uint4*>(list)[lane];
+      const uint32_t lft = dpp_keep<kDppWaveShr1>(P4 - k, tt.z);  // terminator of code 2c-1
+      const uint32_t df0 = ((tt.x - lft - k) << fs) | tt.y, df1 = ((tt.z - tt.x - k) << fs) | tt.w;
       const uint32_t d0 = (df0 >> 1) ^ (0u - (df0 & 1u)), d1 = (df1 >> 1) ^ (0u - (df1 & 1u));
       const uint32_t inc = wave_incl_sum(d0 + d1);
       const uint32_t lastc = comp ? last1 : last0;
