@@ -39,6 +39,10 @@
 #ifndef RPP_ABLATE
 #define RPP_ABLATE 0
 #endif
+// Encode ablations (diagnostic builds, outputs wrong): 1 code emission, 2 split walk.
+#ifndef RPP_EABLATE
+#define RPP_EABLATE 0
+#endif
 
 #ifdef RPP_STATS
 // Diagnostic build only (-DRPP_STATS): loop trip counters, summed over waves.
@@ -109,24 +113,6 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, 0xF, false);
 }
 
-// Sum over the aligned group of G lanes containing this lane (G pow2 <= 64),
-// broadcast to every lane of the group.  All lanes must be active.
-__device__ __forceinline__ uint32_t group_sum(uint32_t v, uint32_t G) {
-  if (G >= 2) v += dpp<kDppQuadXor1>(v);
-  if (G >= 4) v += dpp<kDppQuadXor2>(v);
-  if (G >= 8) v += dpp<kDppRowHalfMirror>(v);
-  if (G >= 16) v += dpp<kDppRowMirror>(v);
-  if (G >= 32) {
-    auto t = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    v = t[0] + t[1];
-  }
-  if (G >= 64) {
-    auto t = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    v = t[0] + t[1];
-  }
-  return v;
-}
-
 // Inclusive prefix sum over the 64 lanes (all active).
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
   v += dpp<kDppRowShr1>(v);
@@ -147,6 +133,19 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
   v = max(v, dpp<kDppRowBcast15, 0xA>(v));
   v = max(v, dpp<kDppRowBcast31, 0xC>(v));
   return v;
+}
+
+// Orders this wave's LDS accesses (one wave's DS operations execute in
+// order); unlike __syncthreads() it does not drain vmcnt, so outstanding
+// global loads (prefetches) and stores stay in flight.  One-wave workgroups.
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
+
+// DPP move; lanes without a source in range keep `old`.  Called with every
+// lane active (a DPP source lane that is switched off reads as out of range).
+template <int Ctrl, int RowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp_keep(uint32_t old, uint32_t v) {
+  // lanes without a source in range keep `old`
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, Ctrl, RowMask, 0xF, false);
 }
 
 // Value of lane l-1 (0 for lane 0).
@@ -171,29 +170,52 @@ struct EncParams {
   uint32_t bs, cs, be, ulsb;
 };
 
+// Compile-time shape of an encode launch: SPL samples per lane (8 or 16), a
+// ricepp sub-block owned by an aligned group of G lanes (G = next pow2 of
+// ceil(bs / SPL)), CS component streams.  64 / G sub-blocks per iteration.
+
+// Sum over the aligned group of G lanes containing this lane, broadcast to
+// every lane of the group (butterfly; all lanes active).
+template <uint32_t G>
+__device__ __forceinline__ uint32_t gsum(uint32_t v) {
+  if constexpr (G >= 2) v += dpp<kDppQuadXor1>(v);
+  if constexpr (G >= 4) v += dpp<kDppQuadXor2>(v);
+  if constexpr (G >= 8) v += dpp<kDppRowHalfMirror>(v);
+  if constexpr (G >= 16) v += dpp<kDppRowMirror>(v);
+  if constexpr (G >= 32) {
+    auto t = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = t[0] + t[1];
+  }
+  if constexpr (G >= 64) {
+    auto t = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = t[0] + t[1];
+  }
+  return v;
+}
+
 // Per-lane sub-block geometry of one encode iteration.
 struct EncGeom {
   uint32_t n;        // samples in this lane's sub-block (0: no sub-block)
-  uint32_t cnt;      // samples owned by this lane (<= 8)
+  uint32_t cnt;      // samples owned by this lane (<= SPL)
   uint32_t m_first;  // stream index of the lane's first sample
   uint32_t comp;     // component stream
 };
 
-__device__ __forceinline__ EncGeom enc_geom(uint32_t s, uint32_t j, uint32_t nsb, uint32_t N, uint32_t bs,
-                                            uint32_t cs) {
+template <uint32_t SPL, uint32_t CS>
+__device__ __forceinline__ EncGeom enc_geom(uint32_t s, uint32_t j, uint32_t nsb, uint32_t N, uint32_t bs) {
   EncGeom g;
   // codec.h:88-97: chunks of cs*bs samples; component i takes i, i+cs, ...
-  const uint32_t chunk = cs == 1 ? s : s >> 1;
-  g.comp = s - chunk * cs;
-  const uint32_t cbase = chunk * cs * bs;
+  const uint32_t chunk = s / CS;
+  g.comp = s % CS;
+  const uint32_t cbase = chunk * CS * bs;
   g.n = 0;
   if (s < nsb) {
-    const uint32_t rem = (N - cbase) / cs;
+    const uint32_t rem = (N - cbase) / CS;
     g.n = rem < bs ? rem : bs;
   }
-  const uint32_t k0 = 8 * j;
-  g.cnt = k0 < g.n ? min(g.n - k0, 8u) : 0u;
-  g.m_first = cbase + g.comp + cs * k0;
+  const uint32_t k0 = SPL * j;
+  g.cnt = k0 < g.n ? min(g.n - k0, SPL) : 0u;
+  g.m_first = cbase + g.comp + CS * k0;
   return g;
 }
 
@@ -202,49 +224,57 @@ typedef short ss2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
 __device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
 
-// The lane's 8 stored samples as 4 packed pairs (sample 2k in the low half
-// of w[k]) plus the previous same-component sample (the delta reference).
+// The lane's stored samples as SPL / 2 packed pairs (sample 2k in the low
+// half of w[k]) plus the previous same-component stored sample.
+template <uint32_t SPL>
 struct EncRaw {
-  uint4 a, c;     // cs == 1: a holds the 8 samples; cs == 2: a, c hold 16 interleaved
-  uint32_t prev;  // samples, this lane's component is picked at use (not at load)
+  uint32_t w[SPL / 2];
+  uint32_t prev;
 };
 
-__device__ __forceinline__ void enc_words(const EncRaw& r, uint32_t cs, uint32_t comp, uint32_t w[4]) {
-  if (cs == 1) {
-    w[0] = r.a.x; w[1] = r.a.y; w[2] = r.a.z; w[3] = r.a.w;
-  } else {
-    const uint32_t sel = comp ? 0x07060302u : 0x05040100u;
-    w[0] = __builtin_amdgcn_perm(r.a.y, r.a.x, sel);
-    w[1] = __builtin_amdgcn_perm(r.a.w, r.a.z, sel);
-    w[2] = __builtin_amdgcn_perm(r.c.y, r.c.x, sel);
-    w[3] = __builtin_amdgcn_perm(r.c.w, r.c.z, sel);
-  }
-}
-
-// Full iterations (every lane owns 0 or 8 samples): branch-free 16-byte
-// loads, so a double-buffered prefetch stays in flight.
-__device__ __forceinline__ EncRaw enc_load_vec(const uint16_t* in, const EncGeom& g, uint32_t cs) {
-  EncRaw r;
+// Full iterations (every lane owns 0 or SPL samples): 16-byte loads.
+template <uint32_t SPL, uint32_t CS>
+__device__ __forceinline__ EncRaw<SPL> enc_load_vec(const uint16_t* in, const EncGeom& g, bool load_prev) {
+  EncRaw<SPL> r;
   // codec.h:72-73: a component's first sample is its own reference (last = read(in[i]))
-  const uint32_t pi = g.cnt ? (g.m_first >= cs ? g.m_first - cs : g.m_first) : 0u;
-  r.prev = in[pi];
+  if (load_prev) {
+    const uint32_t pi = g.cnt ? (g.m_first >= CS ? g.m_first - CS : g.m_first) : 0u;
+    r.prev = in[pi];
+  } else {
+    r.prev = 0;
+  }
   const uint4* q = reinterpret_cast<const uint4*>(g.cnt ? in + (g.m_first - g.comp) : in);
-  r.a = q[0];
-  r.c = q[cs - 1];  // cs == 1: a harmless reload of q[0] (a select here went through scratch)
+  if constexpr (CS == 1) {
+#pragma unroll
+    for (uint32_t i = 0; i < SPL / 8; ++i) {
+      const uint4 v = q[i];
+      r.w[4 * i] = v.x; r.w[4 * i + 1] = v.y; r.w[4 * i + 2] = v.z; r.w[4 * i + 3] = v.w;
+    }
+  } else {
+    // interleaved (c0, c1) pairs: keep this lane's component
+    const uint32_t sel = g.comp ? 0x07060302u : 0x05040100u;
+#pragma unroll
+    for (uint32_t i = 0; i < SPL / 4; ++i) {
+      const uint4 v = q[i];
+      r.w[2 * i] = __builtin_amdgcn_perm(v.y, v.x, sel);
+      r.w[2 * i + 1] = __builtin_amdgcn_perm(v.w, v.z, sel);
+    }
+  }
   return r;
 }
 
 // Ragged tail / unaligned streams: per-sample loads.
-__device__ __forceinline__ EncRaw enc_load_scalar(const uint16_t* in, const EncGeom& g, uint32_t cs) {
-  EncRaw r;
-  const uint32_t pi = g.m_first >= cs ? g.m_first - cs : g.m_first;
+template <uint32_t SPL, uint32_t CS>
+__device__ __forceinline__ EncRaw<SPL> enc_load_scalar(const uint16_t* in, const EncGeom& g) {
+  EncRaw<SPL> r;
+  const uint32_t pi = g.m_first >= CS ? g.m_first - CS : g.m_first;
   r.prev = g.cnt ? (uint32_t)in[pi] : 0u;
-  uint32_t v[8];
 #pragma unroll
-  for (uint32_t i = 0; i < 8; ++i) v[i] = i < g.cnt ? (uint32_t)in[g.m_first + cs * i] : 0u;
-  // stored as the cs == 1 layout (this lane's samples only)
-  r.a = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
-  r.c = r.a;
+  for (uint32_t k = 0; k < SPL / 2; ++k) {
+    const uint32_t lo = 2 * k < g.cnt ? (uint32_t)in[g.m_first + CS * 2 * k] : 0u;
+    const uint32_t hi = 2 * k + 1 < g.cnt ? (uint32_t)in[g.m_first + CS * (2 * k + 1)] : 0u;
+    r.w[k] = lo | (hi << 16);
+  }
   return r;
 }
 
@@ -264,29 +294,37 @@ struct EncState {
   uint32_t* out32;
   uint32_t win_w0;  // global word index held in win[0] (multiple of 16)
   uint32_t base;    // absolute bit position of the next sub-block
+  uint32_t carry;   // pixel value of the sample before this iteration (DPP-prev mode)
 };
 
 // One group of 64/G sub-blocks: zig-zag deltas, compute_best_split replay,
 // bit positions by one wave scan, codes OR-ed into the LDS window.
-__device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, const EncGeom& geo, uint32_t G,
-                                              uint32_t j, uint32_t be, uint32_t ulsb, bool mask_tail,
-                                              uint32_t cs_layout) {
+// dpp_prev: every lane full and the previous sample of a lane's first sample
+// is the previous lane's last one (CS == 1, bs == G * SPL): no prev loads.
+template <uint32_t SPL, uint32_t G, uint32_t CS>
+__device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r, const EncGeom& geo, uint32_t j,
+                                              uint32_t selbe, uint32_t be, uint32_t ulsb, bool mask_tail,
+                                              bool dpp_prev) {
+  constexpr uint32_t NW = SPL / 2;
   const uint32_t n = geo.n, cnt = geo.cnt;
-  uint32_t rw[4];
-  enc_words(r, cs_layout, geo.comp, rw);
   const bool sb_valid = n != 0;
   // ---- pixel values (ricepp_cpuspecific_traits.h:63-67) and zig-zag deltas
   //      (encode.h:116-123), two samples per instruction ----
-  us2 v[4], d[4];
+  us2 v[NW], d[NW];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t x = be ? __builtin_amdgcn_perm(rw[k], rw[k], 0x02030001u) : rw[k];
-    v[k] = as_us2(x) >> (us2)(unsigned short)ulsb;
+  for (uint32_t k = 0; k < NW; ++k)
+    v[k] = as_us2(__builtin_amdgcn_perm(r.w[k], r.w[k], selbe)) >> (us2)(unsigned short)ulsb;
+  uint32_t pv;
+  if (dpp_prev) {
+    const uint32_t lastv = as_u32(v[NW - 1]) >> 16;
+    pv = dpp_keep<kDppWaveShr1>(st.carry, lastv);  // lane 0: the carried sample
+    st.carry = readlane(lastv, kWave - 1);
+  } else {
+    pv = px_read(r.prev, be, ulsb);
   }
-  const uint32_t pv = px_read(r.prev, be, ulsb);
   uint32_t prevw = pv << 16;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (uint32_t k = 0; k < NW; ++k) {
     const us2 pp = as_us2(__builtin_amdgcn_alignbit(as_u32(v[k]), prevw, 16));
     prevw = as_u32(v[k]);
     const us2 diff = v[k] - pp;
@@ -294,7 +332,7 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, con
   }
   if (mask_tail) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (uint32_t k = 0; k < NW; ++k) {
       const uint32_t keep = (2u * k < cnt ? 0xFFFFu : 0u) | (2u * k + 1 < cnt ? 0xFFFF0000u : 0u);
       d[k] = as_us2(as_u32(d[k]) & keep);
     }
@@ -302,15 +340,15 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, con
   const us2 one = {1, 1};
   uint32_t lsum = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) lsum = __builtin_amdgcn_udot2(d[k], one, lsum, false);
+  for (uint32_t k = 0; k < NW; ++k) lsum = __builtin_amdgcn_udot2(d[k], one, lsum, false);
   auto shr_sum = [&](uint32_t f) -> uint32_t {
     const us2 fv = (us2)(unsigned short)f;
     uint32_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc = __builtin_amdgcn_udot2(d[k] >> fv, one, acc, false);
+    for (uint32_t k = 0; k < NW; ++k) acc = __builtin_amdgcn_udot2(d[k] >> fv, one, acc, false);
     return acc;
   };
-  const uint32_t sum = group_sum(lsum, G);
+  const uint32_t sum = gsum<G>(lsum);
 
   // ---- compute_best_split replay (encode.h:43-90) ----
   // start = max(0, bit_width(sum / n) - 2) without a division:
@@ -321,8 +359,8 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, con
     bwq = t + ((n << t) <= sum ? 1u : 0u);
   }
   const uint32_t start = bwq >= 2 ? bwq - 2 : 0u;
-  const uint32_t bits0 = n * (start + 1) + group_sum(shr_sum(start), G);
-  const uint32_t bits1 = n * (start + 2) + group_sum(shr_sum(start + 1), G);
+  const uint32_t bits0 = n * (start + 1) + gsum<G>(shr_sum(start));
+  const uint32_t bits1 = n * (start + 2) + gsum<G>(shr_sum(start + 1));
   int cand, dir;
   uint32_t bits;
   if (bits1 <= bits0) {
@@ -332,10 +370,10 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, con
   }
   bool walking = sb_valid && sum != 0 && bits0 != bits1;
   for (;;) {
-    const bool act = walking && cand > 0 && cand < 14;
+    const bool act = walking && cand > 0 && cand < 14 && !(RPP_EABLATE & 2);
     if (!__any(act)) break;
     const uint32_t f = act ? (uint32_t)(cand + dir) : 0u;
-    const uint32_t t = n * (f + 1) + group_sum(shr_sum(f), G);
+    const uint32_t t = n * (f + 1) + gsum<G>(shr_sum(f));
     if (act && t <= bits) {
       bits = t;
       cand += dir;
@@ -363,11 +401,11 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, con
     emit_bits(st.win, pos, mode == 0 ? 0u : (mode == 1 ? fs + 1 : 15u));
     pos += 4;
   }
-  if (mode == 1) {
+  if (mode == 1 && !(RPP_EABLATE & 1)) {
     const uint32_t lowmask = (1u << fs) - 1u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if ((uint32_t)i < cnt) {
+    for (uint32_t i = 0; i < SPL; ++i) {
+      if (i < cnt) {
         const uint32_t di = (i & 1) ? (as_u32(d[i >> 1]) >> 16) : (as_u32(d[i >> 1]) & 0xFFFFu);
         pos += di >> fs;  // unary zeros are implicit (the window is zeroed)
         emit_bits(st.win, pos, 1u | ((di & lowmask) << 1));
@@ -376,9 +414,9 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, con
     }
   } else if (mode == 2) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if ((uint32_t)i < cnt) {
-        const uint32_t ri = (i & 1) ? (rw[i >> 1] >> 16) : (rw[i >> 1] & 0xFFFFu);
+    for (uint32_t i = 0; i < SPL; ++i) {
+      if (i < cnt) {
+        const uint32_t ri = (i & 1) ? (r.w[i >> 1] >> 16) : (r.w[i >> 1] & 0xFFFFu);
         emit_bits(st.win, pos, ri);  // raw stored value (encode.h:148-151)
         pos += 16;
       }
@@ -390,7 +428,7 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw& r, con
 // Streams whole 64-byte lines out once >= kEncFlushWords are complete.
 __device__ __forceinline__ void enc_flush(EncState& st, bool final_flush) {
   const uint32_t lane = lane_id();
-  __syncthreads();
+  wave_lds_fence();
   const uint32_t full_end = st.base >> 5;  // words before it are complete
   const uint32_t F = full_end & ~15u;
   if (F >= st.win_w0 + kEncFlushWords || (final_flush && F > st.win_w0)) {
@@ -402,23 +440,26 @@ __device__ __forceinline__ void enc_flush(EncState& st, bool final_flush) {
     const uint32_t used = full_end - st.win_w0 + 1;
     const uint32_t tail0 = F - st.win_w0;
     const uint32_t keep = lane < 16 ? st.win[tail0 + lane] : 0u;
-    __syncthreads();
+    wave_lds_fence();
     for (uint32_t i = lane; i < used; i += kWave) st.win[i] = 0;
-    __syncthreads();
+    wave_lds_fence();
     if (lane < 16) st.win[lane] = keep;
-    __syncthreads();
+    wave_lds_fence();
     st.win_w0 = F;
   }
 }
 
+template <uint32_t SPL, uint32_t G, uint32_t CS>
 __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t win[kEncWin];
+  constexpr uint32_t spw = kWave / G;  // sub-blocks per iteration
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
-  const uint32_t bs = p.bs, cs = p.cs, be = p.be, ulsb = p.ulsb;
+  const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
+  const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
   const uint64_t n64 = p.n_samples[b];
   const uint64_t ooff = p.out_off[b];
-  if (n64 % cs != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ooff & 15u)) {
+  if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ooff & 15u)) {
     if (lane == 0) {
       p.status[b] = RPP_INVALID_ARGUMENT;
       p.out_bytes[b] = 0;
@@ -432,53 +473,52 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   for (uint32_t i = lane; i < kEncWin; i += kWave) win[i] = 0;
   __syncthreads();
 
-  EncState st{win, reinterpret_cast<uint32_t*>(out8), 0u, 16 * cs};
+  EncState st{win, reinterpret_cast<uint32_t*>(out8), 0u, 16 * CS, 0u};
   // codec.h:69-74,81-86: 16-bit initial value read(in[i]) per component.
-  if (lane < cs) emit_bits(win, 16 * lane, N ? px_read(in[lane], be, ulsb) : 0u);
+  if (lane < CS) emit_bits(win, 16 * lane, N ? px_read(in[lane], be, ulsb) : 0u);
+  // DPP-prev mode: the first sample is its own reference
+  st.carry = N ? px_read(in[0], be, ulsb) : 0u;
 
-  const uint32_t chunk_len = cs * bs;
+  const uint32_t chunk_len = CS * bs;
   const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
-  const uint32_t nsb = nchunks * cs;
-  const uint32_t m8 = (bs + 7) >> 3;
-  uint32_t G = 1;
-  while (G < m8) G <<= 1;
-  const uint32_t spw = kWave / G;
-  const uint32_t g = lane / G, j = lane & (G - 1);
-  // full iterations: every sub-block complete, lanes own 0 or 8 samples
-  const bool vec_ok = (bs & 7u) == 0 && ((uintptr_t)in & 15u) == 0;
-  const uint32_t nsb_full = vec_ok ? (N / chunk_len) * cs : 0u;
+  const uint32_t nsb = nchunks * CS;
+  const uint32_t g = lane / G, j = lane % G;
+  // full iterations: every sub-block complete, lanes own 0 or SPL samples
+  const bool vec_ok = bs % SPL == 0 && ((uintptr_t)in & 15u) == 0;
+  const uint32_t nsb_full = vec_ok ? (N / chunk_len) * CS : 0u;
   const uint32_t nfull = nsb_full / spw;
-  const bool empty_lanes = G * 8 != bs;
+  const bool empty_lanes = G * SPL != bs;
+  const bool dpp_prev = CS == 1 && !empty_lanes && !(RPP_EABLATE & 4);
 
   // ---- full iterations, double buffered (no register copies between the
   //      load and its use, so the next group's loads stay in flight) ----
   uint32_t it = 0;
   if (nfull) {
-    EncGeom ga = enc_geom(g, j, nsb, N, bs, cs), gb;
-    EncRaw ra = enc_load_vec(in, ga, cs), rb;
+    EncGeom ga = enc_geom<SPL, CS>(g, j, nsb, N, bs), gb;
+    EncRaw<SPL> ra = enc_load_vec<SPL, CS>(in, ga, !dpp_prev), rb;
     for (; it + 1 < nfull; it += 2) {
-      gb = enc_geom((it + 1) * spw + g, j, nsb, N, bs, cs);
-      rb = enc_load_vec(in, gb, cs);
-      enc_iteration(st, ra, ga, G, j, be, ulsb, empty_lanes, cs);
+      gb = enc_geom<SPL, CS>((it + 1) * spw + g, j, nsb, N, bs);
+      rb = enc_load_vec<SPL, CS>(in, gb, !dpp_prev);
+      enc_iteration<SPL, G, CS>(st, ra, ga, j, selbe, be, ulsb, empty_lanes, dpp_prev);
       enc_flush(st, false);
       if (it + 2 < nfull) {
-        ga = enc_geom((it + 2) * spw + g, j, nsb, N, bs, cs);
-        ra = enc_load_vec(in, ga, cs);
+        ga = enc_geom<SPL, CS>((it + 2) * spw + g, j, nsb, N, bs);
+        ra = enc_load_vec<SPL, CS>(in, ga, !dpp_prev);
       }
-      enc_iteration(st, rb, gb, G, j, be, ulsb, empty_lanes, cs);
+      enc_iteration<SPL, G, CS>(st, rb, gb, j, selbe, be, ulsb, empty_lanes, dpp_prev);
       enc_flush(st, false);
     }
     if (it < nfull) {
-      enc_iteration(st, ra, ga, G, j, be, ulsb, empty_lanes, cs);
+      enc_iteration<SPL, G, CS>(st, ra, ga, j, selbe, be, ulsb, empty_lanes, dpp_prev);
       enc_flush(st, false);
       ++it;
     }
   }
   // ---- ragged tail / unaligned streams: per-sample loads ----
   for (uint32_t s0 = it * spw; s0 < nsb; s0 += spw) {
-    const EncGeom geo = enc_geom(s0 + g, j, nsb, N, bs, cs);
-    const EncRaw r = enc_load_scalar(in, geo, cs);
-    enc_iteration(st, r, geo, G, j, be, ulsb, true, 1u);
+    const EncGeom geo = enc_geom<SPL, CS>(s0 + g, j, nsb, N, bs);
+    const EncRaw<SPL> r = enc_load_scalar<SPL, CS>(in, geo);
+    enc_iteration<SPL, G, CS>(st, r, geo, j, selbe, be, ulsb, true, false);
     enc_flush(st, false);
   }
   enc_flush(st, true);
@@ -494,6 +534,24 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
     p.out_bytes[b] = total_bytes;
     p.status[b] = RPP_OK;
   }
+}
+
+// Host-side kernel choice: SPL 16 for bs > 64 (8 sub-blocks of 128 per
+// iteration), else 8; G = next pow2 of ceil(bs / SPL).
+typedef void (*EncKernel)(EncParams);
+template <uint32_t CS>
+EncKernel enc_kernel_for(uint32_t bs) {
+  if (bs > 64) {
+    const uint32_t m = (bs + 15) / 16;
+    if (m <= 8) return rpp_encode_kernel<16, 8, CS>;
+    if (m <= 16) return rpp_encode_kernel<16, 16, CS>;
+    return rpp_encode_kernel<16, 32, CS>;
+  }
+  const uint32_t m = (bs + 7) / 8;
+  if (m <= 1) return rpp_encode_kernel<8, 1, CS>;
+  if (m <= 2) return rpp_encode_kernel<8, 2, CS>;
+  if (m <= 4) return rpp_encode_kernel<8, 4, CS>;
+  return rpp_encode_kernel<8, 8, CS>;
 }
 
 // ===========================================================================
@@ -631,11 +689,6 @@ struct Map8 {
 };
 __device__ __forceinline__ Map8 comp8(Map8 g, Map8 f) {
   return Map8{__builtin_amdgcn_perm(g.hi, g.lo, f.lo), __builtin_amdgcn_perm(g.hi, g.lo, f.hi)};
-}
-template <int Ctrl, int RowMask = 0xF>
-__device__ __forceinline__ uint32_t dpp_keep(uint32_t old, uint32_t v) {
-  // lanes without a source in range keep `old`
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, Ctrl, RowMask, 0xF, false);
 }
 template <int Ctrl, int RowMask = 0xF>
 __device__ __forceinline__ Map8 scan_step8(Map8 m) {
@@ -990,8 +1043,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           const bool ok0 = i0 < m, ok1 = i0 + 1 < m;
           const uint2 tt = *reinterpret_cast<const uint2*>(&list[min(i0, kListDump - 2)]);
           const uint32_t t0 = tt.x, t1 = ok1 ? tt.y : t0;
-          const uint32_t lft = from_left(t1 + k);  // end of code i0 - 1
-          const uint32_t st0 = lane == 0 ? start : lft;
+          const uint32_t st0 = dpp_keep<kDppWaveShr1>(start, t1 + k);  // end of code i0 - 1
           const uint32_t r0 = peek32(t0 + 1) & fmask, r1 = peek32(t1 + 1) & fmask;
           const uint32_t df0 = ((t0 - st0) << fs) | r0, df1 = ((t1 - t0 - k) << fs) | r1;
           const uint32_t d0 = ok0 ? (df0 >> 1) ^ (0u - (df0 & 1u)) : 0u;
@@ -1164,7 +1216,9 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
   EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count};
-  hipLaunchKernelGGL(rpp_encode_kernel, dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
+  const EncKernel k = cfg->component_stream_count == 1 ? enc_kernel_for<1>(cfg->block_size)
+                                                       : enc_kernel_for<2>(cfg->block_size);
+  hipLaunchKernelGGL(k, dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
