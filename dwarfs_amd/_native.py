@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "rpp_worst_case_bytes",
     "rpp_encode_batch",
     "rpp_decode_batch",
+    "rpp_unused_lsb_batch",
     "rpp_frame_header",
     "rpp_parse_frame",
 )
@@ -87,6 +88,8 @@ def lib() -> C.CDLL:
         L.rpp_encode_batch.restype = C.c_int
         L.rpp_decode_batch.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, P]
         L.rpp_decode_batch.restype = C.c_int
+        L.rpp_unused_lsb_batch.argtypes = [P, P, P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P]
+        L.rpp_unused_lsb_batch.restype = C.c_int
         L.rpp_frame_header.argtypes = [C.POINTER(RppFrame), P]
         L.rpp_frame_header.restype = C.c_size_t
         L.rpp_parse_frame.argtypes = [P, C.c_size_t, C.POINTER(RppFrame)]

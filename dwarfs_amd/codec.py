@@ -226,6 +226,39 @@ def decode_batch(
     return out, status
 
 
+def unused_lsb_count_batch(
+    samples: torch.Tensor,
+    offsets: Sequence[int],
+    n_samples: Sequence[int],
+    big_endian: bool = True,
+    stream: Optional[torch.cuda.Stream] = None,
+) -> torch.Tensor:
+    """Unused least-significant bits of 16-bit images, one launch per batch.
+
+    The FITS categorizer's ``get_unused_lsb_count<uint16_t>``
+    (src/writer/categorizer/fits_categorizer.cpp:118-178): the number of
+    trailing zero bits of the OR of all samples of an image (16 for an
+    all-zero or empty image).  Image ``i`` is
+    ``samples[offsets[i] : offsets[i] + n_samples[i]]``.  Returns an int32
+    device tensor of counts.
+    """
+    dev = samples.device
+    n_samples = np.asarray(n_samples, dtype=np.int64)
+    ni = len(n_samples)
+    counts = torch.empty(ni, dtype=torch.int32, device=dev)
+    if ni == 0:
+        return counts
+    d_off = _dev_u64(offsets, dev)
+    d_n = _dev_u64(n_samples, dev)
+    work = torch.empty(ni, dtype=torch.int32, device=dev)
+    st = N.lib().rpp_unused_lsb_batch(
+        C.c_void_p(samples.data_ptr()), C.c_void_p(d_off.data_ptr()), C.c_void_p(d_n.data_ptr()),
+        int(n_samples.max()), ni, 1 if big_endian else 0, C.c_void_p(work.data_ptr()),
+        C.c_void_p(counts.data_ptr()), _stream_ptr(stream))
+    _raise_status(st)
+    return counts
+
+
 class Encoder:
     """``encoder_interface<uint16_t>`` (encoder_interface.h:38-60)."""
 

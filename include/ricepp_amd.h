@@ -20,6 +20,9 @@
  *                            (ricepp/include/ricepp/decoder_interface.h:37-50,
  *                            ricepp/ricepp_cpuspecific.cpp:127-144), called by
  *                            src/compression/ricepp.cpp:215-232
+ *   rpp_unused_lsb_batch  <- the FITS categorizer's unused-LSB detection
+ *                            (src/writer/categorizer/fits_categorizer.cpp:118-178),
+ *                            which picks the codec's unused_lsb_count
  *   rpp_frame_header /    <- the DwarFS block framing of src/compression/ricepp.cpp:
  *   rpp_parse_frame          varint size + thrift-compact ricepp_block_header
  *                            (:107-127 write, :186-201,237-249 read)
@@ -103,6 +106,23 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
                      const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
                      const uint64_t* d_out_offsets, const uint64_t* d_n_samples,
                      int32_t* d_status, void* stream);
+
+/*
+ * Unused least-significant bits of 16-bit images (the FITS categorizer's
+ * get_unused_lsb_count, src/writer/categorizer/fits_categorizer.cpp:118-178):
+ * for each image, the OR of all its samples (converted from big endian when
+ * big_endian != 0) and d_counts[i] = its number of trailing zero bits
+ * (std::countr_zero of a uint16_t: 16 for an all-zero or empty image).
+ *   d_in          stored uint16 samples
+ *   d_offsets     [nimages] first sample of image i
+ *   d_n_samples   [nimages] samples of image i, each <= max_samples
+ *   d_work        [nimages] device scratch (overwritten)
+ *   d_counts      [nimages] written: unused LSB count of image i
+ * Asynchronous on `stream`; nimages <= 65535 per call.
+ */
+int rpp_unused_lsb_batch(const uint16_t* d_in, const uint64_t* d_offsets, const uint64_t* d_n_samples,
+                         uint64_t max_samples, uint32_t nimages, uint32_t big_endian, uint32_t* d_work,
+                         uint32_t* d_counts, void* stream);
 
 /*
  * DwarFS ricepp block framing (host memory).  rpp_frame_header writes

@@ -150,3 +150,16 @@ def frame_header(uncompressed_bytes, block_size, component_count, bytes_per_samp
     n = lib().rpo_frame_header(_p(out), uncompressed_bytes, block_size, component_count, bytes_per_sample, ulsb,
                                1 if big_endian else 0, version)
     return out[:n].tobytes()
+
+
+def unused_lsb_count(samples: np.ndarray, big_endian: bool = True) -> int:
+    """get_unused_lsb_count<uint16_t> (src/writer/categorizer/fits_categorizer.cpp:
+    118-178): std::countr_zero of the OR of all samples (after the big-endian
+    conversion of :161), 16 for an all-zero or empty image."""
+    a = np.asarray(samples, dtype=np.uint16)
+    b16 = int(np.bitwise_or.reduce(a)) if a.size else 0
+    if big_endian:
+        b16 = ((b16 >> 8) | (b16 << 8)) & 0xFFFF
+    if b16 == 0:
+        return 16
+    return (b16 & -b16).bit_length() - 1
