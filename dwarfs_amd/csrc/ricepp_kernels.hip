@@ -35,7 +35,8 @@
 
 // Diagnostic builds only: -DRPP_ABLATE=<mask> removes decode phases to time
 // them (outputs are then wrong): 1 flush, 2 extraction, 4 async ring refill,
-// 8 output stores.
+// 8 output stores; fast loop: 32 everything after the parse (pairs, deltas,
+// stores), 64 output stores.
 #ifndef RPP_ABLATE
 #define RPP_ABLATE 0
 #endif
@@ -696,6 +697,42 @@ __device__ __forceinline__ Map8 scan_step8(Map8 m) {
   return comp8(m, d);
 }
 
+// The same step in one instruction per dword: v_cndmask_b32 with the DPP
+// source as its false operand -- lanes in the constant lane mask (those
+// without a source: identity) take the identity map held in id (two VGPRs
+// loaded once), the rest the map from the left; out-of-range sources read 0
+// (bound_ctrl) and are always masked.  Saves the per-step identity moves a
+// DPP move into a fresh `old` needs.
+#define RPP_SCAN8_STEP(NAME, CTRL, MASK)                                                                  \
+  __device__ __forceinline__ Map8 NAME(Map8 m, Map8 id) {                                                 \
+    Map8 d;                                                                                               \
+    asm("s_mov_b64 vcc, %6\n\ts_nop 0\n\t"                                                                \
+        "v_cndmask_b32_dpp %0, %2, %4, vcc " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"          \
+        "v_cndmask_b32_dpp %1, %3, %5, vcc " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1"              \
+        : "=&v"(d.lo), "=&v"(d.hi)                                                                        \
+        : "v"(m.lo), "v"(m.hi), "v"(id.lo), "v"(id.hi), "s"((uint64_t)(MASK))                           \
+        : "vcc");                                                                                         \
+    return comp8(m, d);                                                                                   \
+  }
+RPP_SCAN8_STEP(scan8_shr1, "row_shr:1", 0x0001000100010001ull)
+RPP_SCAN8_STEP(scan8_shr2, "row_shr:2", 0x0003000300030003ull)
+RPP_SCAN8_STEP(scan8_shr4, "row_shr:4", 0x000F000F000F000Full)
+RPP_SCAN8_STEP(scan8_shr8, "row_shr:8", 0x00FF00FF00FF00FFull)
+RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", 0x0000FFFF0000FFFFull)
+RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", 0x00000000FFFFFFFFull)
+#undef RPP_SCAN8_STEP
+// exclusive form: the map of lanes 0..l-1 (identity on lane 0)
+__device__ __forceinline__ Map8 shift8_wave(Map8 m, Map8 id) {
+  Map8 d;
+  asm("s_mov_b64 vcc, 1\n\ts_nop 0\n\t"
+      "v_cndmask_b32_dpp %0, %2, %4, vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_cndmask_b32_dpp %1, %3, %5, vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=&v"(d.lo), "=&v"(d.hi)
+      : "v"(m.lo), "v"(m.hi), "v"(id.lo), "v"(id.hi)
+      : "vcc");
+  return d;
+}
+
 // 16-entry maps (states 0..15) for fs >= 8.
 struct Map16 {
   uint32_t w[4];
@@ -739,6 +776,15 @@ __device__ __forceinline__ void glds4(const void* gsrc, uint32_t m0) {
                : "=&s"(keep) : "v"(gsrc), "s"(m0) : "memory");
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Waits for all but the last `after` vector-memory instructions (vmcnt
+// decrements in issue order on gfx9), bucketed to a few immediates; a lower
+// count only waits longer.
+__device__ __forceinline__ void vm_wait_all_but(uint32_t after) {
+  if (after >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (after >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (after >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
@@ -816,9 +862,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   //      path (start-up, the zero-padded tail, long sub-blocks). ----
   uint32_t fill_w = 0;
   bool pend = false;  // a requested chunk is in flight
+  // vector-memory instructions known to be issued after the pending request
+  // (the fast loop's output stores; elsewhere reset to 0 = unknown), so that
+  // retiring it need not wait for the stores
+  uint32_t vm_after = 0;
   auto retire = [&]() {
     if (pend) {
-      vm_drain();
+      vm_wait_all_but(vm_after);
       fill_w += kChunkWords;
       pend = false;
     }
@@ -850,6 +900,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
     if ((fill_w & kRingMask) == 0)  // the mirror of words 0..63
       glds4(src + 4u * lane, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[kRingWords]));
     pend = true;
+    vm_after = 0;
   };
   refill_sync();
   refill_sync();
@@ -888,100 +939,174 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   };
   // keep the look-ahead: retire the pending chunk once it is needed soon;
   // request the next once the look-ahead drops below 766 words (it
-  // overwrites words [fill_w - 1024, fill_w - 768), all below P >> 5)
-  auto ring_keep = [&]() {
-    if (pend && fill_w < (P >> 5) + kAhead + 128) retire();
-    if (!(RPP_ABLATE & 4) && !pend && fill_w <= (P >> 5) + 766) request();
+  // overwrites words [fill_w - 1024, fill_w - 768), all below q >> 5, the
+  // next bit to be read)
+  auto ring_keep = [&](uint32_t q) {
+    if (pend && fill_w < (q >> 5) + kAhead + 128) retire();
+    if (!(RPP_ABLATE & 4) && !pend && fill_w <= (q >> 5) + 766) request();
   };
   const uint32_t nsb = nchunks * CS;
   // sub-blocks the fast loop may take: those of full 128-sample chunks
-  const uint32_t nsb_fast = bs == 2 * kWave ? (N / chunk_len) * CS : 0u;
-  const bool dw = CS == 1 && (((uintptr_t)out) & 3u) == 0;  // 2-sample stores are dword aligned
+  // (CS 1: the 2-sample stores must be dword aligned)
+  const uint32_t nsb_fast =
+      bs == 2 * kWave && (CS == 2 || (((uintptr_t)out) & 3u) == 0) ? (N / chunk_len) * CS : 0u;
+  // the stream's output as a raw buffer (N * 2 < 2^28 bytes; stores past it are dropped)
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(2 * N), 0x00020000);
+  Map8 vid{kId0, kId1};  // the identity map, kept in VGPRs for the scan steps
+  asm volatile("" : "+v"(vid.lo), "+v"(vid.hi));
 
   for (uint32_t s = 0; s < nsb && status == RPP_OK; ++s) {
     // ---- fast loop (the common case): Rice sub-blocks of 128 codes with fs
-    //      5..7 that lie in one window, ring already resident.  Straight-line
-    //      code: at most 4 terminators per 24-bit segment (codes are >= 6
-    //      bits), every lane owns exactly 2 codes.  Anything else leaves the
-    //      loop and takes the general path below for that sub-block. ----
-    for (; s < nsb_fast; ++s) {
-      if (fill_w < (P >> 5) + kAhead || P + 4 > lim) break;
-      const uint32_t comp = s % CS;
-      uint16_t* dst = out + (s / CS) * chunk_len + comp;
-      uint32_t xl, xh;
-      load_x(P + kSegBits * lane, xl, xh);
-      const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
-      if (fsp1 - 6u > 2u) break;
-      const uint32_t fs = fsp1 - 1, k = fsp1, fmask = (1u << fs) - 1u;
-      const uint32_t n = 2 * kWave, P4 = P + 4;
-      const uint4* tb = tab + 256u * fs;
-      const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
-                  e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
-      Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
-      M = scan_step8<kDppRowShr1>(M);
-      M = scan_step8<kDppRowShr2>(M);
-      M = scan_step8<kDppRowShr4>(M);
-      M = scan_step8<kDppRowShr8>(M);
-      M = scan_step8<kDppRowBcast15, 0xA>(M);
-      M = scan_step8<kDppRowBcast31, 0xC>(M);
-      const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
-      // state 4 at the window start: skip the header
-      uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 4u | kSelByte0) | kSelByte0;
-      const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-      sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
-      const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
-      sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
-      const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
-      uint32_t tm = a0 | (a1 << 8) | (a2 << 16);
-      const uint32_t cnt = __builtin_popcount(tm);
-      const uint32_t incl = wave_incl_sum(cnt);
-      const uint64_t finm = __ballot(incl >= n);
-      if (!finm) break;
-      const uint32_t excl = incl - cnt;
-      const uint32_t mine = n > excl ? min(cnt, n - excl) : 0u;
-      const uint32_t sb = P + kSegBits * lane;
-      const uint32_t rsel = n - 1 - excl;  // code n-1, in the lane holding it
-      // (terminator position, remainder) of code i -> list pair i
-      uint2* lp = reinterpret_cast<uint2*>(list) + excl;
-      uint32_t ecand = 0;
+    //      5..7 that lie in one window, ring resident.  Straight-line code: at
+    //      most 4 terminators per 24-bit segment (codes are >= 6 bits), every
+    //      lane owns exactly 2 codes.  Software-pipelined: while sub-block s is
+    //      turned into samples, sub-block s+1 is parsed (ring read, table
+    //      lookups, scans) in the same basic block, so the LDS latencies and
+    //      DPP chains of the two overlap.  Anything else leaves the loop and
+    //      takes the general path below for that sub-block. ----
+    if (s < nsb_fast && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
+      constexpr uint32_t n = 2 * kWave;
+      const uint4* const list4 = reinterpret_cast<const uint4*>(list);
+      uint2* const list2 = reinterpret_cast<uint2*>(list);
+      // this lane's 32 bits from bit q + 24 lane (its 24-bit segment and 8
+      // more: a terminator in the segment has its <= 7 remainder bits in them)
+      auto seg_bits = [&](uint32_t q) {
+        const uint32_t sb = q + kSegBits * lane;
+        const uint32_t* w = wptr(sb >> 5);
+        return __builtin_amdgcn_alignbit(w[1], w[0], sb & 31u);
+      };
+      // the header's fs clamped to 5..7, so the lookups stay in range for
+      // any header; the fast loop only keeps sub-blocks whose fs is in range
+      auto fs_of = [](uint32_t h) { return min(max(h & 15u, 6u), 8u) - 1u; };
+      auto header_ok = [](uint32_t h) { return (h & 15u) - 6u <= 2u; };
+      // Parse of the sub-block at bit q: entry states by the map scan,
+      // terminators, (a_i, remainder) of code i into list pair i with a_i =
+      // terminator position - i k (the unary part of code i is then a_i -
+      // a_(i-1), a_(-1) = q + 4).  Returns whether the sub-block ends in the
+      // window, and its end (the header of the next) in Pe.
+      auto parse = [&](uint32_t q, uint32_t xl, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
+        const uint32_t k = fs + 1;
+        Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
+        M = scan8_shr1(M, vid);
+        M = scan8_shr2(M, vid);
+        M = scan8_shr4(M, vid);
+        M = scan8_shr8(M, vid);
+        M = scan8_bc15(M, vid);
+        M = scan8_bc31(M, vid);
+        const Map8 X = shift8_wave(M, vid);
+        // state 4 at the window start: skip the header
+        uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 4u | kSelByte0) | kSelByte0;
+        const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+        sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+        const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+        sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+        const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+        uint32_t tm = a0 | (a1 << 8) | (a2 << 16);
+        const uint32_t cnt = __builtin_popcount(tm);
+        const uint32_t incl = wave_incl_sum(cnt);
+        const uint64_t finm = __ballot(incl >= n);
+        const uint32_t excl = incl - cnt;
+        // terminator positions t0 < t1 < t2 < t3 in the segment (garbage
+        // past cnt)
+        uint32_t t[4];
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t t = ffbl(tm);
-        tm &= tm - 1;
-        const uint32_t tg = sb + t;
-        const uint32_t rem = __builtin_amdgcn_alignbit(xh, xl, t + 1) & fmask;
-        *(j < mine ? lp + j : reinterpret_cast<uint2*>(list) + kListDump / 2) = make_uint2(tg, rem);
-        ecand = j == rsel ? tg : ecand;
+        for (uint32_t j = 0; j < 4; ++j) {
+          t[j] = ffbl(tm);
+          tm &= tm - 1;
+        }
+        // the next sub-block starts after code n-1's remainder: terminator
+        // n-1-excl of the first lane whose inclusive count reaches n
+        // (positions <= 23 packed in bytes and picked by one bit-field
+        // extract: no selects, no branches)
+        const uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
+        const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (n - 1 - excl), 8);
+        const uint32_t lz = finm ? (uint32_t)__builtin_ctzll(finm) : 0u;
+        Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
+        // pair excl + j for j = 3 .. 0, one instruction each (kept apart: a
+        // merged ds_write2 would put two j in one instruction): a slot past
+        // this lane's codes belongs to a later lane, which writes it in a
+        // later instruction (its j is smaller); lanes without terminators
+        // write the unused pairs 256..259
+        const uint32_t base = cnt ? excl : 256u;
+        const uint32_t sb = q + kSegBits * lane;
+        uint32_t abase = sb - __umul24(base, k);
+        asm volatile("" : "+v"(abase));  // computed once, not per pair
+        const uint32_t xr = xl >> 1;     // the remainder of a terminator at t is bits t+1 .. t+fs
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          list2[base + j] = make_uint2(abase + t[j] - j * k, __builtin_amdgcn_ubfe(xr, t[j], fs));
+          lds_fence();
+        }
+        return finm != 0;
+      };
+      // codes 2c, 2c+1 of sub-block sx (at bit q) on lane c -> zig-zag deltas
+      // (decode.h:66-69) -> values -> stored samples
+      auto extract = [&](uint4 tt, uint32_t q, uint32_t fs, uint32_t sx) {
+        const uint32_t lft = dpp_keep<kDppWaveShr1>(q + 4, tt.z);  // a of code 2c-1
+        const uint32_t df0 = ((tt.x - lft) << fs) | tt.y, df1 = ((tt.z - tt.x) << fs) | tt.w;
+        const uint32_t d0 = (df0 >> 1) ^ (0u - (df0 & 1u)), d1 = (df1 >> 1) ^ (0u - (df1 & 1u));
+        const uint32_t inc = wave_incl_sum(d0 + d1);
+        const uint32_t comp = sx % CS;
+        const uint32_t lastc = comp ? last1 : last0;
+        const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (mod 2^16)
+        const uint32_t o = px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb);
+        if (!(RPP_ABLATE & 64)) {
+          // buffer stores: scalar base + 32-bit lane offset
+          if constexpr (CS == 1) {
+            __builtin_amdgcn_raw_buffer_store_b32(o, orsrc, 4 * lane, (int)(sx * (2 * n)), 0);
+            vm_after += 1;
+          } else {
+            const int sbase = (int)(2 * ((sx / CS) * chunk_len + comp));
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, 4 * CS * lane, sbase, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(o >> 16), orsrc, 4 * CS * lane + 2 * CS, sbase, 0);
+            vm_after += 2;
+          }
+        }
+        const uint32_t lnew = (lastc + wave_last(inc)) & 0xFFFFu;
+        if (comp) last1 = lnew;
+        else last0 = lnew;
+      };
+      auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2) {
+        const uint4* tb = tab + 256u * fs;
+        e0 = tb[xl & 0xFFu];
+        e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
+        e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+      };
+
+      // prologue: parse sub-block s
+      uint32_t Pn;
+      uint32_t xl = seg_bits(P);
+      const uint32_t h = __builtin_amdgcn_readfirstlane(xl);
+      uint32_t fs = fs_of(h);
+      uint4 e0, e1, e2;
+      lookups(xl, fs, e0, e1, e2);
+      bool ok = parse(P, xl, fs, e0, e1, e2, Pn) && header_ok(h);
+      while (ok) {
+        // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
+        const bool nxt = s + 1 < nsb_fast && fill_w >= (Pn >> 5) + kAhead && Pn + 4 <= lim;
+        const uint32_t xlB = seg_bits(Pn);
+        const uint4 tt = list4[lane];
+        const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
+        const uint32_t fsB = fs_of(hB);
+        lookups(xlB, fsB, e0, e1, e2);
+        extract(tt, P, fs, s);
+        uint32_t PnB;
+        ok = parse(Pn, xlB, fsB, e0, e1, e2, PnB) && header_ok(hB) && nxt;
+        ++s;
+        P = Pn;
+        if (P > lim) {
+          status = RPP_TRUNCATED_INPUT;
+          break;
+        }
+        if (!ok) break;
+        Pn = PnB;
+        fs = fsB;
+        ring_keep(Pn);
       }
-      lds_fence();
-      // codes 2c, 2c+1 on lane c -> zig-zag deltas (decode.h:66-69) -> values
-      const uint4 tt = reinterpret_cast<const uint4*>(list)[lane];
-      const uint32_t lft = dpp_keep<kDppWaveShr1>(P4 - k, tt.z);  // terminator of code 2c-1
-      const uint32_t df0 = ((tt.x - lft - k) << fs) | tt.y, df1 = ((tt.z - tt.x - k) << fs) | tt.w;
-      const uint32_t d0 = (df0 >> 1) ^ (0u - (df0 & 1u)), d1 = (df1 >> 1) ^ (0u - (df1 & 1u));
-      const uint32_t inc = wave_incl_sum(d0 + d1);
-      const uint32_t lastc = comp ? last1 : last0;
-      const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (mod 2^16)
-      const uint32_t o = px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb);
-      if (dw) {
-        *reinterpret_cast<uint32_t*>(dst + 2 * lane) = o;
-      } else {
-        dst[CS * 2 * lane] = (uint16_t)o;
-        dst[CS * (2 * lane + 1)] = (uint16_t)(o >> 16);
-      }
-      const uint32_t lnew = (lastc + wave_last(inc)) & 0xFFFFu;
-      if (comp) last1 = lnew;
-      else last0 = lnew;
-      // the next sub-block starts after code n-1's remainder
-      P = readlane(ecand, (int)__builtin_ctzll(finm)) + k;
-      if (P > lim) {
-        status = RPP_TRUNCATED_INPUT;
-        break;
-      }
-      ring_keep();
     }
     if (s >= nsb || status != RPP_OK) break;
     // ---- general path: one sub-block of any kind ----
+    vm_after = 0;
     const uint32_t comp = s % CS;
     const uint32_t cbase = (s / CS) * chunk_len;
     const uint32_t n = min(N - cbase, chunk_len) / CS;  // samples per component sub-block
@@ -1157,7 +1282,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       }
     }
     RPP_TSTAMP(14);
-    ring_keep();
+    ring_keep(P);
   }
   retire();
   if (lane == 0) p.status[b] = status;
