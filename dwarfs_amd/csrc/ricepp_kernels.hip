@@ -36,7 +36,9 @@
 // Diagnostic builds only: -DRPP_ABLATE=<mask> removes decode phases to time
 // them (outputs are then wrong): 1 flush, 2 extraction, 4 async ring refill,
 // 8 output stores; fast loop: 32 everything after the parse (pairs, deltas,
-// stores), 64 output stores.
+// stores), 64 output stores; pipelined loop: 256 count scan, 512
+// extraction, 1024 / 4096 / 32768 20 extra v_nop / v_add / v_perm, 2048 20
+// s_nop, 8192 / 16384 an extra random / linear table read.
 #ifndef RPP_ABLATE
 #define RPP_ABLATE 0
 #endif
@@ -103,6 +105,7 @@ constexpr int kDppRowShr2 = 0x112;
 constexpr int kDppRowShr4 = 0x114;
 constexpr int kDppRowShr8 = 0x118;
 constexpr int kDppWaveShr1 = 0x138;
+constexpr int kDppWaveRor1 = 0x13C;
 constexpr int kDppRowMirror = 0x140;
 constexpr int kDppRowHalfMirror = 0x141;
 constexpr int kDppRowBcast15 = 0x142;
@@ -786,6 +789,19 @@ __device__ __forceinline__ void vm_wait_all_but(uint32_t after) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// (a << s) | b in one v_lshl_or_b32 (s uniform)
+__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t sh, uint32_t b) {
+  uint32_t r;
+  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(sh), "v"(b));
+  return r;
+}
+// -(x & 1) in one v_bfe_i32
+__device__ __forceinline__ uint32_t neg_lsb(uint32_t x) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
   uint32_t r;
@@ -804,7 +820,8 @@ __device__ __forceinline__ uint32_t stream_word(const uint8_t* in, uint32_t nbyt
   return v;
 }
 
-template <uint32_t CS>
+// SH: unused_lsb_count != 0 (the pixel write shifts)
+template <uint32_t CS, bool SH>
 __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
   // ---- the transfer tables, one copy per workgroup ----
@@ -816,10 +833,16 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint4* tab = dsm;
   const uint32_t lane = lane_id();
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + kMapEntries) + wv * kWaveLdsWords;
+  // (one opaque scalar word offset, so that ring addresses fold into one
+  // scalar base)
+  uint32_t ring_w = kTabBytes / 4 + wv * kWaveLdsWords;
+  asm("" : "+s"(ring_w));
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + ring_w;
   uint32_t* list = ring + kRingWords + kRingPad;  // terminator positions of the current sub-block
   const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
+  const uint32_t selpack = be ? 0x04050001u : 0x05040100u;  // v_perm(hi, lo): pack two samples (+ swap)
+  const uint32_t lane24 = kSegBits * lane, lane24m4 = lane24 - 4u;
   const uint32_t b = blockIdx.x * p.waves + wv;
   if (b >= p.nblocks) return;  // no barrier below this point
 #ifdef RPP_STATS
@@ -970,19 +993,29 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       uint2* const list2 = reinterpret_cast<uint2*>(list);
       // this lane's 32 bits from bit q + 24 lane (its 24-bit segment and 8
       // more: a terminator in the segment has its <= 7 remainder bits in them)
+      // (window start word and bit offset are scalar; the lane's words lie
+      // within 50 words of the window start, inside the ring's mirror)
       auto seg_bits = [&](uint32_t q) {
-        const uint32_t sb = q + kSegBits * lane;
-        const uint32_t* w = wptr(sb >> 5);
-        return __builtin_amdgcn_alignbit(w[1], w[0], sb & 31u);
+        const uint32_t o = lane24 + (q & 31u);
+        const uint32_t* w = ring + ((q >> 5) & kRingMask) + (o >> 5);
+        return __builtin_amdgcn_alignbit(w[1], w[0], o);  // (shift o mod 32)
       };
-      // the header's fs clamped to 5..7, so the lookups stay in range for
-      // any header; the fast loop only keeps sub-blocks whose fs is in range
-      auto fs_of = [](uint32_t h) { return min(max(h & 15u, 6u), 8u) - 1u; };
+      // the header's fs clamped to 5..7 (scalar), so the lookups stay in
+      // range for any header; the fast loop only keeps sub-blocks whose fs
+      // is in range
+      auto fs_of = [](uint32_t h) {
+        uint32_t r;
+        asm("s_and_b32 %0, %1, 15\n\ts_max_u32 %0, %0, 6\n\ts_min_u32 %0, %0, 8\n\ts_sub_u32 %0, %0, 1"
+            : "=&s"(r)
+            : "s"(h)
+            : "scc");
+        return r;
+      };
       auto header_ok = [](uint32_t h) { return (h & 15u) - 6u <= 2u; };
       // Parse of the sub-block at bit q: entry states by the map scan,
       // terminators, (a_i, remainder) of code i into list pair i with a_i =
-      // terminator position - i k (the unary part of code i is then a_i -
-      // a_(i-1), a_(-1) = q + 4).  Returns whether the sub-block ends in the
+      // terminator position - (q + 4) - i k (the unary part of code i is then
+      // a_i - a_(i-1), a_(-1) = 0).  Returns whether the sub-block ends in the
       // window, and its end (the header of the next) in Pe.
       auto parse = [&](uint32_t q, uint32_t xl, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
         const uint32_t k = fs + 1;
@@ -994,18 +1027,26 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         M = scan8_bc15(M, vid);
         M = scan8_bc31(M, vid);
         const Map8 X = shift8_wave(M, vid);
-        // state 4 at the window start: skip the header
-        uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 4u | kSelByte0) | kSelByte0;
+        RPP_TSTAMP(3);
+        // state 4 at the window start: skip the header.  The selectors
+        // carry the state in byte 0 and 0xFF (a v_perm selector for 0xFF)
+        // in bytes 1-3, so each byte's next state comes out of its v_perm
+        // as the next selector, with no masking.
+        uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
         const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-        sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+        sel = __builtin_amdgcn_perm(e0.y, e0.x, sel);
         const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
-        sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+        sel = __builtin_amdgcn_perm(e1.y, e1.x, sel);
         const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
-        uint32_t tm = a0 | (a1 << 8) | (a2 << 16);
-        const uint32_t cnt = __builtin_popcount(tm);
-        const uint32_t incl = wave_incl_sum(cnt);
+        // terminator mask: byte 0 of a0, a1, a2 -> bytes 0, 1, 2
+        uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
+        const uint32_t tm0 = tm;
+        uint32_t cnt = __builtin_popcount(tm);
+        asm volatile("" : "+v"(cnt));  // keeps the scan's first step a plain DPP add
+        const uint32_t incl = (RPP_ABLATE & 256) ? cnt + 2 * lane : wave_incl_sum(cnt);
         const uint64_t finm = __ballot(incl >= n);
         const uint32_t excl = incl - cnt;
+        RPP_TSTAMP(7);
         // terminator positions t0 < t1 < t2 < t3 in the segment (garbage
         // past cnt)
         uint32_t t[4];
@@ -1015,21 +1056,23 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           tm &= tm - 1;
         }
         // the next sub-block starts after code n-1's remainder: terminator
-        // n-1-excl of the first lane whose inclusive count reaches n
-        // (positions <= 23 packed in bytes and picked by one bit-field
-        // extract: no selects, no branches)
-        const uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
-        const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (n - 1 - excl), 8);
+        // n-1-excl (0..3) of the first lane whose inclusive count reaches n
+        // (scalar work)
         const uint32_t lz = finm ? (uint32_t)__builtin_ctzll(finm) : 0u;
-        Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
+        uint32_t z = readlane(tm0, (int)lz);
+        const uint32_t zr = n - 1 - readlane(excl, (int)lz);
+        z &= zr > 0 ? z - 1 : ~0u;
+        z &= zr > 1 ? z - 1 : ~0u;
+        z &= zr > 2 ? z - 1 : ~0u;
+        Pe = q + kSegBits * lz + (uint32_t)__builtin_ctz(z | 0x80000000u) + k;
+        RPP_TSTAMP(8);
         // pair excl + j for j = 3 .. 0, one instruction each (kept apart: a
         // merged ds_write2 would put two j in one instruction): a slot past
         // this lane's codes belongs to a later lane, which writes it in a
         // later instruction (its j is smaller); lanes without terminators
         // write the unused pairs 256..259
         const uint32_t base = cnt ? excl : 256u;
-        const uint32_t sb = q + kSegBits * lane;
-        uint32_t abase = sb - __umul24(base, k);
+        uint32_t abase = (uint32_t)((int)lane24m4 + __mul24((int)base, -(int)k));
         asm volatile("" : "+v"(abase));  // computed once, not per pair
         const uint32_t xr = xl >> 1;     // the remainder of a terminator at t is bits t+1 .. t+fs
 #pragma unroll
@@ -1037,19 +1080,26 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           list2[base + j] = make_uint2(abase + t[j] - j * k, __builtin_amdgcn_ubfe(xr, t[j], fs));
           lds_fence();
         }
+        RPP_TSTAMP(13);
         return finm != 0;
       };
       // codes 2c, 2c+1 of sub-block sx (at bit q) on lane c -> zig-zag deltas
       // (decode.h:66-69) -> values -> stored samples
-      auto extract = [&](uint4 tt, uint32_t q, uint32_t fs, uint32_t sx) {
-        const uint32_t lft = dpp_keep<kDppWaveShr1>(q + 4, tt.z);  // a of code 2c-1
-        const uint32_t df0 = ((tt.x - lft) << fs) | tt.y, df1 = ((tt.z - tt.x) << fs) | tt.w;
-        const uint32_t d0 = (df0 >> 1) ^ (0u - (df0 & 1u)), d1 = (df1 >> 1) ^ (0u - (df1 & 1u));
+      auto extract = [&](uint4 tt, uint32_t fs, uint32_t sx) {
+        // a of code 2c-1: lane c-1's tt.z by a wave rotate (a wave_shr
+        // leaves lane 0 unwritten instead of reading 0, so it cannot be
+        // fused into the subtraction); lane 0 takes a_(-1) = 0
+        const uint32_t u0 = tt.x - dpp<kDppWaveRor1>(tt.z);
+        const uint32_t df0 = lshl_or(lane ? u0 : tt.x, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
+        const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0), d1 = (df1 >> 1) ^ neg_lsb(df1);
         const uint32_t inc = wave_incl_sum(d0 + d1);
         const uint32_t comp = sx % CS;
         const uint32_t lastc = comp ? last1 : last0;
         const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (mod 2^16)
-        const uint32_t o = px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb);
+        // samples 2c (low), 2c+1 (high) in stored order: pack and byte-swap
+        // in one v_perm when there is no shift
+        const uint32_t o = SH ? px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb)
+                              : __builtin_amdgcn_perm(v1, v1 - d1, selpack);
         if (!(RPP_ABLATE & 64)) {
           // buffer stores: scalar base + 32-bit lane offset
           if constexpr (CS == 1) {
@@ -1087,9 +1137,32 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t xlB = seg_bits(Pn);
         const uint4 tt = list4[lane];
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
+        RPP_TSTAMP(1);
+        RPP_STAT(0, 1);
         const uint32_t fsB = fs_of(hB);
         lookups(xlB, fsB, e0, e1, e2);
-        extract(tt, P, fs, s);
+        if (!(RPP_ABLATE & 512)) extract(tt, fs, s);
+        if (RPP_ABLATE & 1024) asm volatile(".rept 20\n\tv_nop\n\t.endr" ::: "memory");
+        if (RPP_ABLATE & 2048) asm volatile(".rept 20\n\ts_nop 0\n\t.endr" ::: "memory");
+        if (RPP_ABLATE & 4096) {  // 20 independent integer VALU ops
+          uint32_t d0 = lane, d1 = lane + 1, d2 = lane + 2, d3 = lane + 3;
+          asm volatile(".rept 5\n\tv_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1\n\t.endr"
+                       : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+        }
+        if (RPP_ABLATE & 32768) {  // 20 independent v_perm
+          uint32_t d0 = lane, d1 = lane + 1, d2 = lane + 2, d3 = lane + 3;
+          asm volatile(".rept 5\n\tv_perm_b32 %0, %0, %1, %2\n\tv_perm_b32 %1, %1, %2, %3\n\tv_perm_b32 %2, %2, %3, %0\n\tv_perm_b32 %3, %3, %0, %1\n\t.endr"
+                       : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+        }
+        if (RPP_ABLATE & 8192) {  // one extra random table read
+          const uint4 x = tab[256u * fsB + ((xlB >> 4) & 0xFFu)];
+          asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w));
+        }
+        if (RPP_ABLATE & 16384) {  // one extra conflict-free read
+          const uint4 x = tab[256u * fsB + lane];
+          asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w));
+        }
+        RPP_TSTAMP(2);
         uint32_t PnB;
         ok = parse(Pn, xlB, fsB, e0, e1, e2, PnB) && header_ok(hB) && nxt;
         ++s;
@@ -1102,6 +1175,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         Pn = PnB;
         fs = fsB;
         ring_keep(Pn);
+        RPP_TSTAMP(15);
       }
     }
     if (s >= nsb || status != RPP_OK) break;
@@ -1361,24 +1435,22 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
   if (const char* e = getenv("RICEPP_DEC_WAVES")) W = std::min<uint32_t>(kDecMaxWaves, std::max(1, atoi(e)));  // diagnostics
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
+  static void (*const kernels[4])(DecParams) = {rpp_decode_kernel<1, false>, rpp_decode_kernel<1, true>,
+                                                 rpp_decode_kernel<2, false>, rpp_decode_kernel<2, true>};
   static std::once_flag attr_once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(attr_once, [] {
     const int mx = (int)(kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4);
-    attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&rpp_decode_kernel<1>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    if (attr_err == hipSuccess)
-      attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&rpp_decode_kernel<2>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    for (auto k : kernels)
+      if (attr_err == hipSuccess)
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   });
   if (attr_err != hipSuccess) return RPP_HIP_ERROR;
   DecParams p{d_in, d_in_offsets, d_in_bytes, d_out, d_out_offsets, d_n_samples, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count, W};
-  if (cfg->component_stream_count == 1)
-    hipLaunchKernelGGL(rpp_decode_kernel<1>, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
-  else
-    hipLaunchKernelGGL(rpp_decode_kernel<2>, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
+  const auto k = kernels[2 * (cfg->component_stream_count - 1) + (cfg->unused_lsb_count ? 1 : 0)];
+  hipLaunchKernelGGL(k, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 

@@ -1,5 +1,6 @@
 """Diagnostic: runs the bench workload against the -DRPP_STATS build and
-prints per-sub-block loop trip counts.  Build: tools/build_stats.sh"""
+prints the per-slot phase cycles per fast-loop iteration (slot 0 counts the
+iterations).  Build: tools/build_stats.sh.  Usage: python tools/stats_run.py [nblocks] [waves]"""
 import ctypes as C
 import os
 import sys
@@ -7,6 +8,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 os.environ["RICEPP_AMD_LIB"] = str(ROOT / "dwarfs_amd" / "lib" / "libricepp_amd_stats.so")
+nblocks = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+if len(sys.argv) > 2:
+    os.environ["RICEPP_DEC_WAVES"] = sys.argv[2]
 sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -15,7 +19,7 @@ from dwarfs_amd import _native, codec, parallel  # noqa: E402
 
 L = _native.lib()
 L.rpp_stats_fetch.argtypes = [C.c_void_p, C.c_int]
-nblocks, n = 4096, 32768
+n = 32768
 x = make_poisson_blocks(nblocks, n, 1000.0, 42, torch.device("cuda:0"))
 pipe = parallel.ShardPipeline(codec.CodecConfig(128, 1, "big", 0), x, np.arange(nblocks) * n, np.full(nblocks, n))
 pipe.encode()
@@ -26,9 +30,8 @@ pipe.decode()
 torch.cuda.synchronize()
 pipe.check(x)
 L.rpp_stats_fetch(st.ctypes.data, 1)
-names = ["windows", "-", "-", "-", "t_looptop", "t_ensure",
-         "subblocks", "t_load+header", "-", "t_zero/raw", "t_lookup", "t_maps+terms", "t_count+extract", "-",
-         "t_winend", "t_flush+request"]
-sb = float(st[6])
-for i, nm in enumerate(names):
-    print(f"{nm:20s} total={int(st[i]):12d}  per_subblock={st[i] / sb:8.3f}")
+it = float(st[0])
+print(f"nblocks {nblocks} waves {os.environ.get('RICEPP_DEC_WAVES', 'auto')}: fast iterations {int(it)}")
+for i in range(1, 16):
+    if st[i]:
+        print(f"slot {i:2d} cycles/iteration {st[i] / it:8.1f}")
