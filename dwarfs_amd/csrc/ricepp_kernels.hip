@@ -290,6 +290,14 @@ __device__ __forceinline__ void emit_bits(uint32_t* win, uint32_t rel, uint32_t 
   atomicOr(&win[w + 1], (v >> 1) >> (31u - sh));
 }
 
+// The same for codes of <= 32 bits by one 64-bit shift.
+__device__ __forceinline__ void emit_bits64(uint32_t* win, uint32_t rel, uint32_t v) {
+  const uint64_t x = (uint64_t)v << (rel & 31u);
+  uint32_t* w = win + (rel >> 5);
+  atomicOr(w, (uint32_t)x);
+  atomicOr(w + 1, (uint32_t)(x >> 32));
+}
+
 constexpr uint32_t kEncWin = 1024;      // LDS output window (words, 4 KiB)
 constexpr uint32_t kEncFlushWords = 256;  // stream out once >= 1 KiB of whole 64-byte lines is ready
 
@@ -363,23 +371,28 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
     bwq = t + ((n << t) <= sum ? 1u : 0u);
   }
   const uint32_t start = bwq >= 2 ? bwq - 2 : 0u;
-  const uint32_t bits0 = n * (start + 1) + gsum<G>(shr_sum(start));
-  const uint32_t bits1 = n * (start + 2) + gsum<G>(shr_sum(start + 1));
+  // (the lane's share of the unary bits of the current candidate is kept:
+  // the chosen fs needs it again for the bit positions)
+  const uint32_t lq0 = shr_sum(start), lq1 = shr_sum(start + 1);
+  const uint32_t bits0 = n * (start + 1) + gsum<G>(lq0);
+  const uint32_t bits1 = n * (start + 2) + gsum<G>(lq1);
   int cand, dir;
-  uint32_t bits;
+  uint32_t bits, lq;
   if (bits1 <= bits0) {
-    cand = (int)start + 1; bits = bits1; dir = 1;
+    cand = (int)start + 1; bits = bits1; dir = 1; lq = lq1;
   } else {
-    cand = (int)start; bits = bits0; dir = -1;
+    cand = (int)start; bits = bits0; dir = -1; lq = lq0;
   }
   bool walking = sb_valid && sum != 0 && bits0 != bits1;
   for (;;) {
     const bool act = walking && cand > 0 && cand < 14 && !(RPP_EABLATE & 2);
     if (!__any(act)) break;
     const uint32_t f = act ? (uint32_t)(cand + dir) : 0u;
-    const uint32_t t = n * (f + 1) + gsum<G>(shr_sum(f));
+    const uint32_t lt = shr_sum(f);
+    const uint32_t t = n * (f + 1) + gsum<G>(lt);
     if (act && t <= bits) {
       bits = t;
+      lq = lt;
       cand += dir;
     } else {
       walking = false;
@@ -394,7 +407,7 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
 
   // ---- bit positions: one wave-wide scan ----
   uint32_t lbits = (sb_valid && j == 0) ? 4u : 0u;
-  if (mode == 1) lbits += shr_sum(fs) + cnt * (fs + 1);
+  if (mode == 1) lbits += lq + cnt * (fs + 1);
   else if (mode == 2) lbits += 16 * cnt;
   const uint32_t incl = wave_incl_sum(lbits);
   const uint32_t total = readlane(incl, kWave - 1);
@@ -405,7 +418,24 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
     emit_bits(st.win, pos, mode == 0 ? 0u : (mode == 1 ? fs + 1 : 15u));
     pos += 4;
   }
-  if (mode == 1 && !(RPP_EABLATE & 1)) {
+  if (mode == 1 && !mask_tail && !(RPP_EABLATE & 1)) {
+    // every lane owns SPL samples: two codes per packed step.  The '1' of
+    // code i sits at e_i = e_(i-1) + k + q_i; the code value (1 | r << 1,
+    // <= 15 bits) is OR-ed in by one 64-bit shift and two ds_or_b32.
+    const uint32_t k = fs + 1;
+    const uint32_t m2 = ((2u << fs) - 1u) * 0x10001u;
+    uint32_t e = pos - k;
+#pragma unroll
+    for (uint32_t h = 0; h < SPL / 2; ++h) {
+      const us2 dd = d[h];
+      const uint32_t qq = as_u32(dd >> (us2)(unsigned short)fs);
+      const uint32_t cc = (as_u32(dd << (us2)1) & m2) | 0x10001u;
+      e += k + (qq & 0xFFFFu);
+      emit_bits64(st.win, e, cc & 0xFFFFu);
+      e += k + (qq >> 16);
+      emit_bits64(st.win, e, cc >> 16);
+    }
+  } else if (mode == 1 && !(RPP_EABLATE & 1)) {
     const uint32_t lowmask = (1u << fs) - 1u;
 #pragma unroll
     for (uint32_t i = 0; i < SPL; ++i) {
