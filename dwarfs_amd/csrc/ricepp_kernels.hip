@@ -305,27 +305,59 @@ struct EncState {
   uint32_t* win;
   uint32_t* out32;
   uint32_t win_w0;  // global word index held in win[0] (multiple of 16)
-  uint32_t base;    // absolute bit position of the next sub-block
-  uint32_t carry;   // pixel value of the sample before this iteration (DPP-prev mode)
+  uint32_t base;       // absolute bit position after the emitted codes
+  uint32_t plan_base;  // absolute bit position after the planned codes
+  uint32_t carry;      // pixel value of the sample before this iteration (DPP-prev mode)
 };
 
-// One group of 64/G sub-blocks: zig-zag deltas, compute_best_split replay,
-// bit positions by one wave scan, codes OR-ed into the LDS window.
+// sum over the lane's samples of d >> f (the lane's unary bits at fs = f)
+template <uint32_t SPL>
+__device__ __forceinline__ uint32_t enc_shr_sum(const us2* d, uint32_t f) {
+  const us2 fv = (us2)(unsigned short)f, one = {1, 1};
+  uint32_t acc = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < SPL / 2; ++k) acc = __builtin_amdgcn_udot2(d[k] >> fv, one, acc, false);
+  return acc;
+}
+
+// One group of 64/G sub-blocks is encoded in three steps, so that the full
+// iterations can be software-pipelined (the plan of group i+1 is computed
+// while group i is emitted):
+//   enc_plan_a: zig-zag deltas, sums, compute_best_split start and first pair
+//   enc_plan_b: the split walk, mode, bit positions by one wave scan
+//   enc_emit:   header and codes OR-ed into the LDS window
 // dpp_prev: every lane full and the previous sample of a lane's first sample
 // is the previous lane's last one (CS == 1, bs == G * SPL): no prev loads.
+template <uint32_t SPL>
+struct EncPlan {
+  us2 d[SPL / 2];       // zig-zag deltas
+  uint32_t w[SPL / 2];  // stored samples (raw sub-blocks)
+  uint32_t n, cnt, sum;
+  uint32_t bits, lq;    // best cost so far, this lane's unary bits at that fs
+  int cand, dir;
+  bool walking;
+  uint32_t mode, fs;    // 0 = all-zero, 1 = Rice, 2 = raw
+  uint32_t pos;         // absolute bit position of this lane's first bit
+  uint32_t end;         // absolute bit position after the group
+};
+
 template <uint32_t SPL, uint32_t G, uint32_t CS>
-__device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r, const EncGeom& geo, uint32_t j,
-                                              uint32_t selbe, uint32_t be, uint32_t ulsb, bool mask_tail,
-                                              bool dpp_prev) {
+__device__ __forceinline__ void enc_plan_a(EncPlan<SPL>& P, EncState& st, const EncRaw<SPL>& r, const EncGeom& geo,
+                                           uint32_t selbe, uint32_t be, uint32_t ulsb, bool mask_tail,
+                                           bool dpp_prev) {
   constexpr uint32_t NW = SPL / 2;
   const uint32_t n = geo.n, cnt = geo.cnt;
+  P.n = n;
+  P.cnt = cnt;
   const bool sb_valid = n != 0;
   // ---- pixel values (ricepp_cpuspecific_traits.h:63-67) and zig-zag deltas
   //      (encode.h:116-123), two samples per instruction ----
-  us2 v[NW], d[NW];
+  us2 v[NW];
 #pragma unroll
-  for (uint32_t k = 0; k < NW; ++k)
+  for (uint32_t k = 0; k < NW; ++k) {
+    P.w[k] = r.w[k];
     v[k] = as_us2(__builtin_amdgcn_perm(r.w[k], r.w[k], selbe)) >> (us2)(unsigned short)ulsb;
+  }
   uint32_t pv;
   if (dpp_prev) {
     const uint32_t lastv = as_u32(v[NW - 1]) >> 16;
@@ -340,29 +372,23 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
     const us2 pp = as_us2(__builtin_amdgcn_alignbit(as_u32(v[k]), prevw, 16));
     prevw = as_u32(v[k]);
     const us2 diff = v[k] - pp;
-    d[k] = (diff << (us2)1) ^ as_us2(__builtin_bit_cast(uint32_t, (__builtin_bit_cast(ss2, diff) >> (ss2)15)));
+    P.d[k] = (diff << (us2)1) ^ as_us2(__builtin_bit_cast(uint32_t, (__builtin_bit_cast(ss2, diff) >> (ss2)15)));
   }
   if (mask_tail) {
 #pragma unroll
     for (uint32_t k = 0; k < NW; ++k) {
       const uint32_t keep = (2u * k < cnt ? 0xFFFFu : 0u) | (2u * k + 1 < cnt ? 0xFFFF0000u : 0u);
-      d[k] = as_us2(as_u32(d[k]) & keep);
+      P.d[k] = as_us2(as_u32(P.d[k]) & keep);
     }
   }
   const us2 one = {1, 1};
   uint32_t lsum = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < NW; ++k) lsum = __builtin_amdgcn_udot2(d[k], one, lsum, false);
-  auto shr_sum = [&](uint32_t f) -> uint32_t {
-    const us2 fv = (us2)(unsigned short)f;
-    uint32_t acc = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < NW; ++k) acc = __builtin_amdgcn_udot2(d[k] >> fv, one, acc, false);
-    return acc;
-  };
+  for (uint32_t k = 0; k < NW; ++k) lsum = __builtin_amdgcn_udot2(P.d[k], one, lsum, false);
   const uint32_t sum = gsum<G>(lsum);
+  P.sum = sum;
 
-  // ---- compute_best_split replay (encode.h:43-90) ----
+  // ---- compute_best_split replay (encode.h:43-90), first pair ----
   // start = max(0, bit_width(sum / n) - 2) without a division:
   // bit_width(floor(s/n)) = t + (s >= n << t), t = floor(log2 s) - floor(log2 n)
   uint32_t bwq = 0;
@@ -373,48 +399,58 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
   const uint32_t start = bwq >= 2 ? bwq - 2 : 0u;
   // (the lane's share of the unary bits of the current candidate is kept:
   // the chosen fs needs it again for the bit positions)
-  const uint32_t lq0 = shr_sum(start), lq1 = shr_sum(start + 1);
+  const uint32_t lq0 = enc_shr_sum<SPL>(P.d, start), lq1 = enc_shr_sum<SPL>(P.d, start + 1);
   const uint32_t bits0 = n * (start + 1) + gsum<G>(lq0);
   const uint32_t bits1 = n * (start + 2) + gsum<G>(lq1);
-  int cand, dir;
-  uint32_t bits, lq;
   if (bits1 <= bits0) {
-    cand = (int)start + 1; bits = bits1; dir = 1; lq = lq1;
+    P.cand = (int)start + 1; P.bits = bits1; P.dir = 1; P.lq = lq1;
   } else {
-    cand = (int)start; bits = bits0; dir = -1; lq = lq0;
+    P.cand = (int)start; P.bits = bits0; P.dir = -1; P.lq = lq0;
   }
-  bool walking = sb_valid && sum != 0 && bits0 != bits1;
+  P.walking = sb_valid && sum != 0 && bits0 != bits1;
+}
+
+template <uint32_t SPL, uint32_t G>
+__device__ __forceinline__ void enc_plan_b(EncPlan<SPL>& P, EncState& st, uint32_t j) {
+  const uint32_t n = P.n, cnt = P.cnt;
+  const bool sb_valid = n != 0;
+  // ---- compute_best_split replay: the walk ----
   for (;;) {
-    const bool act = walking && cand > 0 && cand < 14 && !(RPP_EABLATE & 2);
+    const bool act = P.walking && P.cand > 0 && P.cand < 14 && !(RPP_EABLATE & 2);
     if (!__any(act)) break;
-    const uint32_t f = act ? (uint32_t)(cand + dir) : 0u;
-    const uint32_t lt = shr_sum(f);
+    const uint32_t f = act ? (uint32_t)(P.cand + P.dir) : 0u;
+    const uint32_t lt = enc_shr_sum<SPL>(P.d, f);
     const uint32_t t = n * (f + 1) + gsum<G>(lt);
-    if (act && t <= bits) {
-      bits = t;
-      lq = lt;
-      cand += dir;
+    if (act && t <= P.bits) {
+      P.bits = t;
+      P.lq = lt;
+      P.cand += P.dir;
     } else {
-      walking = false;
+      P.walking = false;
     }
   }
   // encode.h:127-156: 0 = all-zero, 1 = Rice, 2 = raw
-  uint32_t mode = 0, fs = 0;
-  if (sb_valid && sum != 0) {
-    fs = (uint32_t)cand;
-    mode = (fs < 14 && bits < 16 * n) ? 1u : 2u;
+  P.mode = 0;
+  P.fs = 0;
+  if (sb_valid && P.sum != 0) {
+    P.fs = (uint32_t)P.cand;
+    P.mode = (P.fs < 14 && P.bits < 16 * n) ? 1u : 2u;
   }
-
   // ---- bit positions: one wave-wide scan ----
   uint32_t lbits = (sb_valid && j == 0) ? 4u : 0u;
-  if (mode == 1) lbits += lq + cnt * (fs + 1);
-  else if (mode == 2) lbits += 16 * cnt;
+  if (P.mode == 1) lbits += P.lq + cnt * (P.fs + 1);
+  else if (P.mode == 2) lbits += 16 * cnt;
   const uint32_t incl = wave_incl_sum(lbits);
-  const uint32_t total = readlane(incl, kWave - 1);
-  uint32_t pos = st.base + incl - lbits - 32 * st.win_w0;  // window-relative
+  P.pos = st.plan_base + incl - lbits;
+  st.plan_base += readlane(incl, kWave - 1);
+  P.end = st.plan_base;
+}
 
-  // ---- emit codes into the LDS window ----
-  if (sb_valid && j == 0) {
+template <uint32_t SPL>
+__device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, uint32_t j, bool mask_tail) {
+  const uint32_t cnt = P.cnt, mode = P.mode, fs = P.fs;
+  uint32_t pos = P.pos - 32 * st.win_w0;  // window-relative
+  if (P.n != 0 && j == 0) {
     emit_bits(st.win, pos, mode == 0 ? 0u : (mode == 1 ? fs + 1 : 15u));
     pos += 4;
   }
@@ -427,7 +463,7 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
     uint32_t e = pos - k;
 #pragma unroll
     for (uint32_t h = 0; h < SPL / 2; ++h) {
-      const us2 dd = d[h];
+      const us2 dd = P.d[h];
       const uint32_t qq = as_u32(dd >> (us2)(unsigned short)fs);
       const uint32_t cc = (as_u32(dd << (us2)1) & m2) | 0x10001u;
       e += k + (qq & 0xFFFFu);
@@ -440,7 +476,7 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
 #pragma unroll
     for (uint32_t i = 0; i < SPL; ++i) {
       if (i < cnt) {
-        const uint32_t di = (i & 1) ? (as_u32(d[i >> 1]) >> 16) : (as_u32(d[i >> 1]) & 0xFFFFu);
+        const uint32_t di = (i & 1) ? (as_u32(P.d[i >> 1]) >> 16) : (as_u32(P.d[i >> 1]) & 0xFFFFu);
         pos += di >> fs;  // unary zeros are implicit (the window is zeroed)
         emit_bits(st.win, pos, 1u | ((di & lowmask) << 1));
         pos += fs + 1;
@@ -450,13 +486,24 @@ __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r
 #pragma unroll
     for (uint32_t i = 0; i < SPL; ++i) {
       if (i < cnt) {
-        const uint32_t ri = (i & 1) ? (r.w[i >> 1] >> 16) : (r.w[i >> 1] & 0xFFFFu);
+        const uint32_t ri = (i & 1) ? (P.w[i >> 1] >> 16) : (P.w[i >> 1] & 0xFFFFu);
         emit_bits(st.win, pos, ri);  // raw stored value (encode.h:148-151)
         pos += 16;
       }
     }
   }
-  st.base += total;
+  st.base = P.end;
+}
+
+// The three steps back to back (ragged tails, unpipelined groups).
+template <uint32_t SPL, uint32_t G, uint32_t CS>
+__device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r, const EncGeom& geo, uint32_t j,
+                                              uint32_t selbe, uint32_t be, uint32_t ulsb, bool mask_tail,
+                                              bool dpp_prev) {
+  EncPlan<SPL> P;
+  enc_plan_a<SPL, G, CS>(P, st, r, geo, selbe, be, ulsb, mask_tail, dpp_prev);
+  enc_plan_b<SPL, G>(P, st, j);
+  enc_emit<SPL>(P, st, j, mask_tail);
 }
 
 // Streams whole 64-byte lines out once >= kEncFlushWords are complete.
@@ -503,11 +550,16 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint32_t N = (uint32_t)n64;
   const uint16_t* in = p.in + p.in_off[b];
   uint8_t* out8 = p.out + ooff;
+#ifdef RPP_STATS
+  uint32_t stat_acc[16] = {0};
+  unsigned long long tprev_;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
+#endif
 
   for (uint32_t i = lane; i < kEncWin; i += kWave) win[i] = 0;
   __syncthreads();
 
-  EncState st{win, reinterpret_cast<uint32_t*>(out8), 0u, 16 * CS, 0u};
+  EncState st{win, reinterpret_cast<uint32_t*>(out8), 0u, 16 * CS, 16 * CS, 0u};
   // codec.h:69-74,81-86: 16-bit initial value read(in[i]) per component.
   if (lane < CS) emit_bits(win, 16 * lane, N ? px_read(in[lane], be, ulsb) : 0u);
   // DPP-prev mode: the first sample is its own reference
@@ -524,29 +576,52 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const bool empty_lanes = G * SPL != bs;
   const bool dpp_prev = CS == 1 && !empty_lanes && !(RPP_EABLATE & 4);
 
-  // ---- full iterations, double buffered (no register copies between the
-  //      load and its use, so the next group's loads stay in flight) ----
+  // ---- full iterations, software-pipelined: group it+1 is planned
+  //      (deltas, split, positions) around the emission of group it, so the
+  //      two dependency chains overlap.  Samples are loaded three groups
+  //      ahead into three rotating buffers (unrolled by three: a register
+  //      copy of a loaded value would wait for the load) ----
   uint32_t it = 0;
   if (nfull) {
-    EncGeom ga = enc_geom<SPL, CS>(g, j, nsb, N, bs), gb;
-    EncRaw<SPL> ra = enc_load_vec<SPL, CS>(in, ga, !dpp_prev), rb;
-    for (; it + 1 < nfull; it += 2) {
-      gb = enc_geom<SPL, CS>((it + 1) * spw + g, j, nsb, N, bs);
-      rb = enc_load_vec<SPL, CS>(in, gb, !dpp_prev);
-      enc_iteration<SPL, G, CS>(st, ra, ga, j, selbe, be, ulsb, empty_lanes, dpp_prev);
+    EncGeom g0 = enc_geom<SPL, CS>(g, j, nsb, N, bs);
+    EncRaw<SPL> r0 = enc_load_vec<SPL, CS>(in, g0, !dpp_prev);
+    EncGeom g1 = enc_geom<SPL, CS>(spw + g, j, nsb, N, bs);
+    EncRaw<SPL> r1 = enc_load_vec<SPL, CS>(in, g1, !dpp_prev);
+    EncGeom g2 = enc_geom<SPL, CS>(2 * spw + g, j, nsb, N, bs);
+    EncRaw<SPL> r2 = enc_load_vec<SPL, CS>(in, g2, !dpp_prev);
+    EncPlan<SPL> P, Q;
+    enc_plan_a<SPL, G, CS>(P, st, r0, g0, selbe, be, ulsb, empty_lanes, dpp_prev);
+    enc_plan_b<SPL, G>(P, st, j);
+    // emits group `it` (plan P) while planning group it+1 (from rn); group
+    // it's buffer rl then takes group it+3.  Loads are unconditional: past
+    // the last group the geometry is empty and the load reads the stream
+    // start (a conditional load would make every later wait cover it).
+    auto step = [&](EncRaw<SPL>& rn, const EncGeom& gn, EncRaw<SPL>& rl, EncGeom& gl) {
+      gl = enc_geom<SPL, CS>((it + 3) * spw + g, j, nsb, N, bs);
+      rl = enc_load_vec<SPL, CS>(in, gl, !dpp_prev);
+      RPP_STAT(0, 1);
+      RPP_TSTAMP(1);
+      enc_plan_a<SPL, G, CS>(Q, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
+      RPP_TSTAMP(2);
+      enc_emit<SPL>(P, st, j, empty_lanes);
+      RPP_TSTAMP(3);
+      enc_plan_b<SPL, G>(Q, st, j);
+      RPP_TSTAMP(4);
+      P = Q;
       enc_flush(st, false);
-      if (it + 2 < nfull) {
-        ga = enc_geom<SPL, CS>((it + 2) * spw + g, j, nsb, N, bs);
-        ra = enc_load_vec<SPL, CS>(in, ga, !dpp_prev);
-      }
-      enc_iteration<SPL, G, CS>(st, rb, gb, j, selbe, be, ulsb, empty_lanes, dpp_prev);
-      enc_flush(st, false);
-    }
-    if (it < nfull) {
-      enc_iteration<SPL, G, CS>(st, ra, ga, j, selbe, be, ulsb, empty_lanes, dpp_prev);
-      enc_flush(st, false);
+      RPP_TSTAMP(5);
       ++it;
+    };
+    while (it + 1 < nfull) {
+      step(r1, g1, r0, g0);
+      if (it + 1 >= nfull) break;
+      step(r2, g2, r1, g1);
+      if (it + 1 >= nfull) break;
+      step(r0, g0, r2, g2);
     }
+    enc_emit<SPL>(P, st, j, empty_lanes);
+    enc_flush(st, false);
+    ++it;
   }
   // ---- ragged tail / unaligned streams: per-sample loads ----
   for (uint32_t s0 = it * spw; s0 < nsb; s0 += spw) {
@@ -568,6 +643,10 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
     p.out_bytes[b] = total_bytes;
     p.status[b] = RPP_OK;
   }
+#ifdef RPP_STATS
+  if (lane == 0)
+    for (int i = 0; i < 16; ++i) atomicAdd(&g_rpp_stats[i], (unsigned long long)stat_acc[i]);
+#endif
 }
 
 // Host-side kernel choice: SPL 16 for bs > 64 (8 sub-blocks of 128 per
@@ -736,23 +815,30 @@ __device__ __forceinline__ Map8 scan_step8(Map8 m) {
 // loaded once), the rest the map from the left; out-of-range sources read 0
 // (bound_ctrl) and are always masked.  Saves the per-step identity moves a
 // DPP move into a fresh `old` needs.
-#define RPP_SCAN8_STEP(NAME, CTRL, MASK)                                                                  \
-  __device__ __forceinline__ Map8 NAME(Map8 m, Map8 id) {                                                 \
+#define RPP_SCAN8_STEP(NAME, CTRL)                                                                        \
+  __device__ __forceinline__ Map8 NAME(Map8 m, Map8 id, uint64_t mask) {                                  \
     Map8 d;                                                                                               \
     asm("s_mov_b64 vcc, %6\n\ts_nop 0\n\t"                                                                \
         "v_cndmask_b32_dpp %0, %2, %4, vcc " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"          \
         "v_cndmask_b32_dpp %1, %3, %5, vcc " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1"              \
         : "=&v"(d.lo), "=&v"(d.hi)                                                                        \
-        : "v"(m.lo), "v"(m.hi), "v"(id.lo), "v"(id.hi), "s"((uint64_t)(MASK))                           \
+        : "v"(m.lo), "v"(m.hi), "v"(id.lo), "v"(id.hi), "s"(mask)                                          \
         : "vcc");                                                                                         \
     return comp8(m, d);                                                                                   \
   }
-RPP_SCAN8_STEP(scan8_shr1, "row_shr:1", 0x0001000100010001ull)
-RPP_SCAN8_STEP(scan8_shr2, "row_shr:2", 0x0003000300030003ull)
-RPP_SCAN8_STEP(scan8_shr4, "row_shr:4", 0x000F000F000F000Full)
-RPP_SCAN8_STEP(scan8_shr8, "row_shr:8", 0x00FF00FF00FF00FFull)
-RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", 0x0000FFFF0000FFFFull)
-RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", 0x00000000FFFFFFFFull)
+RPP_SCAN8_STEP(scan8_shr1, "row_shr:1")
+RPP_SCAN8_STEP(scan8_shr2, "row_shr:2")
+RPP_SCAN8_STEP(scan8_shr4, "row_shr:4")
+RPP_SCAN8_STEP(scan8_shr8, "row_shr:8")
+RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15")
+RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31")
+// the lanes of each step that have no source (they take the identity),
+// held in SGPR pairs across the loop (opaque, so not rematerialised)
+struct ScanMasks {
+  uint64_t r1 = 0x0001000100010001ull, r2 = 0x0003000300030003ull, r4 = 0x000F000F000F000Full,
+           r8 = 0x00FF00FF00FF00FFull, b15 = 0x0000FFFF0000FFFFull, b31 = 0x00000000FFFFFFFFull;
+  __device__ ScanMasks() { asm volatile("" : "+s"(r1), "+s"(r2), "+s"(r4), "+s"(r8), "+s"(b15), "+s"(b31)); }
+};
 #undef RPP_SCAN8_STEP
 // exclusive form: the map of lanes 0..l-1 (identity on lane 0)
 __device__ __forceinline__ Map8 shift8_wave(Map8 m, Map8 id) {
@@ -1007,6 +1093,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(2 * N), 0x00020000);
   Map8 vid{kId0, kId1};  // the identity map, kept in VGPRs for the scan steps
   asm volatile("" : "+v"(vid.lo), "+v"(vid.hi));
+  const ScanMasks smask;
 
   for (uint32_t s = 0; s < nsb && status == RPP_OK; ++s) {
     // ---- fast loop (the common case): Rice sub-blocks of 128 codes with fs
@@ -1050,12 +1137,12 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       auto parse = [&](uint32_t q, uint32_t xl, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
         const uint32_t k = fs + 1;
         Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
-        M = scan8_shr1(M, vid);
-        M = scan8_shr2(M, vid);
-        M = scan8_shr4(M, vid);
-        M = scan8_shr8(M, vid);
-        M = scan8_bc15(M, vid);
-        M = scan8_bc31(M, vid);
+        M = scan8_shr1(M, vid, smask.r1);
+        M = scan8_shr2(M, vid, smask.r2);
+        M = scan8_shr4(M, vid, smask.r4);
+        M = scan8_shr8(M, vid, smask.r8);
+        M = scan8_bc15(M, vid, smask.b15);
+        M = scan8_bc31(M, vid, smask.b31);
         const Map8 X = shift8_wave(M, vid);
         RPP_TSTAMP(3);
         // state 4 at the window start: skip the header.  The selectors
@@ -1070,7 +1157,6 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
         // terminator mask: byte 0 of a0, a1, a2 -> bytes 0, 1, 2
         uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
-        const uint32_t tm0 = tm;
         uint32_t cnt = __builtin_popcount(tm);
         asm volatile("" : "+v"(cnt));  // keeps the scan's first step a plain DPP add
         const uint32_t incl = (RPP_ABLATE & 256) ? cnt + 2 * lane : wave_incl_sum(cnt);
@@ -1087,14 +1173,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         }
         // the next sub-block starts after code n-1's remainder: terminator
         // n-1-excl (0..3) of the first lane whose inclusive count reaches n
-        // (scalar work)
+        // (positions <= 23 packed in bytes and picked by one bit-field
+        // extract: a few vector ops rather than a chain of scalar ones,
+        // the scalar unit being shared by the CU's 16 waves)
+        const uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
+        const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (n - 1 - excl), 8);
         const uint32_t lz = finm ? (uint32_t)__builtin_ctzll(finm) : 0u;
-        uint32_t z = readlane(tm0, (int)lz);
-        const uint32_t zr = n - 1 - readlane(excl, (int)lz);
-        z &= zr > 0 ? z - 1 : ~0u;
-        z &= zr > 1 ? z - 1 : ~0u;
-        z &= zr > 2 ? z - 1 : ~0u;
-        Pe = q + kSegBits * lz + (uint32_t)__builtin_ctz(z | 0x80000000u) + k;
+        Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
         RPP_TSTAMP(8);
         // pair excl + j for j = 3 .. 0, one instruction each (kept apart: a
         // merged ds_write2 would put two j in one instruction): a slot past
