@@ -765,7 +765,7 @@ constexpr uint32_t kAhead = 288;                 // words kept resident ahead of
 constexpr uint32_t kDecMaxWaves = 16;            // waves per workgroup (one table copy each)
 constexpr uint32_t kRingPad = 64;               // ring words 0..63 mirrored after the ring end
 constexpr uint32_t kListDump = 512;            // list slot written by masked-off lanes
-constexpr uint32_t kListWords = kListDump + 8;  // terminator positions of one sub-block (bs <= 512)
+constexpr uint32_t kListWords = kListDump + 16;  // terminator positions of one sub-block (bs <= 512), dump pairs
 constexpr uint32_t kWaveLdsWords = kRingWords + kRingPad + kListWords;
 constexpr uint32_t kTabBytes = kMapEntries * 16;
 
@@ -1104,7 +1104,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
     //      lookups, scans) in the same basic block, so the LDS latencies and
     //      DPP chains of the two overlap.  Anything else leaves the loop and
     //      takes the general path below for that sub-block. ----
-    if (s < nsb_fast && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
+    // MT: terminators a 24-bit segment can hold (codes of >= fs + 1 bits),
+    // [LO, HI]: the fs range of this instance
+    auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI>() {
       constexpr uint32_t n = 2 * kWave;
       const uint4* const list4 = reinterpret_cast<const uint4*>(list);
       uint2* const list2 = reinterpret_cast<uint2*>(list);
@@ -1117,18 +1119,18 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t* w = ring + ((q >> 5) & kRingMask) + (o >> 5);
         return __builtin_amdgcn_alignbit(w[1], w[0], o);  // (shift o mod 32)
       };
-      // the header's fs clamped to 5..7 (scalar), so the lookups stay in
-      // range for any header; the fast loop only keeps sub-blocks whose fs
-      // is in range
+      // the header's fs clamped to [LO, HI] (scalar), so the lookups stay in
+      // range for any header; the loop only keeps sub-blocks whose fs is in
+      // range
       auto fs_of = [](uint32_t h) {
         uint32_t r;
-        asm("s_and_b32 %0, %1, 15\n\ts_max_u32 %0, %0, 6\n\ts_min_u32 %0, %0, 8\n\ts_sub_u32 %0, %0, 1"
+        asm("s_and_b32 %0, %1, 15\n\ts_max_u32 %0, %0, %2\n\ts_min_u32 %0, %0, %3\n\ts_sub_u32 %0, %0, 1"
             : "=&s"(r)
-            : "s"(h)
+            : "s"(h), "n"(LO + 1), "n"(HI + 1)
             : "scc");
         return r;
       };
-      auto header_ok = [](uint32_t h) { return (h & 15u) - 6u <= 2u; };
+      auto header_ok = [](uint32_t h) { return (h & 15u) - (LO + 1) <= HI - LO; };
       // Parse of the sub-block at bit q: entry states by the map scan,
       // terminators, (a_i, remainder) of code i into list pair i with a_i =
       // terminator position - (q + 4) - i k (the unary part of code i is then
@@ -1163,35 +1165,40 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint64_t finm = __ballot(incl >= n);
         const uint32_t excl = incl - cnt;
         RPP_TSTAMP(7);
-        // terminator positions t0 < t1 < t2 < t3 in the segment (garbage
-        // past cnt)
-        uint32_t t[4];
+        // terminator positions t0 < t1 < ... in the segment (garbage past
+        // cnt)
+        uint32_t t[MT];
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
+        for (uint32_t j = 0; j < MT; ++j) {
           t[j] = ffbl(tm);
           tm &= tm - 1;
         }
         // the next sub-block starts after code n-1's remainder: terminator
-        // n-1-excl (0..3) of the first lane whose inclusive count reaches n
+        // n-1-excl (< MT) of the first lane whose inclusive count reaches n
         // (positions <= 23 packed in bytes and picked by one bit-field
         // extract: a few vector ops rather than a chain of scalar ones,
         // the scalar unit being shared by the CU's 16 waves)
-        const uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
-        const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (n - 1 - excl), 8);
+        const uint32_t r = n - 1 - excl;
+        uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
+        if constexpr (MT > 4) {
+          const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
+          tpk = r < 4 ? tpk : tpk1;
+        }
+        const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
         const uint32_t lz = finm ? (uint32_t)__builtin_ctzll(finm) : 0u;
         Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
         RPP_TSTAMP(8);
-        // pair excl + j for j = 3 .. 0, one instruction each (kept apart: a
-        // merged ds_write2 would put two j in one instruction): a slot past
+        // pair excl + j for j = MT-1 .. 0, one instruction each (kept apart:
+        // a merged ds_write2 would put two j in one instruction): a slot past
         // this lane's codes belongs to a later lane, which writes it in a
-        // later instruction (its j is smaller); lanes without terminators
-        // write the unused pairs 256..259
-        const uint32_t base = cnt ? excl : 256u;
+        // later instruction (its j is smaller); lanes without terminators or
+        // past the sub-block write the unused pairs from 256
+        const uint32_t base = cnt != 0 && excl < n ? excl : 256u;
         uint32_t abase = (uint32_t)((int)lane24m4 + __mul24((int)base, -(int)k));
         asm volatile("" : "+v"(abase));  // computed once, not per pair
         const uint32_t xr = xl >> 1;     // the remainder of a terminator at t is bits t+1 .. t+fs
 #pragma unroll
-        for (int j = 3; j >= 0; --j) {
+        for (int j = MT - 1; j >= 0; --j) {
           list2[base + j] = make_uint2(abase + t[j] - j * k, __builtin_amdgcn_ubfe(xr, t[j], fs));
           lds_fence();
         }
@@ -1292,6 +1299,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         ring_keep(Pn);
         RPP_TSTAMP(15);
       }
+    };
+    if (s < nsb_fast && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
+      // dispatch on the sub-block's fs class
+      const uint32_t* w = ring + ((P >> 5) & kRingMask);
+      const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
+      if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
+      else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
     }
     if (s >= nsb || status != RPP_OK) break;
     // ---- general path: one sub-block of any kind ----
