@@ -78,6 +78,22 @@ def test_config_matrix(bs, cs):
             run_batch(codec.CodecConfig(bs, cs, "big" if be else "little", ulsb), blocks)
 
 
+@pytest.mark.parametrize("cs", [1, 2])
+@pytest.mark.parametrize("ulsb", [0, 4])
+def test_rice_parameter_classes(cs, ulsb):
+    """bs 128 streams whose sub-blocks take every Rice parameter (fs 0-13),
+    each class alone (the decoder's fs 2-4 and 5-7 fast loops and the
+    general path) and switching class from one sub-block to the next
+    (Poisson lambda varied per 128-sample run)."""
+    rng = np.random.default_rng(77 + 10 * cs + ulsb)
+    lams = [0.3, 2, 6, 20, 60, 200, 600, 2000, 6000, 20000]
+    blocks = [datagen.poisson_data(rng, 128 * cs * 40, lam=lam, ulsb=ulsb) for lam in lams]
+    runs = [datagen.poisson_data(rng, 128 * cs, lam=lams[int(rng.integers(0, len(lams)))], ulsb=ulsb)
+            for _ in range(120)]
+    blocks.append(np.concatenate(runs))
+    run_batch(codec.CodecConfig(128, cs, "big", ulsb), blocks)
+
+
 @pytest.mark.parametrize("ulsb", list(range(0, 16)))
 def test_unused_lsb_sweep(ulsb):
     rng = np.random.default_rng(ulsb)
