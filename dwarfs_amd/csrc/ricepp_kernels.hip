@@ -341,7 +341,7 @@ struct EncPlan {
   uint32_t end;         // absolute bit position after the group
 };
 
-template <uint32_t SPL, uint32_t G, uint32_t CS>
+template <uint32_t SPL, uint32_t G, uint32_t CS, bool SH>
 __device__ __forceinline__ void enc_plan_a(EncPlan<SPL>& P, EncState& st, const EncRaw<SPL>& r, const EncGeom& geo,
                                            uint32_t selbe, uint32_t be, uint32_t ulsb, bool mask_tail,
                                            bool dpp_prev) {
@@ -356,7 +356,8 @@ __device__ __forceinline__ void enc_plan_a(EncPlan<SPL>& P, EncState& st, const 
 #pragma unroll
   for (uint32_t k = 0; k < NW; ++k) {
     P.w[k] = r.w[k];
-    v[k] = as_us2(__builtin_amdgcn_perm(r.w[k], r.w[k], selbe)) >> (us2)(unsigned short)ulsb;
+    v[k] = as_us2(__builtin_amdgcn_perm(r.w[k], r.w[k], selbe));
+    if constexpr (SH) v[k] = v[k] >> (us2)(unsigned short)ulsb;
   }
   uint32_t pv;
   if (dpp_prev) {
@@ -414,10 +415,10 @@ template <uint32_t SPL, uint32_t G>
 __device__ __forceinline__ void enc_plan_b(EncPlan<SPL>& P, EncState& st, uint32_t j) {
   const uint32_t n = P.n, cnt = P.cnt;
   const bool sb_valid = n != 0;
-  // ---- compute_best_split replay: the walk ----
-  for (;;) {
-    const bool act = P.walking && P.cand > 0 && P.cand < 14 && !(RPP_EABLATE & 2);
-    if (!__any(act)) break;
+  // ---- compute_best_split replay: the walk.  Almost every sub-block takes
+  //      exactly one more candidate (that does not improve), so the first
+  //      step runs unconditionally, without a vote and a branch ----
+  auto walk_step = [&](bool act) {
     const uint32_t f = act ? (uint32_t)(P.cand + P.dir) : 0u;
     const uint32_t lt = enc_shr_sum<SPL>(P.d, f);
     const uint32_t t = n * (f + 1) + gsum<G>(lt);
@@ -428,6 +429,12 @@ __device__ __forceinline__ void enc_plan_b(EncPlan<SPL>& P, EncState& st, uint32
     } else {
       P.walking = false;
     }
+  };
+  walk_step(P.walking && P.cand > 0 && P.cand < 14 && !(RPP_EABLATE & 2));
+  for (;;) {
+    const bool act = P.walking && P.cand > 0 && P.cand < 14 && !(RPP_EABLATE & 2);
+    if (!__any(act)) break;
+    walk_step(act);
   }
   // encode.h:127-156: 0 = all-zero, 1 = Rice, 2 = raw
   P.mode = 0;
@@ -496,12 +503,12 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
 }
 
 // The three steps back to back (ragged tails, unpipelined groups).
-template <uint32_t SPL, uint32_t G, uint32_t CS>
+template <uint32_t SPL, uint32_t G, uint32_t CS, bool SH>
 __device__ __forceinline__ void enc_iteration(EncState& st, const EncRaw<SPL>& r, const EncGeom& geo, uint32_t j,
                                               uint32_t selbe, uint32_t be, uint32_t ulsb, bool mask_tail,
                                               bool dpp_prev) {
   EncPlan<SPL> P;
-  enc_plan_a<SPL, G, CS>(P, st, r, geo, selbe, be, ulsb, mask_tail, dpp_prev);
+  enc_plan_a<SPL, G, CS, SH>(P, st, r, geo, selbe, be, ulsb, mask_tail, dpp_prev);
   enc_plan_b<SPL, G>(P, st, j);
   enc_emit<SPL>(P, st, j, mask_tail);
 }
@@ -530,7 +537,8 @@ __device__ __forceinline__ void enc_flush(EncState& st, bool final_flush) {
   }
 }
 
-template <uint32_t SPL, uint32_t G, uint32_t CS>
+// SH: unused_lsb_count != 0 (the pixel read shifts)
+template <uint32_t SPL, uint32_t G, uint32_t CS, bool SH>
 __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t win[kEncWin];
   constexpr uint32_t spw = kWave / G;  // sub-blocks per iteration
@@ -590,7 +598,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
     EncGeom g2 = enc_geom<SPL, CS>(2 * spw + g, j, nsb, N, bs);
     EncRaw<SPL> r2 = enc_load_vec<SPL, CS>(in, g2, !dpp_prev);
     EncPlan<SPL> P, Q;
-    enc_plan_a<SPL, G, CS>(P, st, r0, g0, selbe, be, ulsb, empty_lanes, dpp_prev);
+    enc_plan_a<SPL, G, CS, SH>(P, st, r0, g0, selbe, be, ulsb, empty_lanes, dpp_prev);
     enc_plan_b<SPL, G>(P, st, j);
     // emits group `it` (plan P) while planning group it+1 (from rn); group
     // it's buffer rl then takes group it+3.  Loads are unconditional: past
@@ -601,7 +609,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
       rl = enc_load_vec<SPL, CS>(in, gl, !dpp_prev);
       RPP_STAT(0, 1);
       RPP_TSTAMP(1);
-      enc_plan_a<SPL, G, CS>(Q, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
+      enc_plan_a<SPL, G, CS, SH>(Q, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
       RPP_TSTAMP(2);
       enc_emit<SPL>(P, st, j, empty_lanes);
       RPP_TSTAMP(3);
@@ -627,7 +635,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   for (uint32_t s0 = it * spw; s0 < nsb; s0 += spw) {
     const EncGeom geo = enc_geom<SPL, CS>(s0 + g, j, nsb, N, bs);
     const EncRaw<SPL> r = enc_load_scalar<SPL, CS>(in, geo);
-    enc_iteration<SPL, G, CS>(st, r, geo, j, selbe, be, ulsb, true, false);
+    enc_iteration<SPL, G, CS, SH>(st, r, geo, j, selbe, be, ulsb, true, false);
     enc_flush(st, false);
   }
   enc_flush(st, true);
@@ -652,19 +660,19 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
 // Host-side kernel choice: SPL 16 for bs > 64 (8 sub-blocks of 128 per
 // iteration), else 8; G = next pow2 of ceil(bs / SPL).
 typedef void (*EncKernel)(EncParams);
-template <uint32_t CS>
+template <uint32_t CS, bool SH>
 EncKernel enc_kernel_for(uint32_t bs) {
   if (bs > 64) {
     const uint32_t m = (bs + 15) / 16;
-    if (m <= 8) return rpp_encode_kernel<16, 8, CS>;
-    if (m <= 16) return rpp_encode_kernel<16, 16, CS>;
-    return rpp_encode_kernel<16, 32, CS>;
+    if (m <= 8) return rpp_encode_kernel<16, 8, CS, SH>;
+    if (m <= 16) return rpp_encode_kernel<16, 16, CS, SH>;
+    return rpp_encode_kernel<16, 32, CS, SH>;
   }
   const uint32_t m = (bs + 7) / 8;
-  if (m <= 1) return rpp_encode_kernel<8, 1, CS>;
-  if (m <= 2) return rpp_encode_kernel<8, 2, CS>;
-  if (m <= 4) return rpp_encode_kernel<8, 4, CS>;
-  return rpp_encode_kernel<8, 8, CS>;
+  if (m <= 1) return rpp_encode_kernel<8, 1, CS, SH>;
+  if (m <= 2) return rpp_encode_kernel<8, 2, CS, SH>;
+  if (m <= 4) return rpp_encode_kernel<8, 4, CS, SH>;
+  return rpp_encode_kernel<8, 8, CS, SH>;
 }
 
 // ===========================================================================
@@ -1544,8 +1552,10 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
   EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count};
-  const EncKernel k = cfg->component_stream_count == 1 ? enc_kernel_for<1>(cfg->block_size)
-                                                       : enc_kernel_for<2>(cfg->block_size);
+  const bool sh = cfg->unused_lsb_count != 0;
+  const EncKernel k = cfg->component_stream_count == 1
+                          ? (sh ? enc_kernel_for<1, true>(cfg->block_size) : enc_kernel_for<1, false>(cfg->block_size))
+                          : (sh ? enc_kernel_for<2, true>(cfg->block_size) : enc_kernel_for<2, false>(cfg->block_size));
   hipLaunchKernelGGL(k, dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
