@@ -1253,6 +1253,16 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
       };
 
+      // Ring bounds, recomputed only when the ring changes: the next window
+      // start may be at most pn_limit (resident look-ahead, the header
+      // inside the input), and ring_keep has something to do once the
+      // window start reaches word trig_w (lim >= P + 4 here).
+      uint32_t pn_limit, trig_w;
+      auto ring_bounds = [&]() {
+        pn_limit = min(lim - 4u, 32u * (fill_w - kAhead) + 31u);
+        trig_w = pend ? fill_w - (kAhead + 127u) : (fill_w > 766u ? fill_w - 766u : 0u);
+      };
+      ring_bounds();
       // prologue: parse sub-block s
       uint32_t Pn;
       uint32_t xl = seg_bits(P);
@@ -1263,7 +1273,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       bool ok = parse(P, xl, fs, e0, e1, e2, Pn) && header_ok(h);
       while (ok) {
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
-        const bool nxt = s + 1 < nsb_fast && fill_w >= (Pn >> 5) + kAhead && Pn + 4 <= lim;
+        const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
         const uint32_t xlB = seg_bits(Pn);
         const uint4 tt = list4[lane];
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
@@ -1304,7 +1314,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         if (!ok) break;
         Pn = PnB;
         fs = fsB;
-        ring_keep(Pn);
+        if ((Pn >> 5) >= trig_w) {
+          ring_keep(Pn);
+          ring_bounds();
+        }
         RPP_TSTAMP(15);
       }
     };
