@@ -1124,7 +1124,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // within 50 words of the window start, inside the ring's mirror)
       auto seg_bits = [&](uint32_t q) {
         const uint32_t o = lane24 + (q & 31u);
-        const uint32_t* w = ring + ((q >> 5) & kRingMask) + (o >> 5);
+        uint32_t oi = o >> 5;
+        asm("" : "+v"(oi));  // (else the compiler masks o >> 3: one more op)
+        const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
         return __builtin_amdgcn_alignbit(w[1], w[0], o);  // (shift o mod 32)
       };
       // the header's fs clamped to [LO, HI] (scalar), so the lookups stay in
@@ -1146,7 +1148,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // window, and its end (the header of the next) in Pe.
       auto parse = [&](uint32_t q, uint32_t xl, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
         const uint32_t k = fs + 1;
-        Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
+        const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});  // (also gives byte 2's entry state)
+        Map8 M = comp8(Map8{e2.x, e2.y}, M01);
         M = scan8_shr1(M, vid, smask.r1);
         M = scan8_shr2(M, vid, smask.r2);
         M = scan8_shr4(M, vid, smask.r4);
@@ -1159,12 +1162,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // carry the state in byte 0 and 0xFF (a v_perm selector for 0xFF)
         // in bytes 1-3, so each byte's next state comes out of its v_perm
         // as the next selector, with no masking.
-        uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
+        const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
         const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-        sel = __builtin_amdgcn_perm(e0.y, e0.x, sel);
-        const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
-        sel = __builtin_amdgcn_perm(e1.y, e1.x, sel);
-        const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+        const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
+        const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
         // terminator mask: byte 0 of a0, a1, a2 -> bytes 0, 1, 2
         uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
         uint32_t cnt = __builtin_popcount(tm);
@@ -1274,8 +1275,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       while (ok) {
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
-        const uint32_t xlB = seg_bits(Pn);
         const uint4 tt = list4[lane];
+        const uint32_t xlB = seg_bits(Pn);
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
         RPP_TSTAMP(1);
         RPP_STAT(0, 1);
