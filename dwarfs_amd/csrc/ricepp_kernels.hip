@@ -586,48 +586,48 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
 
   // ---- full iterations, software-pipelined: group it+1 is planned
   //      (deltas, split, positions) around the emission of group it, so the
-  //      two dependency chains overlap.  Samples are loaded three groups
-  //      ahead into three rotating buffers (unrolled by three: a register
-  //      copy of a loaded value would wait for the load) ----
+  //      two dependency chains overlap.  Two sample buffers: the one just
+  //      planned from is reloaded at once with the group after next, about
+  //      two steps before its use; unrolled by two so that plans and loaded
+  //      samples stay in place (no register copies) ----
   uint32_t it = 0;
   if (nfull) {
     EncGeom g0 = enc_geom<SPL, CS>(g, j, nsb, N, bs);
     EncRaw<SPL> r0 = enc_load_vec<SPL, CS>(in, g0, !dpp_prev);
     EncGeom g1 = enc_geom<SPL, CS>(spw + g, j, nsb, N, bs);
     EncRaw<SPL> r1 = enc_load_vec<SPL, CS>(in, g1, !dpp_prev);
-    EncGeom g2 = enc_geom<SPL, CS>(2 * spw + g, j, nsb, N, bs);
-    EncRaw<SPL> r2 = enc_load_vec<SPL, CS>(in, g2, !dpp_prev);
     EncPlan<SPL> P, Q;
     enc_plan_a<SPL, G, CS, SH>(P, st, r0, g0, selbe, be, ulsb, empty_lanes, dpp_prev);
+    // (loads are unconditional: past the last group the geometry is empty
+    // and the load reads the stream start; a conditional load would make
+    // every later wait cover it)
+    g0 = enc_geom<SPL, CS>(2 * spw + g, j, nsb, N, bs);
+    r0 = enc_load_vec<SPL, CS>(in, g0, !dpp_prev);
     enc_plan_b<SPL, G>(P, st, j);
-    // emits group `it` (plan P) while planning group it+1 (from rn); group
-    // it's buffer rl then takes group it+3.  Loads are unconditional: past
-    // the last group the geometry is empty and the load reads the stream
-    // start (a conditional load would make every later wait cover it).
-    auto step = [&](EncRaw<SPL>& rn, const EncGeom& gn, EncRaw<SPL>& rl, EncGeom& gl) {
-      gl = enc_geom<SPL, CS>((it + 3) * spw + g, j, nsb, N, bs);
-      rl = enc_load_vec<SPL, CS>(in, gl, !dpp_prev);
+    // emits group `it` (plan E) while planning group it+1 (into F, from rn,
+    // which then takes group it+3)
+    auto step = [&](EncPlan<SPL>& E, EncPlan<SPL>& F, EncRaw<SPL>& rn, EncGeom& gn) {
       RPP_STAT(0, 1);
       RPP_TSTAMP(1);
-      enc_plan_a<SPL, G, CS, SH>(Q, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
+      enc_plan_a<SPL, G, CS, SH>(F, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
+      gn = enc_geom<SPL, CS>((it + 3) * spw + g, j, nsb, N, bs);
+      rn = enc_load_vec<SPL, CS>(in, gn, !dpp_prev);
       RPP_TSTAMP(2);
-      enc_emit<SPL>(P, st, j, empty_lanes);
+      enc_emit<SPL>(E, st, j, empty_lanes);
       RPP_TSTAMP(3);
-      enc_plan_b<SPL, G>(Q, st, j);
+      enc_plan_b<SPL, G>(F, st, j);
       RPP_TSTAMP(4);
-      P = Q;
       enc_flush(st, false);
       RPP_TSTAMP(5);
       ++it;
     };
     while (it + 1 < nfull) {
-      step(r1, g1, r0, g0);
+      step(P, Q, r1, g1);  // P = group it, r1 = group it+1 -> Q
       if (it + 1 >= nfull) break;
-      step(r2, g2, r1, g1);
-      if (it + 1 >= nfull) break;
-      step(r0, g0, r2, g2);
+      step(Q, P, r0, g0);  // Q = group it, r0 = group it+1 -> P
     }
-    enc_emit<SPL>(P, st, j, empty_lanes);
+    // the last group: in P after an even number of steps, else in Q
+    enc_emit<SPL>((it & 1) ? Q : P, st, j, empty_lanes);
     enc_flush(st, false);
     ++it;
   }
