@@ -33,12 +33,11 @@
 
 #include "ricepp_amd.h"
 
-// Diagnostic builds only: -DRPP_ABLATE=<mask> removes decode phases to time
-// them (outputs are then wrong): 1 flush, 2 extraction, 4 async ring refill,
-// 8 output stores; fast loop: 32 everything after the parse (pairs, deltas,
-// stores), 64 output stores; pipelined loop: 256 count scan, 512
-// extraction, 1024 / 4096 / 32768 20 extra v_nop / v_add / v_perm, 2048 20
-// s_nop, 8192 / 16384 an extra random / linear table read.
+// Diagnostic builds only: -DRPP_ABLATE=<mask> changes the decode to time
+// its parts (outputs are then wrong): 4 no async ring refill, 64 no output
+// stores in the fast loop; in the fast loop, per sub-block, 1024 / 4096 /
+// 32768 add 20 independent v_nop / v_add / v_perm, 2048 20 s_nop, 8192 /
+// 16384 an extra random / linear table read.
 #ifndef RPP_ABLATE
 #define RPP_ABLATE 0
 #endif
@@ -1146,7 +1145,11 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // terminator position - (q + 4) - i k (the unary part of code i is then
       // a_i - a_(i-1), a_(-1) = 0).  Returns whether the sub-block ends in the
       // window, and its end (the header of the next) in Pe.
-      auto parse = [&](uint32_t q, uint32_t xl, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
+      // The count scan also carries a rider: the previous sub-block's delta
+      // sums in the high halves (mod 2^16; counts <= 512 stay in the low
+      // halves), so that sub-block's value prefix costs no scan of its own.
+      auto parse = [&](uint32_t q, uint32_t xl, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe,
+                       uint32_t rider, uint32_t& rider_incl) -> bool {
         const uint32_t k = fs + 1;
         const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});  // (also gives byte 2's entry state)
         Map8 M = comp8(Map8{e2.x, e2.y}, M01);
@@ -1168,9 +1171,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
         // terminator mask: byte 0 of a0, a1, a2 -> bytes 0, 1, 2
         uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
-        uint32_t cnt = __builtin_popcount(tm);
-        asm volatile("" : "+v"(cnt));  // keeps the scan's first step a plain DPP add
-        const uint32_t incl = (RPP_ABLATE & 256) ? cnt + 2 * lane : wave_incl_sum(cnt);
+        const uint32_t cnt = __builtin_popcount(tm);
+        const uint32_t incl2 = wave_incl_sum(cnt | (rider << 16));
+        const uint32_t incl = incl2 & 0xFFFFu;
+        rider_incl = incl2 >> 16;
         const uint64_t finm = __ballot(incl >= n);
         const uint32_t excl = incl - cnt;
         RPP_TSTAMP(7);
@@ -1214,16 +1218,21 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         RPP_TSTAMP(13);
         return finm != 0;
       };
-      // codes 2c, 2c+1 of sub-block sx (at bit q) on lane c -> zig-zag deltas
-      // (decode.h:66-69) -> values -> stored samples
-      auto extract = [&](uint4 tt, uint32_t fs, uint32_t sx) {
+      // codes 2c, 2c+1 of a sub-block on lane c -> zig-zag deltas
+      // (decode.h:66-69): d1 and the lane's sum d0 + d1
+      auto deltas = [&](uint4 tt, uint32_t fs, uint32_t& d1, uint32_t& dsum) {
         // a of code 2c-1: lane c-1's tt.z by a wave rotate (a wave_shr
         // leaves lane 0 unwritten instead of reading 0, so it cannot be
         // fused into the subtraction); lane 0 takes a_(-1) = 0
         const uint32_t u0 = tt.x - dpp<kDppWaveRor1>(tt.z);
         const uint32_t df0 = lshl_or(lane ? u0 : tt.x, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
-        const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0), d1 = (df1 >> 1) ^ neg_lsb(df1);
-        const uint32_t inc = wave_incl_sum(d0 + d1);
+        const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
+        d1 = (df1 >> 1) ^ neg_lsb(df1);
+        dsum = d0 + d1;
+      };
+      // inclusive prefix inc of the delta sums -> values -> stored samples of
+      // sub-block sx
+      auto store = [&](uint32_t d1, uint32_t inc, uint32_t sx) {
         const uint32_t comp = sx % CS;
         const uint32_t lastc = comp ? last1 : last0;
         const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (mod 2^16)
@@ -1271,7 +1280,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       uint32_t fs = fs_of(h);
       uint4 e0, e1, e2;
       lookups(xl, fs, e0, e1, e2);
-      bool ok = parse(P, xl, fs, e0, e1, e2, Pn) && header_ok(h);
+      uint32_t unused_rider;
+      bool ok = parse(P, xl, fs, e0, e1, e2, Pn, 0u, unused_rider) && header_ok(h);
       while (ok) {
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
@@ -1282,7 +1292,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         RPP_STAT(0, 1);
         const uint32_t fsB = fs_of(hB);
         lookups(xlB, fsB, e0, e1, e2);
-        if (!(RPP_ABLATE & 512)) extract(tt, fs, s);
+        uint32_t d1A, sumA, incA;
+        deltas(tt, fs, d1A, sumA);
         if (RPP_ABLATE & 1024) asm volatile(".rept 20\n\tv_nop\n\t.endr" ::: "memory");
         if (RPP_ABLATE & 2048) asm volatile(".rept 20\n\ts_nop 0\n\t.endr" ::: "memory");
         if (RPP_ABLATE & 4096) {  // 20 independent integer VALU ops
@@ -1305,7 +1316,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         }
         RPP_TSTAMP(2);
         uint32_t PnB;
-        ok = parse(Pn, xlB, fsB, e0, e1, e2, PnB) && header_ok(hB) && nxt;
+        ok = parse(Pn, xlB, fsB, e0, e1, e2, PnB, sumA, incA) && header_ok(hB) && nxt;
+        store(d1A, incA, s);
         ++s;
         P = Pn;
         if (P > lim) {
