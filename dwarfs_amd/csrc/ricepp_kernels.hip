@@ -822,41 +822,49 @@ __device__ __forceinline__ Map8 scan_step8(Map8 m) {
 // loaded once), the rest the map from the left; out-of-range sources read 0
 // (bound_ctrl) and are always masked.  Saves the per-step identity moves a
 // DPP move into a fresh `old` needs.
-#define RPP_SCAN8_STEP(NAME, CTRL)                                                                        \
-  __device__ __forceinline__ Map8 NAME(Map8 m, Map8 id, uint64_t mask) {                                  \
-    Map8 d;                                                                                               \
-    asm("s_mov_b64 vcc, %6\n\ts_nop 0\n\t"                                                                \
-        "v_cndmask_b32_dpp %0, %2, %4, vcc " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"          \
-        "v_cndmask_b32_dpp %1, %3, %5, vcc " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1"              \
-        : "=&v"(d.lo), "=&v"(d.hi)                                                                        \
-        : "v"(m.lo), "v"(m.hi), "v"(id.lo), "v"(id.hi), "s"(mask)                                          \
-        : "vcc");                                                                                         \
-    return comp8(m, d);                                                                                   \
+// One scan step as two DPP moves into persistent registers: lanes without a
+// source (row_shr: the first lanes of each row; row_bcast: the rows the row
+// mask leaves out; wave_shr: lane 0) are not written by a DPP move without
+// bound_ctrl, so they keep the identity map the register was initialised
+// with -- no mask, no vcc.  s_nop 1: a DPP read of a VGPR written by the
+// previous VALU instruction needs two wait states.
+#define RPP_SCAN8_STEP(NAME, CTRL, RM)                                                                    \
+  __device__ __forceinline__ Map8 NAME(Map8 m, Map8& keep) {                                              \
+    asm("s_nop 1\n\t"                                                                                    \
+        "v_mov_b32_dpp %0, %2 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"                                \
+        "v_mov_b32_dpp %1, %3 " CTRL " row_mask:" RM " bank_mask:0xf"                                      \
+        : "+v"(keep.lo), "+v"(keep.hi)                                                                    \
+        : "v"(m.lo), "v"(m.hi));                                                                          \
+    return comp8(m, keep);                                                                                \
   }
-RPP_SCAN8_STEP(scan8_shr1, "row_shr:1")
-RPP_SCAN8_STEP(scan8_shr2, "row_shr:2")
-RPP_SCAN8_STEP(scan8_shr4, "row_shr:4")
-RPP_SCAN8_STEP(scan8_shr8, "row_shr:8")
-RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15")
-RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31")
-// the lanes of each step that have no source (they take the identity),
-// held in SGPR pairs across the loop (opaque, so not rematerialised)
-struct ScanMasks {
-  uint64_t r1 = 0x0001000100010001ull, r2 = 0x0003000300030003ull, r4 = 0x000F000F000F000Full,
-           r8 = 0x00FF00FF00FF00FFull, b15 = 0x0000FFFF0000FFFFull, b31 = 0x00000000FFFFFFFFull;
-  __device__ ScanMasks() { asm volatile("" : "+s"(r1), "+s"(r2), "+s"(r4), "+s"(r8), "+s"(b15), "+s"(b31)); }
+RPP_SCAN8_STEP(scan8_shr1, "row_shr:1", "0xf")
+RPP_SCAN8_STEP(scan8_shr2, "row_shr:2", "0xf")
+RPP_SCAN8_STEP(scan8_shr4, "row_shr:4", "0xf")
+RPP_SCAN8_STEP(scan8_shr8, "row_shr:8", "0xf")
+RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", "0xa")
+RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc")
+// the persistent destination registers of the six steps and of the final
+// shift, initialised to the identity map (opaque to the compiler)
+struct ScanRegs {
+  Map8 r1, r2, r4, r8, b15, b31, w1;
+  __device__ ScanRegs() {
+    Map8* all[7] = {&r1, &r2, &r4, &r8, &b15, &b31, &w1};
+    for (Map8* x : all) {
+      x->lo = kId0;
+      x->hi = kId1;
+      asm volatile("" : "+v"(x->lo), "+v"(x->hi));
+    }
+  }
 };
 #undef RPP_SCAN8_STEP
 // exclusive form: the map of lanes 0..l-1 (identity on lane 0)
-__device__ __forceinline__ Map8 shift8_wave(Map8 m, Map8 id) {
-  Map8 d;
-  asm("s_mov_b64 vcc, 1\n\ts_nop 0\n\t"
-      "v_cndmask_b32_dpp %0, %2, %4, vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_cndmask_b32_dpp %1, %3, %5, vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "=&v"(d.lo), "=&v"(d.hi)
-      : "v"(m.lo), "v"(m.hi), "v"(id.lo), "v"(id.hi)
-      : "vcc");
-  return d;
+__device__ __forceinline__ Map8 shift8_wave(Map8 m, Map8& keep) {
+  asm("s_nop 1\n\t"
+      "v_mov_b32_dpp %0, %2 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %1, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
+      : "+v"(keep.lo), "+v"(keep.hi)
+      : "v"(m.lo), "v"(m.hi));
+  return keep;
 }
 
 // 16-entry maps (states 0..15) for fs >= 8.
@@ -1098,9 +1106,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       bs == 2 * kWave && (CS == 2 || (((uintptr_t)out) & 3u) == 0) ? (N / chunk_len) * CS : 0u;
   // the stream's output as a raw buffer (N * 2 < 2^28 bytes; stores past it are dropped)
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(2 * N), 0x00020000);
-  Map8 vid{kId0, kId1};  // the identity map, kept in VGPRs for the scan steps
-  asm volatile("" : "+v"(vid.lo), "+v"(vid.hi));
-  const ScanMasks smask;
+  ScanRegs sreg;
 
   for (uint32_t s = 0; s < nsb && status == RPP_OK; ++s) {
     // ---- fast loop (the common case): Rice sub-blocks of 128 codes with fs
@@ -1153,13 +1159,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t k = fs + 1;
         const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});  // (also gives byte 2's entry state)
         Map8 M = comp8(Map8{e2.x, e2.y}, M01);
-        M = scan8_shr1(M, vid, smask.r1);
-        M = scan8_shr2(M, vid, smask.r2);
-        M = scan8_shr4(M, vid, smask.r4);
-        M = scan8_shr8(M, vid, smask.r8);
-        M = scan8_bc15(M, vid, smask.b15);
-        M = scan8_bc31(M, vid, smask.b31);
-        const Map8 X = shift8_wave(M, vid);
+        M = scan8_shr1(M, sreg.r1);
+        M = scan8_shr2(M, sreg.r2);
+        M = scan8_shr4(M, sreg.r4);
+        M = scan8_shr8(M, sreg.r8);
+        M = scan8_bc15(M, sreg.b15);
+        M = scan8_bc31(M, sreg.b31);
+        const Map8 X = shift8_wave(M, sreg.w1);
         RPP_TSTAMP(3);
         // state 4 at the window start: skip the header.  The selectors
         // carry the state in byte 0 and 0xFF (a v_perm selector for 0xFF)
