@@ -1204,7 +1204,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           tpk = r < 4 ? tpk : tpk1;
         }
         const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
-        const uint32_t lz = finm ? (uint32_t)__builtin_ctzll(finm) : 0u;
+        // (bit 63 set: a defined lane when no lane ends the sub-block; Pe is
+        // then unused)
+        const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
         Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
         RPP_TSTAMP(8);
         // pair excl + j for j = MT-1 .. 0, one instruction each (kept apart:
@@ -1326,11 +1328,11 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         store(d1A, incA, s);
         ++s;
         P = Pn;
-        if (P > lim) {
-          status = RPP_TRUNCATED_INPUT;
+        if (!ok) {
+          // (with ok, nxt held: P <= pn_limit < lim)
+          if (P > lim) status = RPP_TRUNCATED_INPUT;
           break;
         }
-        if (!ok) break;
         Pn = PnB;
         fs = fsB;
         if ((Pn >> 5) >= trig_w) {
