@@ -1260,7 +1260,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
             vm_after += 2;
           }
         }
-        const uint32_t lnew = (lastc + wave_last(inc)) & 0xFFFFu;
+        // (kept mod 2^32 here, only the low 16 bits count; masked when the
+        // loop is left)
+        const uint32_t lnew = lastc + wave_last(inc);
         if (comp) last1 = lnew;
         else last0 = lnew;
       };
@@ -1348,6 +1350,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
       if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
       else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
+      last0 &= 0xFFFFu;
+      last1 &= 0xFFFFu;
     }
     if (s >= nsb || status != RPP_OK) break;
     // ---- general path: one sub-block of any kind ----
