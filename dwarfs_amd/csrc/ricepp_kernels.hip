@@ -1344,14 +1344,17 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         RPP_TSTAMP(15);
       }
     };
-    if (s < nsb_fast && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
-      // dispatch on the sub-block's fs class
+    // dispatch on the sub-block's fs class; a loop that stops at a
+    // sub-block of the other class hands over to the other loop directly
+    while (s < nsb_fast && status == RPP_OK && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
       const uint32_t* w = ring + ((P >> 5) & kRingMask);
       const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
+      const uint32_t s0 = s;
       if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
       else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
       last0 &= 0xFFFFu;
       last1 &= 0xFFFFu;
+      if (s == s0) break;  // no progress: the general path takes this sub-block
     }
     if (s >= nsb || status != RPP_OK) break;
     // ---- general path: one sub-block of any kind ----
