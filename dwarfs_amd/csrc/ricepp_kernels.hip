@@ -1102,8 +1102,14 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint32_t nsb = nchunks * CS;
   // sub-blocks the fast loop may take: those of full 128-sample chunks
   // (CS 1: the 2-sample stores must be dword aligned)
-  const uint32_t nsb_fast =
-      bs == 2 * kWave && (CS == 2 || (((uintptr_t)out) & 3u) == 0) ? (N / chunk_len) * CS : 0u;
+  // bs 128: two codes per lane, 2-sample stores (CS 1: dword aligned);
+  // bs 16, 32, 64: one code per lane
+  const bool fast_bs = bs == 2 * kWave ? (CS == 2 || (((uintptr_t)out) & 3u) == 0)
+                                       : (bs == 16 || bs == 32 || bs == 64);
+  const uint32_t nsb_fast = fast_bs ? (N / chunk_len) * CS : 0u;
+  // one-code-per-lane stores: this lane's byte offset in a sub-block, far
+  // out of range (dropped) for lanes past it
+  const uint32_t lane_off1 = lane < bs ? 2u * CS * lane : 0x7FFFFFF0u;
   // the stream's output as a raw buffer (N * 2 < 2^28 bytes; stores past it are dropped)
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(2 * N), 0x00020000);
   ScanRegs sreg;
@@ -1119,8 +1125,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
     //      takes the general path below for that sub-block. ----
     // MT: terminators a 24-bit segment can hold (codes of >= fs + 1 bits),
     // [LO, HI]: the fs range of this instance
-    auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI>() {
-      constexpr uint32_t n = 2 * kWave;
+    // TWO: bs 128, two codes per lane; else bs <= 64, one code per lane
+    auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI, bool TWO>() {
+      const uint32_t n = TWO ? 2 * kWave : bs;
       const uint4* const list4 = reinterpret_cast<const uint4*>(list);
       uint2* const list2 = reinterpret_cast<uint2*>(list);
       // this lane's 32 bits from bit q + 24 lane (its 24-bit segment and 8
@@ -1229,21 +1236,42 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // codes 2c, 2c+1 of a sub-block on lane c -> zig-zag deltas
       // (decode.h:66-69): d1 and the lane's sum d0 + d1
       auto deltas = [&](uint4 tt, uint32_t fs, uint32_t& d1, uint32_t& dsum) {
-        // a of code 2c-1: lane c-1's tt.z by a wave rotate (a wave_shr
-        // leaves lane 0 unwritten instead of reading 0, so it cannot be
-        // fused into the subtraction); lane 0 takes a_(-1) = 0
-        const uint32_t u0 = tt.x - dpp<kDppWaveRor1>(tt.z);
-        const uint32_t df0 = lshl_or(lane ? u0 : tt.x, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
-        const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
-        d1 = (df1 >> 1) ^ neg_lsb(df1);
-        dsum = d0 + d1;
+        if constexpr (TWO) {
+          // a of code 2c-1: lane c-1's tt.z by a wave rotate (a wave_shr
+          // leaves lane 0 unwritten instead of reading 0, so it cannot be
+          // fused into the subtraction); lane 0 takes a_(-1) = 0
+          const uint32_t u0 = tt.x - dpp<kDppWaveRor1>(tt.z);
+          const uint32_t df0 = lshl_or(lane ? u0 : tt.x, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
+          const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
+          d1 = (df1 >> 1) ^ neg_lsb(df1);
+          dsum = d0 + d1;
+        } else {
+          // code c on lane c (pair c in tt.x, tt.y); lanes past the
+          // sub-block contribute nothing to the prefix
+          const uint32_t u0 = tt.x - dpp<kDppWaveRor1>(tt.x);
+          const uint32_t df = lshl_or(lane ? u0 : tt.x, fs, tt.y);
+          d1 = (df >> 1) ^ neg_lsb(df);
+          dsum = lane < n ? d1 : 0u;
+        }
       };
       // inclusive prefix inc of the delta sums -> values -> stored samples of
       // sub-block sx
       auto store = [&](uint32_t d1, uint32_t inc, uint32_t sx) {
         const uint32_t comp = sx % CS;
         const uint32_t lastc = comp ? last1 : last0;
-        const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (mod 2^16)
+        const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (TWO) or c (mod 2^16)
+        if constexpr (!TWO) {
+          const uint32_t o = SH ? px_write2(v1, selbe, ulsb) : __builtin_amdgcn_perm(v1, v1, selbe);
+          if (!(RPP_ABLATE & 64)) {
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, lane_off1,
+                                                  (int)(2 * ((sx / CS) * chunk_len + comp)), 0);
+            vm_after += 1;
+          }
+          const uint32_t lnew = lastc + wave_last(inc);
+          if (comp) last1 = lnew;
+          else last0 = lnew;
+          return;
+        }
         // samples 2c (low), 2c+1 (high) in stored order: pack and byte-swap
         // in one v_perm when there is no shift
         const uint32_t o = SH ? px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb)
@@ -1295,7 +1323,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       while (ok) {
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
-        const uint4 tt = list4[lane];
+        uint4 tt;
+        if constexpr (TWO) {
+          tt = list4[lane];
+        } else {
+          const uint2 t2 = list2[lane];
+          tt = make_uint4(t2.x, t2.y, 0u, 0u);
+        }
         const uint32_t xlB = seg_bits(Pn);
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
         RPP_TSTAMP(1);
@@ -1350,8 +1384,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       const uint32_t* w = ring + ((P >> 5) & kRingMask);
       const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
       const uint32_t s0 = s;
-      if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
-      else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
+      if (bs == 2 * kWave) {
+        if (h - 6u <= 2u) fast.template operator()<4, 5, 7, true>();
+        else if (h - 3u <= 2u) fast.template operator()<8, 2, 4, true>();
+      } else {
+        if (h - 6u <= 2u) fast.template operator()<4, 5, 7, false>();
+        else if (h - 3u <= 2u) fast.template operator()<8, 2, 4, false>();
+      }
       last0 &= 0xFFFFu;
       last1 &= 0xFFFFu;
       if (s == s0) break;  // no progress: the general path takes this sub-block

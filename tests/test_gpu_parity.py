@@ -78,20 +78,21 @@ def test_config_matrix(bs, cs):
             run_batch(codec.CodecConfig(bs, cs, "big" if be else "little", ulsb), blocks)
 
 
+@pytest.mark.parametrize("bs", [16, 32, 64, 128])
 @pytest.mark.parametrize("cs", [1, 2])
 @pytest.mark.parametrize("ulsb", [0, 4])
-def test_rice_parameter_classes(cs, ulsb):
-    """bs 128 streams whose sub-blocks take every Rice parameter (fs 0-13),
-    each class alone (the decoder's fs 2-4 and 5-7 fast loops and the
-    general path) and switching class from one sub-block to the next
-    (Poisson lambda varied per 128-sample run)."""
-    rng = np.random.default_rng(77 + 10 * cs + ulsb)
+def test_rice_parameter_classes(bs, cs, ulsb):
+    """Streams whose sub-blocks take every Rice parameter (fs 0-13), each
+    class alone (the decoder's fs 2-4 and 5-7 fast loops, one or two codes
+    per lane, and the general path) and switching class from one sub-block
+    to the next (Poisson lambda varied per sub-block run)."""
+    rng = np.random.default_rng(77 + 10 * cs + ulsb + bs)
     lams = [0.3, 2, 6, 20, 60, 200, 600, 2000, 6000, 20000]
-    blocks = [datagen.poisson_data(rng, 128 * cs * 40, lam=lam, ulsb=ulsb) for lam in lams]
-    runs = [datagen.poisson_data(rng, 128 * cs, lam=lams[int(rng.integers(0, len(lams)))], ulsb=ulsb)
+    blocks = [datagen.poisson_data(rng, bs * cs * 40, lam=lam, ulsb=ulsb) for lam in lams]
+    runs = [datagen.poisson_data(rng, bs * cs, lam=lams[int(rng.integers(0, len(lams)))], ulsb=ulsb)
             for _ in range(120)]
     blocks.append(np.concatenate(runs))
-    run_batch(codec.CodecConfig(128, cs, "big", ulsb), blocks)
+    run_batch(codec.CodecConfig(bs, cs, "big", ulsb), blocks)
 
 
 @pytest.mark.parametrize("ulsb", list(range(0, 16)))
