@@ -47,31 +47,74 @@ def partition_blocks(block_bytes: Sequence[int], world: int) -> List[Tuple[int, 
     return ranges
 
 
+class SizeGather:
+    """All-gather of int64 per-block encoded sizes, rank order, ragged counts
+    allowed.  The per-rank block counts are fixed for a shard, so they are
+    exchanged once (the only host synchronisation); every later call is one
+    collective into preallocated buffers: `all_gather_into_tensor` straight
+    from the sizes when every rank holds the same count (RCCL on the GPU
+    path), else pad -> gather -> one index_select."""
+
+    def __init__(self, local_count: int, device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if group is not None and dist.is_initialized() else 1
+        self.device = torch.device(device)
+        if self.world == 1:
+            self.counts = [local_count]
+            return
+        cnt = torch.tensor([local_count], dtype=torch.int64, device=self.device)
+        counts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(counts, cnt, group=group)
+        self.counts = [int(c.item()) for c in counts]
+        self.m = max(self.counts)
+        self.uniform = all(c == self.m for c in self.counts)
+        self.out = torch.empty(self.world * self.m, dtype=torch.int64, device=self.device)
+        self.padded = None if self.uniform else torch.zeros(self.m, dtype=torch.int64, device=self.device)
+        if not self.uniform:
+            idx = np.concatenate([r * self.m + np.arange(c) for r, c in enumerate(self.counts)]).astype(np.int64)
+            self.index = torch.as_tensor(idx, device=self.device)
+            self.result = torch.empty(int(sum(self.counts)), dtype=torch.int64, device=self.device)
+
+    def __call__(self, local_sizes: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return local_sizes
+        if local_sizes.numel() != self.counts[dist.get_rank(self.group)]:
+            raise ValueError("SizeGather: local block count changed")
+        src = local_sizes
+        if not self.uniform:
+            self.padded[: local_sizes.numel()] = local_sizes
+            src = self.padded
+        if self.device.type == "cuda":
+            dist.all_gather_into_tensor(self.out, src, group=self.group)
+        else:
+            dist.all_gather(list(self.out.view(self.world, self.m)), src, group=self.group)
+        if self.uniform:
+            return self.out
+        return torch.index_select(self.out, 0, self.index, out=self.result)
+
+
 def gather_sizes(local_sizes: torch.Tensor, group=None) -> torch.Tensor:
     """All-gathers int64 per-block sizes from every rank (ragged counts
-    allowed) and returns them concatenated in rank order."""
+    allowed) and returns them concatenated in rank order (one-shot form of
+    SizeGather)."""
     if group is None or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return local_sizes
-    world = dist.get_world_size(group)
-    cnt = torch.tensor([local_sizes.numel()], dtype=torch.int64, device=local_sizes.device)
-    counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
-    m = max(counts)
-    padded = torch.zeros(m, dtype=torch.int64, device=local_sizes.device)
-    padded[: local_sizes.numel()] = local_sizes
-    if local_sizes.device.type == "cuda":
-        out = torch.empty(world * m, dtype=torch.int64, device=local_sizes.device)
-        dist.all_gather_into_tensor(out, padded, group=group)
-        parts = out.view(world, m)
-        return torch.cat([parts[r, : counts[r]] for r in range(world)])
-    parts = [torch.zeros(m, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(parts, padded, group=group)
-    return torch.cat([parts[r][: counts[r]] for r in range(world)])
+    return SizeGather(local_sizes.numel(), local_sizes.device, group)(local_sizes)
 
 
-def global_offsets(all_sizes: torch.Tensor) -> torch.Tensor:
-    """Exclusive prefix sum: byte offset of every block in the concatenated image."""
+def global_offsets(all_sizes: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Exclusive prefix sum: byte offset of every block in the concatenated
+    image.  Device sizes: one launch of the native scan
+    (rpp_exclusive_scan_u64) on the current stream; host sizes (the gloo
+    path): torch on the CPU."""
+    if all_sizes.device.type == "cuda":
+        sizes = all_sizes.contiguous()
+        if out is None or out.numel() != sizes.numel():
+            out = torch.empty_like(sizes)
+        _raise_status(N.lib().rpp_exclusive_scan_u64(
+            C.c_void_p(sizes.data_ptr()), sizes.numel(), C.c_void_p(out.data_ptr()),
+            C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        return out
     off = torch.zeros_like(all_sizes)
     if all_sizes.numel() > 1:
         off[1:] = torch.cumsum(all_sizes[:-1], 0)
@@ -80,8 +123,8 @@ def global_offsets(all_sizes: torch.Tensor) -> torch.Tensor:
 
 class ShardPipeline:
     """This rank's shard of blocks, resident on its GPU, with every device
-    array preallocated so one step is three launches (encode, size gather,
-    decode) and no host-device synchronisation."""
+    array preallocated so one step is encode, size all-gather + image-offset
+    scan, decode, and no host-device synchronisation."""
 
     def __init__(self, config: CodecConfig, samples: torch.Tensor, in_offsets, n_samples, group=None):
         self.cfg = _check(config)
@@ -111,6 +154,7 @@ class ShardPipeline:
         self.dec_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
         self.all_sizes: Optional[torch.Tensor] = None
         self.image_offsets: Optional[torch.Tensor] = None
+        self.size_gather = SizeGather(self.nblocks, dev, group)
 
         class _Enc:
             pass
@@ -136,10 +180,14 @@ class ShardPipeline:
             C.c_void_p(self.dec_status.data_ptr()), self._stream()))
 
     def gather(self) -> None:
-        self.all_sizes = gather_sizes(self.sizes, self.group)
-        self.image_offsets = global_offsets(self.all_sizes)
+        self.all_sizes = self.size_gather(self.sizes)
+        self.image_offsets = global_offsets(self.all_sizes, self.image_offsets)
 
     def step(self) -> None:
+        """encode -> size all-gather + image-offset scan -> decode, in stream
+        order.  (A side stream overlapping the gather/scan with the decode
+        measured slower at N=1: the cross-stream dependency opened a ~7 us
+        gap before the decode, more than the 5 us scan it hid.)"""
         self.encode()
         self.gather()
         self.decode()

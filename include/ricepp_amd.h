@@ -23,6 +23,8 @@
  *   rpp_unused_lsb_batch  <- the FITS categorizer's unused-LSB detection
  *                            (src/writer/categorizer/fits_categorizer.cpp:118-178),
  *                            which picks the codec's unused_lsb_count
+ *   rpp_exclusive_scan_u64 <- the writer's running image offset as it appends
+ *                            compressed blocks (src/writer/filesystem_writer.cpp:255-287)
  *   rpp_frame_header /    <- the DwarFS block framing of src/compression/ricepp.cpp:
  *   rpp_parse_frame          varint size + thrift-compact ricepp_block_header
  *                            (:107-127 write, :186-201,237-249 read)
@@ -123,6 +125,16 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
 int rpp_unused_lsb_batch(const uint16_t* d_in, const uint64_t* d_offsets, const uint64_t* d_n_samples,
                          uint64_t max_samples, uint32_t nimages, uint32_t big_endian, uint32_t* d_work,
                          uint32_t* d_counts, void* stream);
+
+/*
+ * Image offsets of a batch of compressed blocks: d_out[b] = sum of d_in[0..b-1]
+ * (exclusive prefix sum, uint64).  The DwarFS writer appends compressed blocks
+ * back to back (src/writer/filesystem_writer.cpp:255-287); with the encoded
+ * sizes of a GPU batch in device memory (all-gathered across ranks) this gives
+ * every block's position in the image without a host round trip.
+ * d_in may equal d_out only if n <= 1.  Asynchronous on `stream`.
+ */
+int rpp_exclusive_scan_u64(const uint64_t* d_in, uint64_t n, uint64_t* d_out, void* stream);
 
 /*
  * DwarFS ricepp block framing (host memory).  rpp_frame_header writes

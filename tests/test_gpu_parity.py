@@ -264,3 +264,19 @@ def test_large_blocks(mib):
     blocks = [datagen.poisson_data(rng, n), datagen.benchmark_data(rng, n // 2)]
     run_batch(codec.CodecConfig(128, 1, "big", 0), blocks)
     run_batch(codec.CodecConfig(128, 2, "big", 0), [blocks[0]])
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 1000, 4096, 4097, 12289, 100000])
+def test_image_offsets_scan(n):
+    """rpp_exclusive_scan_u64 (image offsets of appended blocks) against numpy,
+    across one and several 4096-entry passes and ragged tails."""
+    from dwarfs_amd import parallel
+    rng = np.random.default_rng(n)
+    sizes = rng.integers(0, 1 << 40, n, dtype=np.int64) if n != 1000 else rng.integers(0, 200000, n, dtype=np.int64)
+    d = torch.as_tensor(sizes, device=DEV)
+    got = parallel.global_offsets(d)
+    torch.cuda.synchronize()
+    want = np.zeros(n, np.int64)
+    if n > 1:
+        want[1:] = np.cumsum(sizes)[:-1]
+    assert np.array_equal(got.cpu().numpy(), want)

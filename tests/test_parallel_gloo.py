@@ -88,3 +88,33 @@ def test_world2_gather_sizes_and_image_offsets(tmp_path):
     b0 = sum(b.nbytes for b in blocks[lo0:hi0])
     total = sum(b.nbytes for b in blocks)
     assert abs(b0 - total / 2) <= max(b.nbytes for b in blocks)
+
+
+def _size_gather_worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    for name, count in (("uniform", 5), ("ragged", 3 + 4 * rank), ("empty", 0 if rank == 0 else 6)):
+        g = parallel.SizeGather(count, "cpu", dist.group.WORLD)
+        got = []
+        for step in range(3):  # the cached buffers are reused every step
+            sizes = torch.arange(count, dtype=torch.int64) + 1000 * rank + 100 * step
+            all_sizes = g(sizes)
+            got.append([all_sizes.tolist(), parallel.global_offsets(all_sizes).tolist()])
+        res[name] = got
+    if rank == 0:
+        json.dump(res, open(out_path, "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_world2_size_gather_cached_uniform_and_ragged(tmp_path):
+    out = tmp_path / "sg.json"
+    mp.spawn(_size_gather_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    res = json.loads(out.read_text())
+    for name, counts in (("uniform", [5, 5]), ("ragged", [3, 7]), ("empty", [0, 6])):
+        for step, (sizes, offs) in enumerate(res[name]):
+            want = [v for r, c in enumerate(counts) for v in (np.arange(c) + 1000 * r + 100 * step).tolist()]
+            assert sizes == want, name
+            assert offs == [0] + np.cumsum(want)[:-1].tolist() if want else offs == [], name
