@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "rpp_decode_batch",
     "rpp_unused_lsb_batch",
     "rpp_exclusive_scan_u64",
+    "rpp_pack_batch",
     "rpp_frame_header",
     "rpp_parse_frame",
 )
@@ -93,6 +94,8 @@ def lib() -> C.CDLL:
         L.rpp_unused_lsb_batch.restype = C.c_int
         L.rpp_exclusive_scan_u64.argtypes = [P, C.c_uint64, P, P]
         L.rpp_exclusive_scan_u64.restype = C.c_int
+        L.rpp_pack_batch.argtypes = [P, P, P, C.c_uint32, P, P, P, P]
+        L.rpp_pack_batch.restype = C.c_int
         L.rpp_frame_header.argtypes = [C.POINTER(RppFrame), P]
         L.rpp_frame_header.restype = C.c_size_t
         L.rpp_parse_frame.argtypes = [P, C.c_size_t, C.POINTER(RppFrame)]

@@ -24,7 +24,7 @@
  *                            (src/writer/categorizer/fits_categorizer.cpp:118-178),
  *                            which picks the codec's unused_lsb_count
  *   rpp_exclusive_scan_u64 <- the writer's running image offset as it appends
- *                            compressed blocks (src/writer/filesystem_writer.cpp:255-287)
+ *   rpp_pack_batch           compressed blocks (src/writer/filesystem_writer.cpp:255-287)
  *   rpp_frame_header /    <- the DwarFS block framing of src/compression/ricepp.cpp:
  *   rpp_parse_frame          varint size + thrift-compact ricepp_block_header
  *                            (:107-127 write, :186-201,237-249 read)
@@ -135,6 +135,20 @@ int rpp_unused_lsb_batch(const uint16_t* d_in, const uint64_t* d_offsets, const 
  * d_in may equal d_out only if n <= 1.  Asynchronous on `stream`.
  */
 int rpp_exclusive_scan_u64(const uint64_t* d_in, uint64_t n, uint64_t* d_out, void* stream);
+
+/*
+ * Pack the encoded streams of a batch (e.g. rpp_encode_batch output, block b at
+ * d_src + d_src_offsets[b], 16-aligned, d_sizes[b] bytes) back to back at
+ * 16-byte-aligned offsets: d_dst_offsets[b] = sum of round_up(d_sizes[j], 16)
+ * for j < b, block b's bytes copied to d_dst + d_dst_offsets[b], *d_total =
+ * the packed length.  d_dst must hold sum(round_up(sizes, 16)) bytes (at most
+ * the sum of the encode capacities); the source slots must be readable up to
+ * round_up(size, 16).  Then one device->host copy of *d_total bytes moves the
+ * batch, instead of its worst-case capacity (the writer's block hand-off,
+ * src/writer/filesystem_writer.cpp:255-287).  Asynchronous on `stream`.
+ */
+int rpp_pack_batch(const uint8_t* d_src, const uint64_t* d_src_offsets, const uint64_t* d_sizes, uint32_t nblocks,
+                   uint8_t* d_dst, uint64_t* d_dst_offsets, uint64_t* d_total, void* stream);
 
 /*
  * DwarFS ricepp block framing (host memory).  rpp_frame_header writes
