@@ -42,6 +42,9 @@ EXPORTED_SYMBOLS = (
     "rpp_pack_batch",
     "rpp_frame_header",
     "rpp_parse_frame",
+    "rpp_pcm_check_format",
+    "rpp_pcm_unpack",
+    "rpp_pcm_pack",
 )
 
 
@@ -65,6 +68,19 @@ class RppFrame(C.Structure):
         ("unused_lsb_count", C.c_uint32),
         ("big_endian", C.c_uint32),
         ("ricepp_version", C.c_uint32),
+    ]
+
+
+class RppPcmFormat(C.Structure):
+    """``rpp_pcm_format`` (pcm_sample_transformer's constructor arguments,
+    include/dwarfs/pcm_sample_transformer.h:36-45)."""
+
+    _fields_ = [
+        ("big_endian", C.c_uint32),
+        ("is_signed", C.c_uint32),
+        ("lsb_padded", C.c_uint32),
+        ("bytes", C.c_uint32),
+        ("bits", C.c_uint32),
     ]
 
 
@@ -100,6 +116,12 @@ def lib() -> C.CDLL:
         L.rpp_frame_header.restype = C.c_size_t
         L.rpp_parse_frame.argtypes = [P, C.c_size_t, C.POINTER(RppFrame)]
         L.rpp_parse_frame.restype = C.c_long
+        L.rpp_pcm_check_format.argtypes = [C.POINTER(RppPcmFormat)]
+        L.rpp_pcm_check_format.restype = C.c_int
+        L.rpp_pcm_unpack.argtypes = [C.POINTER(RppPcmFormat), P, P, C.c_uint64, P]
+        L.rpp_pcm_unpack.restype = C.c_int
+        L.rpp_pcm_pack.argtypes = [C.POINTER(RppPcmFormat), P, P, C.c_uint64, P]
+        L.rpp_pcm_pack.restype = C.c_int
         if L.rpp_abi_version() != 1:
             raise RuntimeError("libricepp_amd.so ABI mismatch")
         _lib = L

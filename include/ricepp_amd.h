@@ -25,6 +25,10 @@
  *                            which picks the codec's unused_lsb_count
  *   rpp_exclusive_scan_u64 <- the writer's running image offset as it appends
  *   rpp_pack_batch           compressed blocks (src/writer/filesystem_writer.cpp:255-287)
+ *   rpp_pcm_unpack /      <- pcm_sample_transformer<int32_t>::unpack / pack
+ *   rpp_pcm_pack             (include/dwarfs/pcm_sample_transformer.h:40-71,
+ *                            src/pcm_sample_transformer.cpp:44-228), the PCM
+ *                            front end of the FLAC compressor (src/compression/flac.cpp:211,322)
  *   rpp_frame_header /    <- the DwarFS block framing of src/compression/ricepp.cpp:
  *   rpp_parse_frame          varint size + thrift-compact ricepp_block_header
  *                            (:107-127 write, :186-201,237-249 read)
@@ -169,6 +173,35 @@ typedef struct rpp_frame {
 
 size_t rpp_frame_header(const rpp_frame* f, uint8_t* out);
 long rpp_parse_frame(const uint8_t* in, size_t in_len, rpp_frame* f);
+
+/*
+ * PCM sample format (pcm_sample_transformer's constructor arguments,
+ * include/dwarfs/pcm_sample_transformer.h:36-45): bytes per sample 1..4,
+ * significant bits 1..8*bytes, big_endian / is_signed / lsb_padded as 0/1.
+ * rpp_pcm_check_format: RPP_OK; RPP_UNSUPPORTED_CONFIG for bytes outside 1..4
+ * (the reference's runtime_error "unsupported number of bytes per sample: N",
+ * src/pcm_sample_transformer.cpp:310-311); RPP_INVALID_ARGUMENT for bits
+ * outside 1..8*bytes (asserted by the reference, :354).
+ */
+typedef struct rpp_pcm_format {
+  uint32_t big_endian;
+  uint32_t is_signed;
+  uint32_t lsb_padded;
+  uint32_t bytes;
+  uint32_t bits;
+} rpp_pcm_format;
+
+int rpp_pcm_check_format(const rpp_pcm_format* f);
+
+/*
+ * n_samples PCM samples of `bytes` bytes each at d_src -> int32 at d_dst
+ * (pcm_sample_transformer<int32_t>::unpack), and the inverse
+ * (pcm_sample_transformer<int32_t>::pack).  Device memory; asynchronous on
+ * `stream`.  Any alignment is accepted (4-byte packed / 16-byte int32 buffers
+ * take the vector path).
+ */
+int rpp_pcm_unpack(const rpp_pcm_format* f, const uint8_t* d_src, int32_t* d_dst, uint64_t n_samples, void* stream);
+int rpp_pcm_pack(const rpp_pcm_format* f, const int32_t* d_src, uint8_t* d_dst, uint64_t n_samples, void* stream);
 
 #ifdef __cplusplus
 }

@@ -163,3 +163,51 @@ def unused_lsb_count(samples: np.ndarray, big_endian: bool = True) -> int:
     if b16 == 0:
         return 16
     return (b16 & -b16).bit_length() - 1
+
+
+def _pcm_args(big_endian, is_signed, lsb_padded, nbytes, bits):
+    if not 1 <= nbytes <= 4:
+        # src/pcm_sample_transformer.cpp:310-311
+        raise RuntimeError(f"unsupported number of bytes per sample: {nbytes}")
+    if not 1 <= bits <= 8 * nbytes:  # asserted at :354
+        raise ValueError(f"bits {bits} outside 1..{8 * nbytes}")
+
+
+def pcm_unpack(packed, big_endian, is_signed, lsb_padded, nbytes, bits) -> np.ndarray:
+    """pcm_sample_transformer<int32_t>::unpack (src/pcm_sample_transformer.cpp:
+    50-93 byte assembly, :141-158 unpack_native), vectorised over samples with
+    uint32 arithmetic mod 2^32: Lsb padding shifts right by 8*bytes-bits;
+    signed sign-extends from bit bits-1 when bits < 32 (upper bits otherwise
+    kept, no masking); unsigned subtracts 1 << (bits-1)."""
+    _pcm_args(big_endian, is_signed, lsb_padded, nbytes, bits)
+    b = np.frombuffer(bytes(packed), np.uint8).reshape(-1, nbytes).astype(np.uint32)
+    t = np.zeros(b.shape[0], np.uint32)
+    for k in range(nbytes):
+        sh = 8 * (nbytes - 1 - k) if big_endian else 8 * k
+        t |= b[:, k] << np.uint32(sh)
+    if lsb_padded:
+        t >>= np.uint32(8 * nbytes - bits)
+    if is_signed:
+        if bits < 32:
+            neg = (t & np.uint32(1 << (bits - 1))) != 0
+            t = np.where(neg, t | np.uint32((0xFFFFFFFF << bits) & 0xFFFFFFFF), t)
+    else:
+        t = t - np.uint32(1 << (bits - 1))
+    return t.astype(np.uint32).view(np.int32)
+
+
+def pcm_pack(samples, big_endian, is_signed, lsb_padded, nbytes, bits) -> bytes:
+    """pcm_sample_transformer<int32_t>::pack (src/pcm_sample_transformer.cpp:
+    160-171 pack_native, :97-138 byte order): unsigned adds 1 << (bits-1), Lsb
+    padding shifts left by 8*bytes-bits, the low `bytes` bytes are stored."""
+    _pcm_args(big_endian, is_signed, lsb_padded, nbytes, bits)
+    s = np.asarray(samples, np.int32).view(np.uint32).copy()
+    if not is_signed:
+        s = s + np.uint32(1 << (bits - 1))
+    if lsb_padded:
+        s = s << np.uint32(8 * nbytes - bits)
+    out = np.zeros((s.shape[0], nbytes), np.uint8)
+    for k in range(nbytes):
+        sh = 8 * (nbytes - 1 - k) if big_endian else 8 * k
+        out[:, k] = (s >> np.uint32(sh)) & np.uint32(0xFF)
+    return out.tobytes()
