@@ -351,4 +351,54 @@ std::vector<uint8_t> block_decompressor::decompress(std::span<uint8_t const> dat
   return out;
 }
 
+// ---- pcm_sample_transformer (src/pcm_sample_transformer.cpp:372-377) ----
+
+struct pcm_sample_transformer::impl {
+  device_ctx ctx;
+};
+
+pcm_sample_transformer::pcm_sample_transformer(pcm_sample_endianness end, pcm_sample_signedness sig,
+                                               pcm_sample_padding pad, int bytes, int bits) {
+  fmt_.big_endian = end == pcm_sample_endianness::Big ? 1u : 0u;
+  fmt_.is_signed = sig == pcm_sample_signedness::Signed ? 1u : 0u;
+  fmt_.lsb_padded = pad == pcm_sample_padding::Lsb ? 1u : 0u;
+  fmt_.bytes = bytes < 0 ? 0u : static_cast<uint32_t>(bytes);
+  fmt_.bits = bits < 0 ? 0u : static_cast<uint32_t>(bits);
+  const int st = rpp_pcm_check_format(&fmt_);
+  if (st == RPP_UNSUPPORTED_CONFIG || bytes < 1 || bytes > 4)
+    throw std::runtime_error("unsupported number of bytes per sample: " + std::to_string(bytes));
+  if (st != RPP_OK) throw std::invalid_argument("pcm_sample_transformer: bits outside 1..8*bytes");
+  impl_ = std::make_unique<impl>();
+}
+
+pcm_sample_transformer::~pcm_sample_transformer() = default;
+pcm_sample_transformer::pcm_sample_transformer(pcm_sample_transformer&&) noexcept = default;
+pcm_sample_transformer& pcm_sample_transformer::operator=(pcm_sample_transformer&&) noexcept = default;
+
+void pcm_sample_transformer::unpack(std::span<int32_t> dst, std::span<uint8_t const> src) const {
+  if (src.size() != fmt_.bytes * dst.size()) throw std::invalid_argument("pcm unpack: src.size() != bytes * dst.size()");
+  if (dst.empty()) return;
+  const size_t off_out = align16(src.size());
+  uint8_t* d = impl_->ctx.reserve(off_out + dst.size_bytes());
+  hipStream_t s = impl_->ctx.stream();
+  hip_check(hipMemcpyAsync(d, src.data(), src.size(), hipMemcpyHostToDevice, s), "H2D pcm");
+  const int st = rpp_pcm_unpack(&fmt_, d, reinterpret_cast<int32_t*>(d + off_out), dst.size(), s);
+  if (st != RPP_OK) throw_status(st);
+  hip_check(hipMemcpyAsync(dst.data(), d + off_out, dst.size_bytes(), hipMemcpyDeviceToHost, s), "D2H pcm");
+  hip_check(hipStreamSynchronize(s), "sync");
+}
+
+void pcm_sample_transformer::pack(std::span<uint8_t> dst, std::span<int32_t const> src) const {
+  if (dst.size() != fmt_.bytes * src.size()) throw std::invalid_argument("pcm pack: dst.size() != bytes * src.size()");
+  if (src.empty()) return;
+  const size_t off_out = align16(src.size_bytes());
+  uint8_t* d = impl_->ctx.reserve(off_out + dst.size());
+  hipStream_t s = impl_->ctx.stream();
+  hip_check(hipMemcpyAsync(d, src.data(), src.size_bytes(), hipMemcpyHostToDevice, s), "H2D pcm");
+  const int st = rpp_pcm_pack(&fmt_, reinterpret_cast<int32_t const*>(d), d + off_out, src.size(), s);
+  if (st != RPP_OK) throw_status(st);
+  hip_check(hipMemcpyAsync(dst.data(), d + off_out, dst.size(), hipMemcpyDeviceToHost, s), "D2H pcm");
+  hip_check(hipStreamSynchronize(s), "sync");
+}
+
 }  // namespace ricepp_amd

@@ -107,4 +107,35 @@ class block_decompressor {
   std::vector<uint8_t>* target_ = nullptr;
 };
 
+// ---- PCM sample transformer (include/dwarfs/pcm_sample_transformer.h:36-71) ----
+//
+// pcm_sample_transformer<int32_t>: (end, sig, pad, bytes, bits) -> unpack / pack
+// of interleaved PCM bytes, on the GPU (rpp_pcm_unpack / rpp_pcm_pack) through
+// a private stream and device staging buffer.  Throws std::runtime_error
+// ("unsupported number of bytes per sample: N") like
+// src/pcm_sample_transformer.cpp:310-311, std::invalid_argument for bits
+// outside 1..8*bytes (an assert in the reference, :354) and for spans whose
+// sizes disagree (asserts at :185,194).
+
+enum class pcm_sample_endianness { Big, Little };
+enum class pcm_sample_signedness { Signed, Unsigned };
+enum class pcm_sample_padding { Lsb, Msb };
+
+class pcm_sample_transformer {
+ public:
+  pcm_sample_transformer(pcm_sample_endianness end, pcm_sample_signedness sig, pcm_sample_padding pad, int bytes,
+                         int bits);
+  ~pcm_sample_transformer();
+  pcm_sample_transformer(pcm_sample_transformer&&) noexcept;
+  pcm_sample_transformer& operator=(pcm_sample_transformer&&) noexcept;
+
+  void unpack(std::span<int32_t> dst, std::span<uint8_t const> src) const;
+  void pack(std::span<uint8_t> dst, std::span<int32_t const> src) const;
+
+ private:
+  struct impl;
+  rpp_pcm_format fmt_{};
+  std::unique_ptr<impl> impl_;
+};
+
 }  // namespace ricepp_amd

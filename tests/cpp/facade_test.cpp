@@ -166,6 +166,34 @@ int main() {
     CHECK(comp.metadata_requirements() ==
           R"({"bytes_per_sample":["set",[2]],"component_count":["range",1,2],"endianness":["set",["big","little"]],"unused_lsb_count":["range",0,8]})");
   }
+  // test/pcm_sample_transformer_test.cpp:33-52 (uint8_8bit) and :258-293 (int24_20bit_be_lsb)
+  {
+    using namespace ricepp_amd;
+    pcm_sample_transformer x8(pcm_sample_endianness::Big, pcm_sample_signedness::Unsigned, pcm_sample_padding::Msb, 1,
+                              8);
+    std::vector<uint8_t> packed{0, 1, 42, 254, 255}, repacked(5);
+    std::vector<int32_t> unpacked(5);
+    x8.unpack(unpacked, packed);
+    x8.pack(repacked, unpacked);
+    CHECK((unpacked == std::vector<int32_t>{-128, -127, -86, 126, 127}));
+    CHECK(repacked == packed);
+    pcm_sample_transformer x24(pcm_sample_endianness::Big, pcm_sample_signedness::Signed, pcm_sample_padding::Lsb, 3,
+                               20);
+    std::vector<int32_t> ref{-524288, -524287, -1, 0, 1, 524286, 524287}, u(7);
+    std::vector<uint8_t> p(21), rp(21);
+    for (size_t i = 0; i < ref.size(); ++i) {
+      const uint32_t v = static_cast<uint32_t>(ref[i]) << 4;
+      p[3 * i] = uint8_t(v >> 16), p[3 * i + 1] = uint8_t(v >> 8), p[3 * i + 2] = uint8_t(v);
+    }
+    x24.unpack(u, p);
+    x24.pack(rp, u);
+    CHECK(u == ref);
+    CHECK(rp == p);
+    CHECK(throws<std::runtime_error>(
+        [] { pcm_sample_transformer t(pcm_sample_endianness::Big, pcm_sample_signedness::Signed,
+                                      pcm_sample_padding::Lsb, 5, 16); },
+        "unsupported number of bytes per sample: 5"));
+  }
   std::printf("facade_test: %s (%d failures)\n", failures ? "FAILED" : "OK", failures);
   return failures ? 1 : 0;
 }
