@@ -47,6 +47,24 @@ def make_poisson_blocks(nblocks: int, n: int, lam: float, seed: int, device) -> 
     return out
 
 
+def device_copy_gbps(dev, nbytes: int = 1 << 30, iters: int = 10) -> float:
+    """Measured device-to-device copy rate (read + write bytes / s), the
+    'achievable' HBM reference of SURVEY.md §8(d) beside the 8 TB/s spec peak."""
+    a = torch.ones(nbytes // 4, dtype=torch.int32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        b.copy_(a)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    gbps = 2 * nbytes * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    return gbps
+
+
 def cpu_baseline(sample: np.ndarray, nblocks: int, n: int, cfg: codec.CodecConfig, min_seconds: float):
     """The CPU oracle (C restatement of ricepp, kind "port") on host cores."""
     from oracle import oracle as O
@@ -177,6 +195,7 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "device_copy_GBps": round(device_copy_gbps(dev), 1),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
