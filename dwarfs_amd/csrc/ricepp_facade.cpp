@@ -12,6 +12,7 @@
 #include <charconv>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 
 namespace ricepp_amd {
@@ -100,6 +101,7 @@ class encoder_impl final : public encoder {
     if (output.size() < wc) throw std::length_error("ricepp_amd: output smaller than worst_case_encoded_bytes");
     size_t const in_bytes = input.size() * 2;
     size_t const off_in = 64, off_out = off_in + align16(in_bytes);
+    std::lock_guard<std::mutex> lock(mu_);  // const and re-entrant like the reference's object
     uint8_t* d = ctx_.reserve(off_out + align16(wc) + 16);
     params hp{0, input.size(), 0, 0, 0, 0, 0};
     auto* dp = reinterpret_cast<params*>(d);
@@ -119,6 +121,7 @@ class encoder_impl final : public encoder {
 
  private:
   rpp_config cfg_;
+  mutable std::mutex mu_;
   mutable device_ctx ctx_;
 };
 
@@ -129,6 +132,7 @@ class decoder_impl final : public decoder {
   // ricepp_cpuspecific.cpp:127-144: decodes exactly output.size() samples
   void decode(std::span<uint16_t> output, std::span<uint8_t const> input) const override {
     size_t const off_in = 64, off_out = off_in + align16(input.size()) + 16;
+    std::lock_guard<std::mutex> lock(mu_);  // const and re-entrant like the reference's object
     uint8_t* d = ctx_.reserve(off_out + align16(output.size() * 2) + 16);
     params hp{0, output.size(), 0, input.size(), 0, 0, 0};
     auto* dp = reinterpret_cast<params*>(d);
@@ -149,6 +153,7 @@ class decoder_impl final : public decoder {
 
  private:
   rpp_config cfg_;
+  mutable std::mutex mu_;
   mutable device_ctx ctx_;
 };
 
@@ -354,6 +359,7 @@ std::vector<uint8_t> block_decompressor::decompress(std::span<uint8_t const> dat
 // ---- pcm_sample_transformer (src/pcm_sample_transformer.cpp:372-377) ----
 
 struct pcm_sample_transformer::impl {
+  std::mutex mu;
   device_ctx ctx;
 };
 
@@ -379,6 +385,7 @@ void pcm_sample_transformer::unpack(std::span<int32_t> dst, std::span<uint8_t co
   if (src.size() != fmt_.bytes * dst.size()) throw std::invalid_argument("pcm unpack: src.size() != bytes * dst.size()");
   if (dst.empty()) return;
   const size_t off_out = align16(src.size());
+  std::lock_guard<std::mutex> lock(impl_->mu);
   uint8_t* d = impl_->ctx.reserve(off_out + dst.size_bytes());
   hipStream_t s = impl_->ctx.stream();
   hip_check(hipMemcpyAsync(d, src.data(), src.size(), hipMemcpyHostToDevice, s), "H2D pcm");
@@ -392,6 +399,7 @@ void pcm_sample_transformer::pack(std::span<uint8_t> dst, std::span<int32_t cons
   if (dst.size() != fmt_.bytes * src.size()) throw std::invalid_argument("pcm pack: dst.size() != bytes * src.size()");
   if (src.empty()) return;
   const size_t off_out = align16(src.size_bytes());
+  std::lock_guard<std::mutex> lock(impl_->mu);
   uint8_t* d = impl_->ctx.reserve(off_out + dst.size());
   hipStream_t s = impl_->ctx.stream();
   hip_check(hipMemcpyAsync(d, src.data(), src.size_bytes(), hipMemcpyHostToDevice, s), "H2D pcm");

@@ -17,9 +17,13 @@
 //    with the same framing, metadata JSON, constraints and error messages.
 //
 // Host spans in, host spans out: the facade stages through device buffers on
-// its own HIP stream (one per object; objects are safe to use from one thread
-// at a time -- clone() per worker thread, as DwarFS does with
-// block_compressor::impl).  The device-resident batch API (rpp_encode_batch /
+// its own HIP stream (one per object).  Every method is const and may be
+// called from several threads at once, as the reference's immutable objects
+// can: an encoder / decoder / pcm_sample_transformer serialises its calls on a
+// per-object lock; block_compressor::compress creates its encoder per call
+// (src/compression/ricepp.cpp:97-102), so DwarFS's worker_group threads
+// compressing through one impl (src/writer/filesystem_writer.cpp:259-268) run
+// concurrently, one stream each.  The device-resident batch API (rpp_encode_batch /
 // rpp_decode_batch) is the fast path; this facade is the drop-in.
 #pragma once
 

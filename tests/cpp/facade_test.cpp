@@ -8,6 +8,7 @@
 #include <random>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ricepp_amd.hpp"
@@ -165,6 +166,40 @@ int main() {
     CHECK(throws<std::runtime_error>([] { ricepp_amd::block_compressor::create("ricepp:block_size=8"); }));
     CHECK(comp.metadata_requirements() ==
           R"({"bytes_per_sample":["set",[2]],"component_count":["range",1,2],"endianness":["set",["big","little"]],"unused_lsb_count":["range",0,8]})");
+  }
+  // concurrency: DwarFS's worker_group calls compress on one block_compressor
+  // impl from many threads (src/writer/filesystem_writer.cpp:259-268); the
+  // reference's encoder/decoder objects are const and re-entrant.  8 threads
+  // share one compressor, one encoder and one decoder; every stream is checked
+  // against the oracle.
+  {
+    using ricepp_amd::byteorder;
+    ricepp_amd::codec_config c{128, 1, byteorder::big, 0};
+    auto shared_enc = ricepp_amd::create_encoder(c);
+    auto shared_dec = ricepp_amd::create_decoder(c);
+    ricepp_amd::block_compressor comp{128};
+    std::string const meta =
+        R"({"bytes_per_sample":2,"component_count":1,"endianness":"big","unused_lsb_count":0})";
+    std::vector<int> bad(8, 0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < 8; ++t) {
+      pool.emplace_back([&, t] {
+        for (int i = 0; i < 6; ++i) {
+          auto x = make_data(20000 + 997 * t + 31 * i, 0, true, 50, 1000 + 10 * t + i);
+          auto bytes = shared_enc->encode(x);
+          if (bytes != oracle_encode(c, x)) ++bad[t];
+          std::vector<uint16_t> y(x.size());
+          shared_dec->decode(y, bytes);
+          if (y != x) ++bad[t];
+          std::vector<uint8_t> raw(x.size() * 2);
+          std::memcpy(raw.data(), x.data(), raw.size());
+          auto framed = comp.compress(raw, &meta);
+          if (ricepp_amd::block_decompressor::decompress(framed) != raw) ++bad[t];
+        }
+      });
+    }
+    for (auto& th : pool) th.join();
+    for (int t = 0; t < 8; ++t) CHECK(bad[t] == 0);
   }
   // test/pcm_sample_transformer_test.cpp:33-52 (uint8_8bit) and :258-293 (int24_20bit_be_lsb)
   {
