@@ -10,7 +10,7 @@
 // result (0) is the same.
 //
 // An HBM-bound OR reduction: 2-D grid (chunk, image); each 256-thread block
-// ORs one 64 KiB chunk with 16-byte loads (ragged head/tail samples
+// ORs one 256 KiB chunk with 16-byte loads, four in flight per lane (ragged head/tail samples
 // separately), reduces in registers/LDS and merges with one atomicOr per
 // block; a one-wave second launch turns the per-image OR into the count.
 #include <hip/hip_runtime.h>
@@ -21,7 +21,7 @@
 namespace {
 
 constexpr uint32_t kLsbThreads = 256;
-constexpr uint32_t kLsbChunkSamples = 32768;  // 64 KiB per block
+constexpr uint32_t kLsbChunkSamples = 131072;  // 256 KiB per block
 
 __global__ __launch_bounds__(kLsbThreads) void rpp_lsb_or_kernel(const uint16_t* in, const uint64_t* offsets,
                                                                  const uint64_t* n_samples, uint32_t* acc) {
@@ -41,7 +41,14 @@ __global__ __launch_bounds__(kLsbThreads) void rpp_lsb_or_kernel(const uint16_t*
   const uint64_t groups = (c1 - m0) / 8u;
   uint32_t v = 0;
   const uint4* q = reinterpret_cast<const uint4*>(p + m0);
-  for (uint64_t g = threadIdx.x; g < groups; g += kLsbThreads) {
+  uint64_t g = threadIdx.x;
+  // four independent 16-byte loads in flight per lane
+  for (; g + 3u * kLsbThreads < groups; g += 4u * kLsbThreads) {
+    const uint4 w0 = q[g], w1 = q[g + kLsbThreads], w2 = q[g + 2u * kLsbThreads], w3 = q[g + 3u * kLsbThreads];
+    v |= (w0.x | w0.y | w0.z | w0.w) | (w1.x | w1.y | w1.z | w1.w) | (w2.x | w2.y | w2.z | w2.w) |
+         (w3.x | w3.y | w3.z | w3.w);
+  }
+  for (; g < groups; g += kLsbThreads) {
     const uint4 w = q[g];
     v |= w.x | w.y | w.z | w.w;
   }
