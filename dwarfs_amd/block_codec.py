@@ -2,7 +2,10 @@
 
 Mirrors src/compression/ricepp.cpp: ``ricepp_block_compressor`` (:57-182),
 ``ricepp_block_decompressor`` (:184-255) and the factory registered as
-``"ricepp"`` with option ``block_size=[16..512]`` (default 128, :272-301).  A
+``"ricepp"`` with option ``block_size`` (default 128, :272-301; like the
+reference's factory the value is not range-checked there: an unsupported
+size raises "Unsupported configuration" from the encoder at compress time,
+:97-102).  A
 compressed DwarFS block is
 
     varint(uncompressed bytes) + thrift-compact ricepp_block_header + bitstream
@@ -25,7 +28,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .codec import CodecConfig, _raise_status, decode_batch, encode_batch
+from .codec import CodecConfig, _check, _raise_status, decode_batch, encode_batch
 
 COMPRESSION_TYPE_RICEPP = 7  # include/dwarfs/compression.h
 RICEPP_VERSION = 1  # src/compression/ricepp.cpp:55
@@ -58,8 +61,6 @@ class RiceppBlockCompressor:
     """``ricepp_block_compressor`` (src/compression/ricepp.cpp:57-182)."""
 
     def __init__(self, block_size: int = 128, device="cuda"):
-        if not 16 <= block_size <= 512:
-            raise RuntimeError("ricepp: block_size must be in [16..512]")
         self.block_size = int(block_size)
         self.device = torch.device(device)
 
@@ -94,7 +95,9 @@ class RiceppBlockCompressor:
         if size % (cs * bps):
             raise RuntimeError(f"unexpected data configuration: {size} bytes to compress, {cs} components, "
                                f"{bps} bytes per sample")
-        return CodecConfig(self.block_size, cs, "big" if endianness == "big" else "little", ulsb)
+        cfg = CodecConfig(self.block_size, cs, "big" if endianness == "big" else "little", ulsb)
+        _check(cfg)  # create_encoder's "Unsupported configuration" (:97-102)
+        return cfg
 
     def compress(self, data: bytes, metadata: Optional[str]) -> bytes:
         return self.compress_many([data], metadata)[0]
@@ -136,8 +139,6 @@ class RiceppBlockDecompressor:
             raise RuntimeError(f"[RICEPP] unsupported version: {f.ricepp_version}")
         self.config = CodecConfig(f.block_size, f.component_count, "big" if f.big_endian else "little",
                                   f.unused_lsb_count)
-        from .codec import _check
-
         _check(self.config)
         if f.bytes_per_sample != 2:
             raise RuntimeError(f"[RICEPP] unsupported bytes per sample: {f.bytes_per_sample}")

@@ -1,19 +1,26 @@
 // ricepp_facade.cpp -- C++ host facade (include/ricepp_amd.hpp) over the C ABI.
 //
-// Host spans are staged through device buffers on a per-object HIP stream and
-// handed to rpp_encode_batch / rpp_decode_batch as a batch of one block.  The
-// DwarFS plugin semantics follow src/compression/ricepp.cpp (file:line cited
-// at each method).
+// The DwarFS plugin semantics follow src/compression/ricepp.cpp (file:line
+// cited at each method).  Encode / decode calls go through a per-(device,
+// config) combining queue: concurrent calls are coalesced into one
+// rpp_encode_batch / rpp_decode_batch launch on a pooled device context
+// (stream + grow-only device arena + grow-only pinned staging), so the
+// worker_group threads of the DwarFS writer (src/writer/filesystem_writer.cpp:
+// 255-287) and block cache (src/reader/internal/block_cache.cpp:628-706) feed
+// the GPU in batches without any per-call stream creation or allocation.
 #include "ricepp_amd.hpp"
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cctype>
 #include <charconv>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 
 namespace ricepp_amd {
 
@@ -28,7 +35,7 @@ rpp_config to_rpp(codec_config const& c) {
   r.block_size = c.block_size > 0xFFFFFFFFu ? 0xFFFFFFFFu : static_cast<uint32_t>(c.block_size);
   r.component_stream_count =
       c.component_stream_count > 0xFFFFFFFFu ? 0xFFFFFFFFu : static_cast<uint32_t>(c.component_stream_count);
-  r.big_endian = c.order == byteorder::big ? 1u : 0u;
+  r.big_endian = c.byteorder == std::endian::big ? 1u : 0u;
   r.unused_lsb_count = c.unused_lsb_count;
   return r;
 }
@@ -43,45 +50,416 @@ rpp_config to_rpp(codec_config const& c) {
   }
 }
 
-// Growable device scratch + a private stream.
+size_t align16(size_t v) { return (v + 15) & ~size_t{15}; }
+
+std::atomic<uint64_t> g_enc_launches{0}, g_enc_blocks{0}, g_dec_launches{0}, g_dec_blocks{0}, g_ctx_created{0};
+
+int current_device() {
+  int d = 0;
+  hip_check(hipGetDevice(&d), "hipGetDevice");
+  return d;
+}
+
+// Makes `dev` current for the calling thread for the guard's lifetime.
+class device_guard {
+ public:
+  explicit device_guard(int dev) : dev_{dev} {
+    hip_check(hipGetDevice(&prev_), "hipGetDevice");
+    if (prev_ != dev_) hip_check(hipSetDevice(dev_), "hipSetDevice");
+  }
+  ~device_guard() {
+    if (prev_ != dev_) (void)hipSetDevice(prev_);
+  }
+  device_guard(device_guard const&) = delete;
+  device_guard& operator=(device_guard const&) = delete;
+
+ private:
+  int dev_;
+  int prev_ = 0;
+};
+
+// A private stream plus grow-only device and pinned host buffers, bound to
+// one device.  Contexts are pooled and never freed while the process runs
+// (no hipFree, which would wait for the whole device, on any call path).
 class device_ctx {
  public:
-  device_ctx() { hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"); }
-  ~device_ctx() {
-    if (buf_) (void)hipFree(buf_);
-    if (stream_) (void)hipStreamDestroy(stream_);
+  explicit device_ctx(int dev) : dev_{dev} {
+    device_guard g{dev_};
+    hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    g_ctx_created.fetch_add(1, std::memory_order_relaxed);
   }
   device_ctx(device_ctx const&) = delete;
   device_ctx& operator=(device_ctx const&) = delete;
 
-  // [params 64 B][in (16-aligned)][out (16-aligned)]
-  uint8_t* reserve(size_t bytes) {
-    if (bytes > cap_) {
-      if (buf_) hip_check(hipFree(buf_), "hipFree");
-      buf_ = nullptr;
-      hip_check(hipMalloc(reinterpret_cast<void**>(&buf_), bytes), "hipMalloc");
-      cap_ = bytes;
-    }
-    return buf_;
-  }
+  int device() const { return dev_; }
   hipStream_t stream() const { return stream_; }
+  uint8_t* dev(size_t bytes) { return grow(dbuf_, dcap_, bytes, false); }
+  uint8_t* pin_in(size_t bytes) { return grow(hin_, hin_cap_, bytes, true); }
+  uint8_t* pin_out(size_t bytes) { return grow(hout_, hout_cap_, bytes, true); }
+  void sync() { hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
 
  private:
+  // geometric growth, so that a warm context no longer allocates
+  static uint8_t* grow(uint8_t*& p, size_t& cap, size_t bytes, bool pinned) {
+    if (bytes <= cap && p) return p;
+    size_t n = cap ? cap : size_t{1} << 20;
+    while (n < bytes) n *= 2;
+    if (p) {
+      if (pinned) (void)hipHostFree(p);
+      else (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    void* q = nullptr;
+    if (pinned) hip_check(hipHostMalloc(&q, n, hipHostMallocDefault), "hipHostMalloc");
+    else hip_check(hipMalloc(&q, n), "hipMalloc");
+    p = static_cast<uint8_t*>(q);
+    cap = n;
+    return p;
+  }
+
+  int dev_;
   hipStream_t stream_ = nullptr;
-  uint8_t* buf_ = nullptr;
-  size_t cap_ = 0;
+  uint8_t* dbuf_ = nullptr;
+  size_t dcap_ = 0;
+  uint8_t* hin_ = nullptr;
+  size_t hin_cap_ = 0;
+  uint8_t* hout_ = nullptr;
+  size_t hout_cap_ = 0;
 };
 
-size_t align16(size_t v) { return (v + 15) & ~size_t{15}; }
-
-struct params {  // device-side per-block arrays of a batch of one
-  uint64_t in_off, n, out_off, in_bytes, out_bytes;
-  int32_t status, pad;
-};
-
-class encoder_impl final : public encoder {
+// Per-device free lists of contexts (intentionally leaked at exit: no HIP
+// calls from static destructors).
+class ctx_pool {
  public:
-  explicit encoder_impl(rpp_config c) : cfg_{c} {}
+  static ctx_pool& get() {
+    static ctx_pool* p = new ctx_pool;
+    return *p;
+  }
+  device_ctx* acquire(int dev) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto& v = free_[dev];
+      if (!v.empty()) {
+        device_ctx* c = v.back();
+        v.pop_back();
+        return c;
+      }
+    }
+    return new device_ctx(dev);
+  }
+  void release(device_ctx* c) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_[c->device()].push_back(c);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<int, std::vector<device_ctx*>> free_;
+};
+
+class ctx_lease {
+ public:
+  explicit ctx_lease(int dev) : c_{ctx_pool::get().acquire(dev)} {}
+  ~ctx_lease() { ctx_pool::get().release(c_); }
+  ctx_lease(ctx_lease const&) = delete;
+  ctx_lease& operator=(ctx_lease const&) = delete;
+  device_ctx* operator->() const { return c_; }
+
+ private:
+  device_ctx* c_;
+};
+
+// ---- combining batch queue ----
+//
+// A request moves QUEUED -> TAKEN (in a batch) -> ASSIGNED (its pinned input
+// slot is known: the caller copies its input in) -> STAGED -> RESULT (its
+// pinned output slot is filled: the caller copies its output out) -> DONE.
+// The first waiting caller that finds a free launch slot takes everything
+// queued (up to the batch caps) and drives the launch; every caller does its
+// own host copies, in parallel.  The leader only touches a request through
+// the batch's counters once the request may have returned.
+enum req_state { QUEUED, TAKEN, ASSIGNED, STAGED, RESULT, DONE };
+
+struct batch_counts {
+  size_t to_stage = 0;  // requests not yet STAGED
+  size_t to_finish = 0;  // requests not yet DONE
+};
+
+struct request {
+  // encode: in = samples, out = caller's output; decode: in = stream bytes,
+  // out = sample bytes
+  uint8_t const* in;
+  size_t in_bytes;
+  uint8_t* out;
+  size_t out_cap;  // encode: output span size; decode: exact sample bytes
+  uint64_t n_samples;
+  // set by the leader
+  uint8_t* pin_in = nullptr;
+  uint8_t const* pin_out = nullptr;
+  size_t result_bytes = 0;
+  int status = RPP_OK;
+  std::string error;  // HIP failure text
+  req_state state = QUEUED;
+  batch_counts* counts = nullptr;
+};
+
+constexpr size_t kMaxBatchBlocks = 8192;
+constexpr size_t kMaxBatchBytes = size_t{512} << 20;  // input bytes per launch
+constexpr int kMaxActive = 2;                         // launches in flight per queue
+
+class batch_queue {
+ public:
+  batch_queue(int dev, rpp_config cfg, bool encode) : dev_{dev}, cfg_{cfg}, encode_{encode} {}
+
+  void run(request& r) {
+    std::unique_lock<std::mutex> lk(mu_);
+    pending_.push_back(&r);
+    for (;;) {
+      switch (r.state) {
+        case DONE: return;
+        case ASSIGNED: copy_in(lk, r); continue;
+        case RESULT: copy_out(lk, r); return;
+        case QUEUED:
+          if (active_ < kMaxActive) {
+            lead(lk, r);
+            continue;
+          }
+          break;
+        default: break;
+      }
+      cv_.wait(lk);
+    }
+  }
+
+ private:
+  void copy_in(std::unique_lock<std::mutex>& lk, request& r) {
+    lk.unlock();
+    if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
+    lk.lock();
+    r.state = STAGED;
+    if (--r.counts->to_stage == 0) cv_.notify_all();
+  }
+  void copy_out(std::unique_lock<std::mutex>& lk, request& r) {
+    lk.unlock();
+    if (r.status == RPP_OK && r.result_bytes) std::memcpy(r.out, r.pin_out, r.result_bytes);
+    lk.lock();
+    r.state = DONE;
+    batch_counts* c = r.counts;  // (r may be gone once DONE is seen)
+    if (--c->to_finish == 0) cv_.notify_all();
+  }
+
+  // Takes a batch from the queue and drives it (lk held on entry and exit).
+  // `self` is the leader's own request, which may or may not be in the batch.
+  void lead(std::unique_lock<std::mutex>& lk, request& self) {
+    std::vector<request*> b;
+    size_t bytes = 0;
+    while (!pending_.empty() && b.size() < kMaxBatchBlocks &&
+           (b.empty() || bytes + pending_.front()->in_bytes <= kMaxBatchBytes)) {
+      request* q = pending_.front();
+      pending_.erase(pending_.begin());
+      bytes += q->in_bytes;
+      q->state = TAKEN;
+      b.push_back(q);
+    }
+    batch_counts counts{b.size(), b.size()};
+    for (request* q : b) q->counts = &counts;
+    ++active_;
+    lk.unlock();
+    {
+      ctx_lease ctx{dev_};
+      bool published = false;
+      try {
+        device_guard g{dev_};
+        if (encode_) launch_encode(lk, b, self, *ctx.operator->());
+        else launch_decode(lk, b, self, *ctx.operator->());
+        published = true;
+      } catch (std::exception const& e) {
+        lk.lock();
+        // requests still waiting for their slot: nothing to copy in
+        for (request* q : b)
+          if (q->state == TAKEN) {
+            q->state = STAGED;
+            --counts.to_stage;
+          }
+        // wait for callers copying in, then report the error to everyone
+        cv_.wait(lk, [&] { return counts.to_stage == 0; });
+        for (request* q : b) {
+          q->status = RPP_HIP_ERROR;
+          q->error = e.what();
+          q->result_bytes = 0;
+          q->state = RESULT;
+        }
+        cv_.notify_all();
+        lk.unlock();
+      }
+      (void)published;
+      lk.lock();
+      // the leader copies its own result out, then waits for the others
+      // before the staging buffers go back to the pool
+      if (self.state == RESULT && self.counts == &counts) copy_out(lk, self);
+      cv_.wait(lk, [&] { return counts.to_finish == 0; });
+      lk.unlock();
+    }
+    lk.lock();
+    --active_;
+    cv_.notify_all();
+  }
+
+  // Hands out the pinned input slots and waits until every caller copied in
+  // (lk not held on entry or exit).
+  void stage_in(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self, uint8_t* pin,
+                std::vector<size_t> const& off) {
+    lk.lock();
+    for (size_t i = 0; i < b.size(); ++i) {
+      b[i]->pin_in = pin + off[i];
+      b[i]->state = ASSIGNED;
+    }
+    cv_.notify_all();
+    if (self.state == ASSIGNED && self.counts == b.front()->counts) copy_in(lk, self);
+    batch_counts* c = b.front()->counts;
+    cv_.wait(lk, [&] { return c->to_stage == 0; });
+    lk.unlock();
+  }
+
+  // Publishes the results (lk not held on entry or exit).
+  void publish(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b) {
+    lk.lock();
+    for (request* q : b) q->state = RESULT;
+    cv_.notify_all();
+    lk.unlock();
+  }
+
+  void launch_encode(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self,
+                     device_ctx& ctx) {
+    const size_t nb = b.size();
+    std::vector<size_t> in_off(nb), out_off(nb);
+    size_t in_total = 0, out_total = 0;
+    for (size_t i = 0; i < nb; ++i) {
+      in_off[i] = in_total;
+      in_total += align16(b[i]->in_bytes);
+      out_off[i] = out_total;
+      out_total += align16(rpp_worst_case_bytes(&cfg_, b[i]->n_samples)) + 16;
+    }
+    // device: [in][out slots][packed][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status]
+    const size_t a_off = in_total + 2 * out_total;
+    const size_t arr_bytes = (5 * nb + 1) * 8 + nb * 4;
+    uint8_t* d = ctx.dev(a_off + arr_bytes + 64);
+    uint8_t* pin = ctx.pin_in(in_total + arr_bytes + 64);
+    auto* h64 = reinterpret_cast<uint64_t*>(pin + in_total);
+    for (size_t i = 0; i < nb; ++i) {
+      h64[i] = in_off[i] / 2;
+      h64[nb + i] = b[i]->n_samples;
+      h64[2 * nb + i] = out_off[i];
+    }
+    stage_in(lk, b, self, pin, in_off);
+    auto* d64 = reinterpret_cast<uint64_t*>(d + a_off);
+    auto* dst = reinterpret_cast<int32_t*>(d + a_off + (5 * nb + 1) * 8);
+    hipStream_t s = ctx.stream();
+    if (in_total) hip_check(hipMemcpyAsync(d, pin, in_total, hipMemcpyHostToDevice, s), "H2D encode input");
+    hip_check(hipMemcpyAsync(d64, h64, 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode params");
+    int st = rpp_encode_batch(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
+                              d + in_total, d64 + 2 * nb, d64 + 3 * nb, dst, s);
+    if (st != RPP_OK) throw_status(st);
+    st = rpp_pack_batch(d + in_total, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb),
+                        d + in_total + out_total, d64 + 4 * nb, d64 + 5 * nb, s);
+    if (st != RPP_OK) throw_status(st);
+    g_enc_launches.fetch_add(1, std::memory_order_relaxed);
+    g_enc_blocks.fetch_add(nb, std::memory_order_relaxed);
+    // sizes, packed offsets, total and status back, then the packed bytes
+    hip_check(hipMemcpyAsync(h64 + 3 * nb, d64 + 3 * nb, (2 * nb + 1) * 8 + nb * 4, hipMemcpyDeviceToHost, s),
+              "D2H encode sizes");
+    ctx.sync();
+    const uint64_t total = h64[5 * nb];
+    uint8_t* pout = ctx.pin_out(total + 16);
+    if (total) hip_check(hipMemcpyAsync(pout, d + in_total + out_total, total, hipMemcpyDeviceToHost, s), "D2H encoded");
+    ctx.sync();
+    auto const* hst = reinterpret_cast<int32_t const*>(h64 + 5 * nb + 1);
+    for (size_t i = 0; i < nb; ++i) {
+      b[i]->status = hst[i];
+      b[i]->result_bytes = hst[i] == RPP_OK ? h64[3 * nb + i] : 0;
+      b[i]->pin_out = pout + h64[4 * nb + i];
+      if (b[i]->status == RPP_OK && b[i]->result_bytes > b[i]->out_cap) b[i]->status = RPP_OUTPUT_TOO_SMALL;
+    }
+    publish(lk, b);
+  }
+
+  void launch_decode(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self,
+                     device_ctx& ctx) {
+    const size_t nb = b.size();
+    std::vector<size_t> in_off(nb), out_off(nb);
+    size_t in_total = 0, out_total = 0;
+    for (size_t i = 0; i < nb; ++i) {
+      in_off[i] = in_total;
+      in_total += align16(b[i]->in_bytes);
+      out_off[i] = out_total;
+      out_total += align16(b[i]->out_cap);
+    }
+    // device: [in][out][u64 in_off | in_bytes | out_off | n][i32 status]
+    const size_t a_off = in_total + out_total;
+    uint8_t* d = ctx.dev(a_off + 4 * nb * 8 + nb * 4 + 64);
+    uint8_t* pin = ctx.pin_in(in_total + 4 * nb * 8 + 64);
+    auto* h64 = reinterpret_cast<uint64_t*>(pin + in_total);
+    for (size_t i = 0; i < nb; ++i) {
+      h64[i] = in_off[i];
+      h64[nb + i] = b[i]->in_bytes;
+      h64[2 * nb + i] = out_off[i] / 2;
+      h64[3 * nb + i] = b[i]->n_samples;
+    }
+    stage_in(lk, b, self, pin, in_off);
+    auto* d64 = reinterpret_cast<uint64_t*>(d + a_off);
+    auto* dst = reinterpret_cast<int32_t*>(d + a_off + 4 * nb * 8);
+    hipStream_t s = ctx.stream();
+    if (in_total) hip_check(hipMemcpyAsync(d, pin, in_total, hipMemcpyHostToDevice, s), "H2D decode input");
+    hip_check(hipMemcpyAsync(d64, h64, 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode params");
+    int st = rpp_decode_batch(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb), reinterpret_cast<uint16_t*>(d + in_total),
+                              d64 + 2 * nb, d64 + 3 * nb, dst, s);
+    if (st != RPP_OK) throw_status(st);
+    g_dec_launches.fetch_add(1, std::memory_order_relaxed);
+    g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);
+    uint8_t* pout = ctx.pin_out(out_total + nb * 4 + 64);
+    if (out_total) hip_check(hipMemcpyAsync(pout, d + in_total, out_total, hipMemcpyDeviceToHost, s), "D2H decoded");
+    auto* hst = reinterpret_cast<int32_t*>(pout + out_total);
+    hip_check(hipMemcpyAsync(hst, dst, nb * 4, hipMemcpyDeviceToHost, s), "D2H decode status");
+    ctx.sync();
+    for (size_t i = 0; i < nb; ++i) {
+      b[i]->status = hst[i];
+      b[i]->result_bytes = hst[i] == RPP_OK ? b[i]->out_cap : 0;
+      b[i]->pin_out = pout + out_off[i];
+    }
+    publish(lk, b);
+  }
+
+  int dev_;
+  rpp_config cfg_;
+  bool encode_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<request*> pending_;
+  int active_ = 0;
+};
+
+batch_queue& queue_for(int dev, rpp_config const& c, bool encode) {
+  static std::mutex mu;
+  static auto* queues = new std::map<std::tuple<int, uint32_t, uint32_t, uint32_t, uint32_t, bool>, batch_queue*>;
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_tuple(dev, c.block_size, c.component_stream_count, c.big_endian, c.unused_lsb_count, encode);
+  auto it = queues->find(key);
+  if (it == queues->end()) it = queues->emplace(key, new batch_queue(dev, c, encode)).first;
+  return *it->second;
+}
+
+// Runs one request through its queue (the calling thread may become the
+// leader of a batch that contains it).
+void submit(batch_queue& q, request& r) {
+  q.run(r);
+  if (r.status == RPP_HIP_ERROR) throw std::runtime_error(r.error.empty() ? "ricepp_amd: HIP error" : r.error);
+  if (r.status != RPP_OK) throw_status(r.status);
+}
+
+class encoder_impl final : public encoder_interface<uint16_t> {
+ public:
+  encoder_impl(rpp_config c, int dev) : cfg_{c}, q_{queue_for(dev, c, true)} {}
 
   size_t worst_case_encoded_bytes(size_t n) const override { return rpp_worst_case_bytes(&cfg_, n); }
   size_t worst_case_encoded_bytes(std::span<uint16_t const> in) const override {
@@ -97,64 +475,35 @@ class encoder_impl final : public encoder {
 
   // ricepp_cpuspecific.cpp:101-108: output must hold the worst case
   std::span<uint8_t> encode(std::span<uint8_t> output, std::span<uint16_t const> input) const override {
-    size_t const wc = worst_case_encoded_bytes(input.size());
-    if (output.size() < wc) throw std::length_error("ricepp_amd: output smaller than worst_case_encoded_bytes");
-    size_t const in_bytes = input.size() * 2;
-    size_t const off_in = 64, off_out = off_in + align16(in_bytes);
-    std::lock_guard<std::mutex> lock(mu_);  // const and re-entrant like the reference's object
-    uint8_t* d = ctx_.reserve(off_out + align16(wc) + 16);
-    params hp{0, input.size(), 0, 0, 0, 0, 0};
-    auto* dp = reinterpret_cast<params*>(d);
-    hipStream_t s = ctx_.stream();
-    hip_check(hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, s), "H2D params");
-    if (in_bytes) hip_check(hipMemcpyAsync(d + off_in, input.data(), in_bytes, hipMemcpyHostToDevice, s), "H2D input");
-    int st = rpp_encode_batch(&cfg_, reinterpret_cast<uint16_t const*>(d + off_in), &dp->in_off, &dp->n, 1,
-                              d + off_out, &dp->out_off, &dp->out_bytes, &dp->status, s);
-    if (st != RPP_OK) throw_status(st);
-    hip_check(hipMemcpyAsync(&hp, dp, sizeof hp, hipMemcpyDeviceToHost, s), "D2H params");
-    hip_check(hipStreamSynchronize(s), "sync");
-    if (hp.status != RPP_OK) throw_status(hp.status);
-    hip_check(hipMemcpyAsync(output.data(), d + off_out, hp.out_bytes, hipMemcpyDeviceToHost, s), "D2H output");
-    hip_check(hipStreamSynchronize(s), "sync");
-    return output.subspan(0, hp.out_bytes);
+    if (output.size() < worst_case_encoded_bytes(input.size()))
+      throw std::length_error("ricepp_amd: output smaller than worst_case_encoded_bytes");
+    if (input.size() % cfg_.component_stream_count) throw_status(RPP_INVALID_ARGUMENT);
+    request r{reinterpret_cast<uint8_t const*>(input.data()), input.size_bytes(), output.data(), output.size(),
+              input.size()};
+    submit(q_, r);
+    return output.subspan(0, r.result_bytes);
   }
 
  private:
   rpp_config cfg_;
-  mutable std::mutex mu_;
-  mutable device_ctx ctx_;
+  batch_queue& q_;
 };
 
-class decoder_impl final : public decoder {
+class decoder_impl final : public decoder_interface<uint16_t> {
  public:
-  explicit decoder_impl(rpp_config c) : cfg_{c} {}
+  decoder_impl(rpp_config c, int dev) : cfg_{c}, q_{queue_for(dev, c, false)} {}
 
   // ricepp_cpuspecific.cpp:127-144: decodes exactly output.size() samples
   void decode(std::span<uint16_t> output, std::span<uint8_t const> input) const override {
-    size_t const off_in = 64, off_out = off_in + align16(input.size()) + 16;
-    std::lock_guard<std::mutex> lock(mu_);  // const and re-entrant like the reference's object
-    uint8_t* d = ctx_.reserve(off_out + align16(output.size() * 2) + 16);
-    params hp{0, output.size(), 0, input.size(), 0, 0, 0};
-    auto* dp = reinterpret_cast<params*>(d);
-    hipStream_t s = ctx_.stream();
-    hip_check(hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, s), "H2D params");
-    if (!input.empty())
-      hip_check(hipMemcpyAsync(d + off_in, input.data(), input.size(), hipMemcpyHostToDevice, s), "H2D input");
-    int st = rpp_decode_batch(&cfg_, d + off_in, &dp->in_off, &dp->in_bytes, 1,
-                              reinterpret_cast<uint16_t*>(d + off_out), &dp->out_off, &dp->n, &dp->status, s);
-    if (st != RPP_OK) throw_status(st);
-    hip_check(hipMemcpyAsync(&hp, dp, sizeof hp, hipMemcpyDeviceToHost, s), "D2H params");
-    hip_check(hipStreamSynchronize(s), "sync");
-    if (hp.status != RPP_OK) throw_status(hp.status);
-    if (!output.empty())
-      hip_check(hipMemcpyAsync(output.data(), d + off_out, output.size() * 2, hipMemcpyDeviceToHost, s), "D2H out");
-    hip_check(hipStreamSynchronize(s), "sync");
+    if (output.size() % cfg_.component_stream_count) throw_status(RPP_INVALID_ARGUMENT);
+    request r{input.data(), input.size(), reinterpret_cast<uint8_t*>(output.data()), output.size_bytes(),
+              output.size()};
+    submit(q_, r);
   }
 
  private:
   rpp_config cfg_;
-  mutable std::mutex mu_;
-  mutable device_ctx ctx_;
+  batch_queue& q_;
 };
 
 // ---- minimal JSON for the flat metadata objects of the plugin ----
@@ -180,7 +529,8 @@ std::map<std::string, std::string> parse_flat_json(std::string const& s) {
   ++i;
   for (;;) {
     skip();
-    if (i < s.size() && s[i] == '}') break;
+    if (i >= s.size()) throw std::runtime_error("ricepp_amd: malformed metadata JSON");
+    if (s[i] == '}') break;
     std::string k = str();
     skip();
     if (i >= s.size() || s[i] != ':') throw std::runtime_error("ricepp_amd: malformed metadata JSON");
@@ -220,27 +570,32 @@ constexpr uint32_t kRiceppVersion = 1;  // src/compression/ricepp.cpp:55
 
 }  // namespace
 
-std::unique_ptr<encoder> create_encoder(codec_config const& config) {
+template <>
+std::unique_ptr<encoder_interface<uint16_t>> create_encoder<uint16_t>(codec_config const& config) {
   rpp_config c = to_rpp(config);
   if (rpp_check_config(&c) != RPP_OK) throw std::runtime_error("Unsupported configuration");
-  return std::make_unique<encoder_impl>(c);
+  return std::make_unique<encoder_impl>(c, current_device());
 }
 
-std::unique_ptr<decoder> create_decoder(codec_config const& config) {
+template <>
+std::unique_ptr<decoder_interface<uint16_t>> create_decoder<uint16_t>(codec_config const& config) {
   rpp_config c = to_rpp(config);
   if (rpp_check_config(&c) != RPP_OK) throw std::runtime_error("Unsupported configuration");
-  return std::make_unique<decoder_impl>(c);
+  return std::make_unique<decoder_impl>(c, current_device());
+}
+
+facade_stats get_facade_stats() {
+  return facade_stats{g_enc_launches.load(), g_enc_blocks.load(), g_dec_launches.load(), g_dec_blocks.load(),
+                      g_ctx_created.load()};
 }
 
 // ---- block_compressor (src/compression/ricepp.cpp:57-182, 272-296) ----
 
-block_compressor::block_compressor(size_t block_size) : block_size_{block_size} {
-  if (block_size < 16 || block_size > 512)
-    throw std::runtime_error("ricepp: block_size must be in [16..512]");  // options_, :284-286
-}
+block_compressor::block_compressor(size_t block_size) : block_size_{block_size} {}
 
 std::unique_ptr<block_compressor> block_compressor::create(std::string const& spec) {
-  // "ricepp" or "ricepp:block_size=N" (option_map, default 128, :280)
+  // "ricepp" or "ricepp:block_size=N" (option_map, default 128, :280); like
+  // the reference's factory, the value is not range-checked here
   size_t bs = 128;
   std::string name = spec.substr(0, spec.find(':'));
   if (name != "ricepp") throw std::runtime_error("unknown compression: " + name);
@@ -292,19 +647,23 @@ std::vector<uint8_t> block_compressor::compress(std::span<uint8_t const> data, s
     throw std::runtime_error("unexpected data configuration: " + std::to_string(data.size()) +
                              " bytes to compress, " + std::to_string(component_count) + " components, " +
                              std::to_string(bytes_per_sample) + " bytes per sample");
-  codec_config cfg{block_size_, static_cast<size_t>(component_count),
-                   endianness == "big" ? byteorder::big : byteorder::little,
-                   static_cast<unsigned>(unused_lsb_count)};
-  auto enc = create_encoder(cfg);
+  auto const byteorder = endianness == "big" ? std::endian::big : std::endian::little;
+  // :97-102 -- throws "Unsupported configuration" for an unsupported block size
+  auto enc = create_encoder<uint16_t>({
+      .block_size = block_size_,
+      .component_stream_count = static_cast<size_t>(component_count),
+      .byteorder = byteorder,
+      .unused_lsb_count = static_cast<unsigned>(unused_lsb_count),
+  });
   rpp_frame f{data.size(), static_cast<uint32_t>(block_size_), static_cast<uint32_t>(component_count),
               static_cast<uint32_t>(bytes_per_sample), static_cast<uint32_t>(unused_lsb_count),
-              endianness == "big" ? 1u : 0u, kRiceppVersion};
+              byteorder == std::endian::big ? 1u : 0u, kRiceppVersion};
   std::vector<uint8_t> out(64);
   size_t hdr = rpp_frame_header(&f, out.data());
   size_t n = data.size() / 2;
-  std::vector<uint16_t> samples(n);
-  if (n) std::memcpy(samples.data(), data.data(), n * 2);
   out.resize(hdr + enc->worst_case_encoded_bytes(n));
+  // (the samples are read in place: the staging copy handles any alignment)
+  std::span<uint16_t const> samples{reinterpret_cast<uint16_t const*>(data.data()), n};
   auto used = enc->encode(std::span<uint8_t>{out}.subspan(hdr), samples);
   out.resize(hdr + used.size());
   out.shrink_to_fit();
@@ -319,8 +678,12 @@ block_decompressor::block_decompressor(std::span<uint8_t const> data) {
   data_ = data.subspan(static_cast<size_t>(h));
   if (frame_.ricepp_version > kRiceppVersion)  // :243-247
     throw std::runtime_error("[RICEPP] unsupported version: " + std::to_string(frame_.ricepp_version));
-  decoder_ = create_decoder({frame_.block_size, frame_.component_count,
-                             frame_.big_endian ? byteorder::big : byteorder::little, frame_.unused_lsb_count});
+  decoder_ = create_decoder<uint16_t>({
+      .block_size = frame_.block_size,
+      .component_stream_count = frame_.component_count,
+      .byteorder = frame_.big_endian ? std::endian::big : std::endian::little,
+      .unused_lsb_count = frame_.unused_lsb_count,
+  });
   if (frame_.bytes_per_sample != 2)  // :196-200
     throw std::runtime_error("[RICEPP] unsupported bytes per sample: " + std::to_string(frame_.bytes_per_sample));
 }
@@ -358,11 +721,6 @@ std::vector<uint8_t> block_decompressor::decompress(std::span<uint8_t const> dat
 
 // ---- pcm_sample_transformer (src/pcm_sample_transformer.cpp:372-377) ----
 
-struct pcm_sample_transformer::impl {
-  std::mutex mu;
-  device_ctx ctx;
-};
-
 pcm_sample_transformer::pcm_sample_transformer(pcm_sample_endianness end, pcm_sample_signedness sig,
                                                pcm_sample_padding pad, int bytes, int bits) {
   fmt_.big_endian = end == pcm_sample_endianness::Big ? 1u : 0u;
@@ -374,7 +732,7 @@ pcm_sample_transformer::pcm_sample_transformer(pcm_sample_endianness end, pcm_sa
   if (st == RPP_UNSUPPORTED_CONFIG || bytes < 1 || bytes > 4)
     throw std::runtime_error("unsupported number of bytes per sample: " + std::to_string(bytes));
   if (st != RPP_OK) throw std::invalid_argument("pcm_sample_transformer: bits outside 1..8*bytes");
-  impl_ = std::make_unique<impl>();
+  device_ = current_device();
 }
 
 pcm_sample_transformer::~pcm_sample_transformer() = default;
@@ -385,28 +743,30 @@ void pcm_sample_transformer::unpack(std::span<int32_t> dst, std::span<uint8_t co
   if (src.size() != fmt_.bytes * dst.size()) throw std::invalid_argument("pcm unpack: src.size() != bytes * dst.size()");
   if (dst.empty()) return;
   const size_t off_out = align16(src.size());
-  std::lock_guard<std::mutex> lock(impl_->mu);
-  uint8_t* d = impl_->ctx.reserve(off_out + dst.size_bytes());
-  hipStream_t s = impl_->ctx.stream();
+  device_guard g{device_};
+  ctx_lease ctx{device_};
+  uint8_t* d = ctx->dev(off_out + dst.size_bytes());
+  hipStream_t s = ctx->stream();
   hip_check(hipMemcpyAsync(d, src.data(), src.size(), hipMemcpyHostToDevice, s), "H2D pcm");
   const int st = rpp_pcm_unpack(&fmt_, d, reinterpret_cast<int32_t*>(d + off_out), dst.size(), s);
   if (st != RPP_OK) throw_status(st);
   hip_check(hipMemcpyAsync(dst.data(), d + off_out, dst.size_bytes(), hipMemcpyDeviceToHost, s), "D2H pcm");
-  hip_check(hipStreamSynchronize(s), "sync");
+  ctx->sync();
 }
 
 void pcm_sample_transformer::pack(std::span<uint8_t> dst, std::span<int32_t const> src) const {
   if (dst.size() != fmt_.bytes * src.size()) throw std::invalid_argument("pcm pack: dst.size() != bytes * src.size()");
   if (src.empty()) return;
   const size_t off_out = align16(src.size_bytes());
-  std::lock_guard<std::mutex> lock(impl_->mu);
-  uint8_t* d = impl_->ctx.reserve(off_out + dst.size());
-  hipStream_t s = impl_->ctx.stream();
+  device_guard g{device_};
+  ctx_lease ctx{device_};
+  uint8_t* d = ctx->dev(off_out + dst.size());
+  hipStream_t s = ctx->stream();
   hip_check(hipMemcpyAsync(d, src.data(), src.size_bytes(), hipMemcpyHostToDevice, s), "H2D pcm");
   const int st = rpp_pcm_pack(&fmt_, reinterpret_cast<int32_t const*>(d), d + off_out, src.size(), s);
   if (st != RPP_OK) throw_status(st);
   hip_check(hipMemcpyAsync(dst.data(), d + off_out, dst.size(), hipMemcpyDeviceToHost, s), "D2H pcm");
-  hip_check(hipStreamSynchronize(s), "sync");
+  ctx->sync();
 }
 
 }  // namespace ricepp_amd

@@ -1,32 +1,45 @@
 // ricepp_amd.hpp -- C++ host facade over the C ABI of ricepp_amd.h.
 //
-// Mirrors the two interfaces the reference exposes for this path:
+// Source-compatible with the two interfaces the reference exposes for this
+// path, so that DwarFS's plugin (src/compression/ricepp.cpp) compiles against
+// it with only its #include lines and the namespace changed
+// (`namespace ricepp = ricepp_amd;`):
 //
-//  * the ricepp library API used by DwarFS's plugin
-//      ricepp::create_encoder<uint16_t> / create_decoder<uint16_t>
-//        (ricepp/include/ricepp/create_encoder.h:39-41, create_decoder.h:39-41)
-//      encoder_interface<uint16_t>::encode / worst_case_encoded_bytes
-//        (ricepp/include/ricepp/encoder_interface.h:38-60)
-//      decoder_interface<uint16_t>::decode (decoder_interface.h:37-50)
-//    Errors: std::runtime_error("Unsupported configuration") for a bad
-//    config, std::out_of_range when decoding runs past the input.
+//  * the ricepp library API
+//      codec_config {block_size, component_stream_count, std::endian byteorder,
+//                    unused_lsb_count}      (ricepp/include/ricepp/codec_config.h:36-41)
+//      template <std::unsigned_integral PixelT>
+//      std::unique_ptr<encoder_interface<PixelT>> create_encoder(codec_config const&)
+//                                            (ricepp/include/ricepp/create_encoder.h:39-41)
+//      ... create_decoder                     (ricepp/include/ricepp/create_decoder.h:39-41)
+//      encoder_interface<PixelT>::encode / worst_case_encoded_bytes
+//                                            (ricepp/include/ricepp/encoder_interface.h:38-60)
+//      decoder_interface<PixelT>::decode      (ricepp/include/ricepp/decoder_interface.h:37-50)
+//    Only PixelT = uint16_t is instantiated, as in the reference
+//    (ricepp/ricepp.cpp:36-48).  Errors: std::runtime_error("Unsupported
+//    configuration") for a bad config (ricepp/ricepp_cpuspecific.cpp:161,173),
+//    std::out_of_range when decoding runs past the input.
 //
 //  * the DwarFS block codec behind block_compressor / block_decompressor
-//      ricepp_block_compressor / ricepp_block_decompressor
-//        (src/compression/ricepp.cpp:57-182, 184-255)
+//      block_compressor / block_decompressor (src/compression/ricepp.cpp:57-255)
 //    with the same framing, metadata JSON, constraints and error messages.
 //
-// Host spans in, host spans out: the facade stages through device buffers on
-// its own HIP stream (one per object).  Every method is const and may be
-// called from several threads at once, as the reference's immutable objects
-// can: an encoder / decoder / pcm_sample_transformer serialises its calls on a
-// per-object lock; block_compressor::compress creates its encoder per call
-// (src/compression/ricepp.cpp:97-102), so DwarFS's worker_group threads
-// compressing through one impl (src/writer/filesystem_writer.cpp:259-268) run
-// concurrently, one stream each.  The device-resident batch API (rpp_encode_batch /
-// rpp_decode_batch) is the fast path; this facade is the drop-in.
+// Threading and batching.  Every method is const and may be called from many
+// threads at once, as the reference's immutable objects can; DwarFS's
+// worker_group threads call compress on one shared block_compressor::impl
+// (src/writer/filesystem_writer.cpp:255-287) and decompress blocks
+// concurrently (src/reader/internal/block_cache.cpp:628-706).  Concurrent
+// encode / decode calls with the same configuration on the same device are
+// coalesced into one rpp_encode_batch / rpp_decode_batch launch (a combining
+// queue: the first waiting caller launches everything queued, the other
+// callers copy their own data in and out of pinned staging in parallel).
+// Device contexts (stream, device and pinned staging) come from a per-device
+// pool and are reused, so no call creates a stream or allocates once the pool
+// is warm.  An object runs on the device that was current when it was created.
 #pragma once
 
+#include <bit>
+#include <concepts>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
@@ -40,35 +53,54 @@
 
 namespace ricepp_amd {
 
-enum class byteorder { little, big };
-
 // ricepp::codec_config (ricepp/include/ricepp/codec_config.h:36-41)
 struct codec_config {
   size_t block_size;
   size_t component_stream_count;
-  byteorder order;
+  std::endian byteorder;
   unsigned unused_lsb_count;
 };
 
-class encoder {
+// ricepp::encoder_interface (ricepp/include/ricepp/encoder_interface.h:38-60)
+template <typename PixelT>
+class encoder_interface {
+  static_assert(std::unsigned_integral<PixelT>, "PixelT must be an unsigned integral type");
+
  public:
-  virtual ~encoder() = default;
-  virtual std::vector<uint8_t> encode(std::span<uint16_t const> input) const = 0;
+  using pixel_type = PixelT;
+
+  virtual ~encoder_interface() = default;
+
+  [[nodiscard]] virtual std::vector<uint8_t> encode(std::span<pixel_type const> input) const = 0;
   virtual size_t worst_case_encoded_bytes(size_t pixel_count) const = 0;
-  virtual size_t worst_case_encoded_bytes(std::span<uint16_t const> input) const = 0;
-  virtual std::span<uint8_t> encode(std::span<uint8_t> output, std::span<uint16_t const> input) const = 0;
+  virtual size_t worst_case_encoded_bytes(std::span<pixel_type const> input) const = 0;
+  virtual std::span<uint8_t> encode(std::span<uint8_t> output, std::span<pixel_type const> input) const = 0;
 };
 
-class decoder {
+// ricepp::decoder_interface (ricepp/include/ricepp/decoder_interface.h:37-50)
+template <typename PixelT>
+class decoder_interface {
+  static_assert(std::unsigned_integral<PixelT>, "PixelT must be an unsigned integral type");
+
  public:
-  virtual ~decoder() = default;
-  virtual void decode(std::span<uint16_t> output, std::span<uint8_t const> input) const = 0;
+  using pixel_type = PixelT;
+
+  virtual ~decoder_interface() = default;
+
+  virtual void decode(std::span<pixel_type> output, std::span<uint8_t const> input) const = 0;
 };
 
-// throw std::runtime_error("Unsupported configuration") like
-// ricepp/ricepp_cpuspecific.cpp:161,173
-std::unique_ptr<encoder> create_encoder(codec_config const& config);
-std::unique_ptr<decoder> create_decoder(codec_config const& config);
+// ricepp::create_encoder / create_decoder: declared for every unsigned PixelT
+// like the reference, defined (in ricepp_facade.cpp) for uint16_t.
+template <std::unsigned_integral PixelT>
+std::unique_ptr<encoder_interface<PixelT>> create_encoder(codec_config const& config);
+template <std::unsigned_integral PixelT>
+std::unique_ptr<decoder_interface<PixelT>> create_decoder(codec_config const& config);
+
+template <>
+std::unique_ptr<encoder_interface<uint16_t>> create_encoder<uint16_t>(codec_config const& config);
+template <>
+std::unique_ptr<decoder_interface<uint16_t>> create_decoder<uint16_t>(codec_config const& config);
 
 // ---- DwarFS block codec (src/compression/ricepp.cpp) ----
 
@@ -77,7 +109,10 @@ inline constexpr int compression_type_ricepp = 7;
 
 class block_compressor {
  public:
-  explicit block_compressor(size_t block_size = 128);  // "ricepp:block_size=N", N in [16, 512]
+  // "ricepp:block_size=N": the factory reads the option without a range check
+  // (src/compression/ricepp.cpp:277-281); an unsupported size throws
+  // "Unsupported configuration" from create_encoder at compress time (:97-102).
+  explicit block_compressor(size_t block_size = 128);
   static std::unique_ptr<block_compressor> create(std::string const& spec);
 
   std::unique_ptr<block_compressor> clone() const;
@@ -107,7 +142,7 @@ class block_decompressor {
  private:
   rpp_frame frame_{};
   std::span<uint8_t const> data_;
-  std::unique_ptr<decoder> decoder_;
+  std::unique_ptr<decoder_interface<uint16_t>> decoder_;
   std::vector<uint8_t>* target_ = nullptr;
 };
 
@@ -115,7 +150,7 @@ class block_decompressor {
 //
 // pcm_sample_transformer<int32_t>: (end, sig, pad, bytes, bits) -> unpack / pack
 // of interleaved PCM bytes, on the GPU (rpp_pcm_unpack / rpp_pcm_pack) through
-// a private stream and device staging buffer.  Throws std::runtime_error
+// a pooled device context.  Throws std::runtime_error
 // ("unsupported number of bytes per sample: N") like
 // src/pcm_sample_transformer.cpp:310-311, std::invalid_argument for bits
 // outside 1..8*bytes (an assert in the reference, :354) and for spans whose
@@ -137,9 +172,15 @@ class pcm_sample_transformer {
   void pack(std::span<uint8_t> dst, std::span<int32_t const> src) const;
 
  private:
-  struct impl;
   rpp_pcm_format fmt_{};
-  std::unique_ptr<impl> impl_;
+  int device_ = 0;
 };
+
+// ---- facade statistics (tests and benchmarks) ----
+struct facade_stats {
+  uint64_t encode_launches, encode_blocks, decode_launches, decode_blocks;
+  uint64_t contexts_created;
+};
+facade_stats get_facade_stats();
 
 }  // namespace ricepp_amd

@@ -2,6 +2,8 @@
 // path: ricepp/test/codec_test.cpp (round trips, worst-case KATs, error
 // contract) and test/ricepp_compressor_test.cpp (block_compressor spec
 // round trip), checking every stream against the CPU oracle byte for byte.
+#include <bit>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -59,9 +61,16 @@ static std::vector<uint16_t> make_data(size_t n, unsigned ulsb, bool be, unsigne
   return v;
 }
 
+static ricepp_amd::codec_config cfg(size_t bs, size_t cs, bool big, unsigned ulsb) {
+  return {.block_size = bs,
+          .component_stream_count = cs,
+          .byteorder = big ? std::endian::big : std::endian::little,
+          .unused_lsb_count = ulsb};
+}
+
 static std::vector<uint8_t> oracle_encode(ricepp_amd::codec_config const& c, std::vector<uint16_t> const& x) {
   rpo_config oc{(uint32_t)c.block_size, (uint32_t)c.component_stream_count,
-                c.order == ricepp_amd::byteorder::big ? 1u : 0u, c.unused_lsb_count};
+                c.byteorder == std::endian::big ? 1u : 0u, c.unused_lsb_count};
   std::vector<uint8_t> out(rpo_worst_case_bytes(&oc, x.size()) + 1);
   size_t n = 0;
   if (rpo_encode(&oc, x.data(), x.size(), out.data(), out.size(), &n) != 0) std::abort();
@@ -70,51 +79,54 @@ static std::vector<uint8_t> oracle_encode(ricepp_amd::codec_config const& c, std
 }
 
 static void roundtrip(ricepp_amd::codec_config const& c, size_t n, unsigned full_chance, uint64_t seed) {
-  auto x = make_data(n, c.unused_lsb_count, c.order == ricepp_amd::byteorder::big, full_chance, seed);
-  auto enc = ricepp_amd::create_encoder(c);
+  auto x = make_data(n, c.unused_lsb_count, c.byteorder == std::endian::big, full_chance, seed);
+  auto enc = ricepp_amd::create_encoder<uint16_t>(c);
   auto bytes = enc->encode(x);
   CHECK(bytes == oracle_encode(c, x));
-  auto dec = ricepp_amd::create_decoder(c);
+  auto dec = ricepp_amd::create_decoder<uint16_t>(c);
   std::vector<uint16_t> y(x.size());
   dec->decode(y, bytes);
   CHECK(y == x);
 }
 
-int main() {
-  using ricepp_amd::byteorder;
+int bench(int argc, char** argv);
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "--bench") return bench(argc, argv);
   // codec_test.cpp:65-152
-  roundtrip({16, 1, byteorder::big, 0}, 12345, 50, 1);
-  roundtrip({13, 1, byteorder::big, 4}, 4321, 50, 2);
-  roundtrip({32, 1, byteorder::big, 0}, 1500, 0, 3);
-  roundtrip({29, 2, byteorder::big, 2}, 23456, 50, 4);
-  roundtrip({128, 1, byteorder::little, 0}, 65536, 50, 5);
-  roundtrip({512, 2, byteorder::little, 3}, 10000, 50, 6);
+  roundtrip(cfg(16, 1, true, 0), 12345, 50, 1);
+  roundtrip(cfg(13, 1, true, 4), 4321, 50, 2);
+  roundtrip(cfg(32, 1, true, 0), 1500, 0, 3);
+  roundtrip(cfg(29, 2, true, 2), 23456, 50, 4);
+  roundtrip(cfg(128, 1, false, 0), 65536, 50, 5);
+  roundtrip(cfg(512, 2, false, 3), 10000, 50, 6);
+  roundtrip(cfg(8, 1, true, 0), 3001, 50, 11);  // the factory accepts any size <= 512
 
   // codec_test.cpp:154-196: worst-case KATs; incompressible == worst case
   {
-    ricepp_amd::codec_config c{29, 1, byteorder::big, 0};
-    auto enc = ricepp_amd::create_encoder(c);
+    auto c = cfg(29, 1, true, 0);
+    auto enc = ricepp_amd::create_encoder<uint16_t>(c);
     auto x = make_data(14443, 0, true, 0, 7);
     CHECK(enc->worst_case_encoded_bytes(x) == 29138);
     std::vector<uint8_t> buf(29138);
     auto used = enc->encode(buf, x);
     CHECK(used.size() == 29138);
-    auto enc2 = ricepp_amd::create_encoder({29, 2, byteorder::big, 0});
+    auto enc2 = ricepp_amd::create_encoder<uint16_t>(cfg(29, 2, true, 0));
     CHECK(enc2->worst_case_encoded_bytes(28886) == 58275);
   }
   // codec_test.cpp:198-222
-  CHECK(throws<std::runtime_error>([] { ricepp_amd::create_encoder({513, 2, byteorder::big, 0}); },
+  CHECK(throws<std::runtime_error>([] { ricepp_amd::create_encoder<uint16_t>(cfg(513, 2, true, 0)); },
                                    "Unsupported configuration"));
-  CHECK(throws<std::runtime_error>([] { ricepp_amd::create_decoder({128, 3, byteorder::big, 0}); },
+  CHECK(throws<std::runtime_error>([] { ricepp_amd::create_decoder<uint16_t>(cfg(128, 3, true, 0)); },
                                    "Unsupported configuration"));
   // bitstream_reader.h:150-152: running out of input is std::out_of_range
   {
-    ricepp_amd::codec_config c{128, 1, byteorder::big, 0};
+    auto c = cfg(128, 1, true, 0);
     auto x = make_data(4096, 0, true, 50, 8);
-    auto bytes = ricepp_amd::create_encoder(c)->encode(x);
+    auto bytes = ricepp_amd::create_encoder<uint16_t>(c)->encode(x);
     bytes.resize((bytes.size() - 1) / 8 * 8);
     std::vector<uint16_t> y(x.size());
-    auto dec = ricepp_amd::create_decoder(c);
+    auto dec = ricepp_amd::create_decoder<uint16_t>(c);
     CHECK(throws<std::out_of_range>([&] { dec->decode(y, bytes); }));
   }
 
@@ -122,7 +134,7 @@ int main() {
   struct P {
     int cs, pixels, ulsb, block;
   };
-  for (P p : {P{1, 1000, 0, 16}, P{2, 1000, 2, 32}, P{1, 1000, 4, 64}, P{2, 3333, 6, 99}}) {
+  for (P p : {P{1, 1000, 0, 16}, P{2, 1000, 2, 32}, P{1, 1000, 4, 64}, P{2, 3333, 6, 99}, P{1, 777, 0, 8}}) {
     auto x = make_data((size_t)p.cs * p.pixels, (unsigned)p.ulsb, true, 50, 9);
     std::vector<uint8_t> data(x.size() * 2);
     std::memcpy(data.data(), x.data(), data.size());
@@ -136,7 +148,7 @@ int main() {
     std::vector<uint8_t> want(64);
     size_t h = rpo_frame_header(want.data(), data.size(), (uint32_t)p.block, (uint32_t)p.cs, 2, (uint32_t)p.ulsb, 1, 1);
     want.resize(h);
-    auto body = oracle_encode({(size_t)p.block, (size_t)p.cs, byteorder::big, (unsigned)p.ulsb}, x);
+    auto body = oracle_encode(cfg((size_t)p.block, (size_t)p.cs, true, (unsigned)p.ulsb), x);
     want.insert(want.end(), body.begin(), body.end());
     CHECK(compressed == want);
     // (ratio < 0.7 needs the compressor test generator; covered by tests/test_gpu_block_codec.py)
@@ -163,7 +175,12 @@ int main() {
     b3.resize(rpo_frame_header(b3.data(), 16, 128, 1, 3, 0, 1, 1));
     CHECK(throws<std::runtime_error>([&] { ricepp_amd::block_decompressor d{b3}; },
                                      "[RICEPP] unsupported bytes per sample: 3"));
-    CHECK(throws<std::runtime_error>([] { ricepp_amd::block_compressor::create("ricepp:block_size=8"); }));
+    // the factory does not range-check block_size (src/compression/ricepp.cpp:277-281); an
+    // unsupported size fails in create_encoder at compress time (:97-102)
+    auto big = ricepp_amd::block_compressor::create("ricepp:block_size=513");
+    CHECK(big->describe() == "ricepp [block_size=513]");
+    std::vector<uint8_t> two(4);
+    CHECK(throws<std::runtime_error>([&] { big->compress(two, &meta); }, "Unsupported configuration"));
     CHECK(comp.metadata_requirements() ==
           R"({"bytes_per_sample":["set",[2]],"component_count":["range",1,2],"endianness":["set",["big","little"]],"unused_lsb_count":["range",0,8]})");
   }
@@ -173,10 +190,9 @@ int main() {
   // share one compressor, one encoder and one decoder; every stream is checked
   // against the oracle.
   {
-    using ricepp_amd::byteorder;
-    ricepp_amd::codec_config c{128, 1, byteorder::big, 0};
-    auto shared_enc = ricepp_amd::create_encoder(c);
-    auto shared_dec = ricepp_amd::create_decoder(c);
+    auto c = cfg(128, 1, true, 0);
+    auto shared_enc = ricepp_amd::create_encoder<uint16_t>(c);
+    auto shared_dec = ricepp_amd::create_decoder<uint16_t>(c);
     ricepp_amd::block_compressor comp{128};
     std::string const meta =
         R"({"bytes_per_sample":2,"component_count":1,"endianness":"big","unused_lsb_count":0})";
@@ -229,6 +245,98 @@ int main() {
                                       pcm_sample_padding::Lsb, 5, 16); },
         "unsupported number of bytes per sample: 5"));
   }
+  // batching: 64 threads encoding and decoding at once through one
+  // configuration are coalesced into fewer launches than calls, and every
+  // result is still the oracle's
+  {
+    auto c = cfg(64, 2, false, 1);
+    auto const before = ricepp_amd::get_facade_stats();
+    std::vector<int> bad(64, 0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < 64; ++t) {
+      pool.emplace_back([&, t] {
+        auto enc = ricepp_amd::create_encoder<uint16_t>(c);
+        auto dec = ricepp_amd::create_decoder<uint16_t>(c);
+        for (int i = 0; i < 8; ++i) {
+          auto x = make_data(2 * (3000 + 101 * t + 7 * i), 1, false, 50, 5000 + 100 * t + i);
+          auto bytes = enc->encode(x);
+          if (bytes != oracle_encode(c, x)) ++bad[t];
+          std::vector<uint16_t> y(x.size());
+          dec->decode(y, bytes);
+          if (y != x) ++bad[t];
+        }
+      });
+    }
+    for (auto& th : pool) th.join();
+    for (int t = 0; t < 64; ++t) CHECK(bad[t] == 0);
+    auto const after = ricepp_amd::get_facade_stats();
+    CHECK(after.encode_blocks - before.encode_blocks == 64 * 8);
+    CHECK(after.decode_blocks - before.decode_blocks == 64 * 8);
+    CHECK(after.encode_launches - before.encode_launches < 64 * 8);
+    std::printf("batching: %llu encode calls in %llu launches, %llu decode calls in %llu launches, %llu contexts\n",
+                (unsigned long long)(after.encode_blocks - before.encode_blocks),
+                (unsigned long long)(after.encode_launches - before.encode_launches),
+                (unsigned long long)(after.decode_blocks - before.decode_blocks),
+                (unsigned long long)(after.decode_launches - before.decode_launches),
+                (unsigned long long)after.contexts_created);
+  }
   std::printf("facade_test: %s (%d failures)\n", failures ? "FAILED" : "OK", failures);
   return failures ? 1 : 0;
+}
+
+// ---- facade throughput (facade_test --bench [blocks] [threads...]) ----
+// DwarFS's worker_group shape: T threads, each compressing / decompressing
+// its share of B independent 64 KiB blocks through the facade (host spans in
+// and out, so PCIe and host copies are included).  One JSON line per T.
+int bench(int argc, char** argv) {
+  size_t const blocks = argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 4096;
+  std::vector<int> threads;
+  for (int i = 3; i < argc; ++i) threads.push_back(std::atoi(argv[i]));
+  if (threads.empty()) threads = {1, 8, 64};
+  size_t const n = 32768;  // 64 KiB of samples
+  auto c = cfg(128, 1, true, 0);
+  std::vector<std::vector<uint16_t>> in(blocks);
+  std::mt19937_64 rng(42);
+  std::poisson_distribution<int> pois(1000.0);
+  for (auto& v : in) {
+    v.resize(n);
+    for (auto& x : v) x = bswap((uint16_t)pois(rng));
+  }
+  std::vector<std::vector<uint8_t>> enc(blocks);
+  std::vector<std::vector<uint16_t>> out(blocks, std::vector<uint16_t>(n));
+  for (int T : threads) {
+    auto run = [&](bool encode) {
+      std::vector<std::thread> pool;
+      auto t0 = std::chrono::steady_clock::now();
+      for (int t = 0; t < T; ++t) {
+        pool.emplace_back([&, t] {
+          auto e = ricepp_amd::create_encoder<uint16_t>(c);
+          auto d = ricepp_amd::create_decoder<uint16_t>(c);
+          for (size_t b = t; b < blocks; b += T) {
+            if (encode) enc[b] = e->encode(in[b]);
+            else d->decode(out[b], enc[b]);
+          }
+        });
+      }
+      for (auto& th : pool) th.join();
+      return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    };
+    run(true);  // warm the contexts
+    auto s0 = ricepp_amd::get_facade_stats();
+    double te = run(true);
+    auto s1 = ricepp_amd::get_facade_stats();
+    double td = run(false);
+    auto s2 = ricepp_amd::get_facade_stats();
+    bool ok = true;
+    for (size_t b = 0; b < blocks; ++b) ok = ok && out[b] == in[b];
+    double gib = double(blocks) * n * 2 / double(1ull << 30);
+    std::printf("{\"facade_bench\": true, \"threads\": %d, \"blocks\": %zu, \"block_bytes\": %zu, "
+                "\"encode_GiBps\": %.3f, \"decode_GiBps\": %.3f, \"encode_launches\": %llu, "
+                "\"decode_launches\": %llu, \"roundtrip_ok\": %s}\n",
+                T, blocks, n * 2, gib / te, gib / td, (unsigned long long)(s1.encode_launches - s0.encode_launches),
+                (unsigned long long)(s2.decode_launches - s1.decode_launches), ok ? "true" : "false");
+    std::fflush(stdout);
+    if (!ok) return 1;
+  }
+  return 0;
 }

@@ -100,8 +100,12 @@ def test_block_compressor_host_side_contract():
         comp.compress(b"\0\0", None)
     with pytest.raises(RuntimeError, match="unexpected data configuration: 6 bytes to compress, 2 components"):
         comp.compress(b"\0" * 6, meta)
-    with pytest.raises(RuntimeError):
-        block_codec.block_compressor("ricepp:block_size=8")
+    # the factory does not range-check (src/compression/ricepp.cpp:277-281): block_size=8 is a
+    # valid ricepp configuration, 513 fails in create_encoder at compress time (:97-102)
+    assert block_codec.block_compressor("ricepp:block_size=8").describe() == "ricepp [block_size=8]"
+    big = block_codec.block_compressor("ricepp:block_size=513")
+    with pytest.raises(RuntimeError, match="Unsupported configuration"):
+        big.compress(b"\0" * 4, meta)
     with pytest.raises(RuntimeError, match="unsupported version: 2"):
         block_codec.RiceppBlockDecompressor(block_codec.frame_header(16, 128, 1, 2, 0, True, version=2))
     with pytest.raises(RuntimeError, match="unsupported bytes per sample: 3"):
@@ -118,3 +122,11 @@ def test_cpp_facade_test_builds():
     r = subprocess.run(["bash", str(ROOT / "tests" / "cpp" / "build.sh")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     assert (ROOT / "tests" / "cpp" / "build" / "facade_test").exists()
+
+
+def test_plugin_callsites_compile_against_facade():
+    """src/compression/ricepp.cpp's ricepp calls compile against include/ricepp_amd.hpp with only the
+    include and the namespace changed (tests/cpp/plugin_callsites.cpp restates the call expressions)."""
+    r = subprocess.run(["g++", "-std=c++20", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I", str(ROOT / "include"),
+                        str(ROOT / "tests" / "cpp" / "plugin_callsites.cpp")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
