@@ -72,14 +72,27 @@ def device_copy_gbps(dev, nbytes: int = 1 << 30, iters: int = 10) -> float:
     return gbps
 
 
-def cpu_baseline(sample: np.ndarray, nblocks: int, n: int, cfg: codec.CodecConfig, min_seconds: float):
-    """The CPU oracle (C restatement of ricepp, kind "port") on host cores."""
-    from oracle import oracle as O
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
-    threads = int(os.environ.get("RICEPP_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    oc = O.cfg(cfg.block_size, cfg.component_stream_count, cfg.byteorder == "big", cfg.unused_lsb_count)
-    offs = (np.arange(nblocks, dtype=np.uint64) * n)
-    cap = O.worst_case_bytes(oc, n)
+
+def cpu_share() -> int:
+    """Host threads this job may use: the affinity mask, capped at the GPU box's CPU share (16 per GPU;
+    os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return int(os.environ.get("RICEPP_CPU_THREADS", min(16, n)))
+
+
+def _cpu_roundtrip(O, oc, sample, offs, n, nblocks, cap, threads, min_seconds):
     reps, t0 = 0, time.perf_counter()
     while True:
         out, oo, sz, st = O.encode_batch(oc, sample, offs, [n] * nblocks, cap, nthreads=threads)
@@ -89,15 +102,60 @@ def cpu_baseline(sample: np.ndarray, nblocks: int, n: int, cfg: codec.CodecConfi
         if el >= min_seconds:
             break
     assert (st == 0).all() and (dst == 0).all() and np.array_equal(dec, sample)
-    gib = reps * sample.nbytes / 2**30
+    return reps * sample.nbytes / 2**30 / el, reps, el
+
+
+def cpu_baseline(sample: np.ndarray, nblocks: int, n: int, cfg: codec.CodecConfig, min_seconds: float):
+    """The CPU oracle (C restatement of ricepp, kind "port") on host cores: one thread and the job's whole
+    CPU share, over independent blocks."""
+    from oracle import oracle as O
+
+    threads = cpu_share()
+    oc = O.cfg(cfg.block_size, cfg.component_stream_count, cfg.byteorder == "big", cfg.unused_lsb_count)
+    offs = (np.arange(nblocks, dtype=np.uint64) * n)
+    cap = O.worst_case_bytes(oc, n)
+    nb1 = max(1, nblocks // 8)  # one thread: a smaller sample, same blocks
+    v1, r1, e1 = _cpu_roundtrip(O, oc, sample[: nb1 * n], offs[:nb1], n, nb1, cap, 1, min_seconds / 2)
+    vn, rn, en = _cpu_roundtrip(O, oc, sample, offs, n, nblocks, cap, threads, min_seconds / 2)
     return {
-        "value": round(gib / el, 4),
+        "value": round(vn, 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
+        "single_thread_value": round(v1, 4),
+        "cpu_model": cpu_model(),
+        "host_cpus": os.cpu_count(),
         "sample": f"{nblocks} x 64 KiB Poisson(1000) BE bs128 cs1 blocks (first {nblocks} of the GPU workload), "
-                  f"encode+decode x{reps}, {el:.1f} s wall, {threads} threads over independent blocks",
+                  f"encode+decode x{rn}, {en:.1f} s wall, {threads} threads over independent blocks; "
+                  f"1 thread: {nb1} blocks x{r1}, {e1:.1f} s",
     }
+
+
+def kernel_source_sha256() -> str:
+    """Identity of the kernels a committed PMC profile was taken of (their HIP sources)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted((ROOT / "dwarfs_amd" / "csrc").glob("*.hip")):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def profiled_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from profiles/pmc_latest.json (rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes, gfx950 corrections of MI355X_MICROARCH.md), only if it was taken of the current sources."""
+    pmc = ROOT / "profiles" / "pmc_latest.json"
+    if not pmc.exists():
+        return None, "no PMC profile"
+    try:
+        j = json.loads(pmc.read_text())
+    except ValueError:
+        return None, "unreadable PMC profile"
+    if j.get("kernel_source_sha256") != kernel_source_sha256():
+        return None, "PMC profile of other kernel sources (stale); not reported"
+    v = j.get(kernel, {}).get("hbm_bytes_per_launch")
+    return v, f"{j.get('source', 'profiles')} (rocprofv3 PMC, kernel sources sha256 {j['kernel_source_sha256'][:12]})"
 
 
 def main() -> None:
@@ -159,13 +217,7 @@ def main() -> None:
     kt, kb = (k_dec, dec_bytes) if dominant == "decode" else (k_enc, enc_bytes)
     achieved = kb / kt / 1e9
 
-    traffic = None
-    pmc = ROOT / "profiles" / "pmc_latest.json"
-    if pmc.exists():
-        try:
-            traffic = json.loads(pmc.read_text()).get(f"rpp_{dominant}_kernel", {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_src = profiled_traffic(f"rpp_{dominant}_kernel")
 
     total_bytes = raw_bytes * world * args.steps
     value = total_bytes / elapsed / 2**30
@@ -202,6 +254,7 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "device_copy_GBps": round(device_copy_gbps(dev), 1),
         },
     }

@@ -251,12 +251,18 @@ def unused_lsb_count_batch(
     d_off = _dev_u64(offsets, dev)
     d_n = _dev_u64(n_samples, dev)
     work = torch.empty(ni, dtype=torch.int32, device=dev)
-    st = N.lib().rpp_unused_lsb_batch(
-        C.c_void_p(samples.data_ptr()), C.c_void_p(d_off.data_ptr()), C.c_void_p(d_n.data_ptr()),
-        int(n_samples.max()), ni, 1 if big_endian else 0, C.c_void_p(work.data_ptr()),
-        C.c_void_p(counts.data_ptr()), _stream_ptr(stream))
-    _raise_status(st)
+    # the C ABI takes at most 65535 images per call (grid.y): slices
+    for i0 in range(0, ni, _LSB_MAX_IMAGES):
+        i1 = min(ni, i0 + _LSB_MAX_IMAGES)
+        st = N.lib().rpp_unused_lsb_batch(
+            C.c_void_p(samples.data_ptr()), C.c_void_p(d_off.data_ptr() + 8 * i0),
+            C.c_void_p(d_n.data_ptr() + 8 * i0), int(n_samples[i0:i1].max()), i1 - i0, 1 if big_endian else 0,
+            C.c_void_p(work.data_ptr() + 4 * i0), C.c_void_p(counts.data_ptr() + 4 * i0), _stream_ptr(stream))
+        _raise_status(st)
     return counts
+
+
+_LSB_MAX_IMAGES = 65535
 
 
 class Encoder:

@@ -109,3 +109,85 @@ def test_gpu_fits_fixtures(name):
     d = torch.from_numpy(np.ascontiguousarray(x).view(np.int16)).to("cuda:0")
     got = codec.unused_lsb_count_batch(d, [0], [len(x)]).cpu().numpy()
     assert int(got[0]) == O.unused_lsb_count(x)
+
+
+def _one_pixel_batch(n, positions, aligns, us):
+    """Images of n samples, each all zero but one sample 1 << u at `pos`, stored at ragged alignments."""
+    imgs, offs, want, pos_total = [], [], [], 0
+    for a in aligns:
+        for p in positions:
+            for u in us:
+                pos_total += a
+                offs.append(pos_total)
+                imgs.append((p, u))
+                want.append(u)
+                pos_total += n
+    flat = np.zeros(pos_total + 16, np.uint16)
+    for o, (p, u) in zip(offs, imgs):
+        flat[o + p] = be(1 << u)
+    return flat, offs, want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [131072 + 3, 3 * 131072 + 5])
+def test_gpu_single_pixel_in_every_load_slot(n):
+    """One set sample in each of the four in-flight 16-byte loads (w0..w3), the remainder loop, the ragged
+    head and tail, and the next chunk, for both chunk sizes (64 KiB for small batches, 256 KiB once the
+    batch gives the 256 CUs four blocks each)."""
+    dev = torch.device("cuda:0")
+    T = 256
+    pos = {0, 1, 7, 8, 9, n - 1, n - 2, n - 9}
+    for chunk in (32768, 131072):
+        for j in range(4):  # w0..w3 of the first unrolled trip, lanes 0 and 255
+            pos |= {8 * (j * T) + 3, 8 * (j * T + T - 1) + 5}
+        pos |= {8 * (4 * T) + 2, chunk - 9, chunk - 1, chunk, chunk + 1, chunk + 8 * (3 * T) + 6}
+        pos |= {min(n - 1, 2 * chunk + 17), chunk - 8 * T + 4}  # remainder loop of a chunk
+    positions = sorted(p for p in pos if 0 <= p < n)
+    flat, offs, want = _one_pixel_batch(n, positions, aligns=(0, 1, 3), us=(0, 7))
+    d = torch.from_numpy(flat.view(np.int16)).to(dev)
+    ns = [n] * len(offs)
+    got = codec.unused_lsb_count_batch(d, offs, ns).cpu().numpy()  # small batch: 64 KiB chunks
+    assert list(got) == want
+    # the same images padded with aliased all-zero images to a big batch: 256 KiB chunks
+    zero_off = len(flat) - 16
+    pad = max(0, 1100 - len(offs))
+    got2 = codec.unused_lsb_count_batch(d, offs + [zero_off] * pad, ns + [1] * pad).cpu().numpy()
+    assert list(got2[:len(offs)]) == want and set(got2[len(offs):]) <= {16}
+
+
+@pytest.mark.gpu
+def test_gpu_images_longer_than_max_samples_are_read_whole():
+    """max_samples only sizes the grid: a caller passing a smaller value still gets whole images scanned
+    (the blocks stride over the chunks)."""
+    import ctypes as C
+
+    from dwarfs_amd import _native as N
+
+    dev = torch.device("cuda:0")
+    n = 5 * 32768 + 11
+    flat, offs, want = _one_pixel_batch(n, [n - 1, 4 * 32768 + 5, 40000], aligns=(0, 2), us=(3,))
+    d = torch.from_numpy(flat.view(np.int16)).to(dev)
+    d_off = torch.as_tensor(np.asarray(offs, np.int64), device=dev)
+    d_n = torch.as_tensor(np.full(len(offs), n, np.int64), device=dev)
+    work = torch.empty(len(offs), dtype=torch.int32, device=dev)
+    counts = torch.empty(len(offs), dtype=torch.int32, device=dev)
+    st = N.lib().rpp_unused_lsb_batch(C.c_void_p(d.data_ptr()), C.c_void_p(d_off.data_ptr()),
+                                      C.c_void_p(d_n.data_ptr()), 1, len(offs), 1, C.c_void_p(work.data_ptr()),
+                                      C.c_void_p(counts.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert st == 0
+    assert list(counts.cpu().numpy()) == want
+
+
+@pytest.mark.gpu
+def test_gpu_more_than_65535_images_are_split():
+    dev = torch.device("cuda:0")
+    ni = 70001
+    x = np.zeros(ni * 4 + 16, np.uint16)
+    want = []
+    for i in range(ni):
+        u = i % 11
+        x[4 * i + (i % 4)] = be(1 << u)
+        want.append(u)
+    d = torch.from_numpy(x.view(np.int16)).to(dev)
+    got = codec.unused_lsb_count_batch(d, [4 * i for i in range(ni)], [4] * ni).cpu().numpy()
+    assert np.array_equal(got, np.array(want))

@@ -280,3 +280,54 @@ def test_image_offsets_scan(n):
     if n > 1:
         want[1:] = np.cumsum(sizes)[:-1]
     assert np.array_equal(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("cs", [1, 2])
+def test_configs3_block_mix_in_one_launch(cs):
+    """BASELINE configs[3]: a shuffled mix of 1, 4 and 16 MiB Poisson blocks (the mkdwarfs block sizes)
+    encoded in ONE rpp_encode_batch and decoded in ONE rpp_decode_batch, every stream byte-identical to
+    the oracle's and every block restored."""
+    rng = np.random.default_rng(300 + cs)
+    sizes_mib = [1, 16, 1, 4, 1, 4, 1]
+    rng.shuffle(sizes_mib)
+    blocks = [datagen.poisson_data(rng, m * (1 << 19), lam=float(rng.integers(200, 3000))) for m in sizes_mib]
+    run_batch(codec.CodecConfig(128, cs, "big", 0), blocks)
+
+
+def _decode_oracle_streams(cfg, blocks):
+    """Decode-only (BASELINE configs[2]): streams produced by the CPU oracle, decoded on the GPU."""
+    oc = ocfg(cfg)
+    streams = [O.encode(oc, b) for b in blocks]
+    offs, pos = [], 0
+    for s in streams:
+        offs.append(pos)
+        pos += (len(s) + 15) // 16 * 16
+    buf = np.zeros(pos + 16, np.uint8)
+    for o, s in zip(offs, streams):
+        buf[o:o + len(s)] = np.frombuffer(s, np.uint8)
+    d = torch.from_numpy(buf).to(DEV)
+    ns = [len(b) for b in blocks]
+    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], ns)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    outn = out.cpu().numpy().view(np.uint16)
+    p = 0
+    for i, b in enumerate(blocks):
+        assert np.array_equal(outn[p:p + len(b)], b), f"block {i}"
+        p += len(b)
+
+
+def test_decode_oracle_encoded_1mib_blocks():
+    """configs[2] as DwarFS stores frames with -S 20: 4096x4096 uint16 frames cut into 1 MiB blocks, the
+    streams encoded by the CPU oracle (per-frame seed 42+i), decoded on the GPU."""
+    blocks = []
+    for i in range(2):
+        frame = datagen.poisson_data(np.random.default_rng(42 + i), 4096 * 4096)
+        blocks += [frame[k:k + (1 << 19)] for k in range(0, len(frame), 1 << 19)][:12]
+    _decode_oracle_streams(codec.CodecConfig(128, 1, "big", 0), blocks)
+
+
+def test_decode_oracle_encoded_32mib_frame():
+    """configs[2] with one stream per frame: a whole 4096x4096 frame (32 MiB) encoded by the CPU oracle."""
+    frame = datagen.poisson_data(np.random.default_rng(42), 4096 * 4096)
+    _decode_oracle_streams(codec.CodecConfig(128, 1, "big", 0), [frame])
