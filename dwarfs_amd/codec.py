@@ -218,12 +218,23 @@ def decode_batch(
     d_n = _dev_u64(n_samples, dev)
     d_out_off = _dev_u64(out_offsets, dev)
     status = torch.empty(nb, dtype=torch.int32, device=dev)
-    st = N.lib().rpp_decode_batch(
+    total = int(n_samples.sum()) if nb else 0
+    ws = decode_workspace(config, total, nb, dev)
+    st = N.lib().rpp_decode_batch_ws(
         C.byref(c), C.c_void_p(data.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
         C.c_void_p(d_in_bytes.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),
-        C.c_void_p(d_n.data_ptr()), C.c_void_p(status.data_ptr()), _stream_ptr(stream))
+        C.c_void_p(d_n.data_ptr()), C.c_void_p(status.data_ptr()), total, C.c_void_p(ws.data_ptr()), ws.numel(),
+        _stream_ptr(stream))
     _raise_status(st)
     return out, status
+
+
+def decode_workspace(config: CodecConfig, total_samples: int, nblocks: int, device) -> torch.Tensor:
+    """Device workspace of ``rpp_decode_batch_ws`` (sub-block start positions, tile scan state) for a
+    batch of ``nblocks`` streams of ``total_samples`` samples."""
+    c = _check(config)
+    nbytes = int(N.lib().rpp_decode_workspace_bytes(C.byref(c), int(total_samples), int(nblocks)))
+    return torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
 
 
 def unused_lsb_count_batch(

@@ -32,6 +32,7 @@
 #include <stdlib.h>
 
 #include "ricepp_amd.h"
+#include "ricepp_internal.h"
 
 // Diagnostic builds only: -DRPP_ABLATE=<mask> changes the decode to time
 // its parts (outputs are then wrong): 4 no async ring refill, 64 no output
@@ -984,26 +985,28 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
 
   // ---- per-stream setup (wave-uniform) ----
   int32_t status = RPP_OK;
-  uint32_t N = 0, nbytes = 0;
+  uint32_t N = 0, nbytes = 0, mis = 0;
   const uint8_t* in = p.in;
   uint16_t* out = p.out;
   {
     const uint64_t n64 = p.n_samples[b];
     const uint64_t ioff = p.in_off[b];
     const uint64_t nb64 = p.in_bytes[b];
-    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ioff & 3u) || nb64 >= (UINT64_C(1) << 29)) {
+    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
       status = RPP_INVALID_ARGUMENT;
     } else {
+      // bit positions from the 4-aligned word holding the first byte
+      mis = (uint32_t)(ioff & 3u);
       N = (uint32_t)n64;
-      nbytes = (uint32_t)nb64;
-      in = p.in + ioff;
+      nbytes = (uint32_t)nb64 + mis;
+      in = p.in + (ioff - mis);
       out = p.out + p.out_off[b];
     }
   }
   const bool aligned16 = ((uintptr_t)in & 15u) == 0;
-  // last readable bit + 1: the reader pulls whole 8-byte packets
-  // (bitstream_reader.h:149-183), so it only throws past this point.
-  const uint32_t lim = 64u * ((nbytes + 7u) >> 3);
+  // last readable bit + 1: the reader pulls whole 8-byte packets of the
+  // stream (bitstream_reader.h:149-183), so it only throws past this point.
+  const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
   const uint32_t chunk_len = CS * bs;
   const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
 
@@ -1076,11 +1079,11 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
 
   // codec.h:69-74,81-86: the 16-bit initial value of each component
   uint32_t last0 = 0, last1 = 0;
-  uint32_t P = 16 * CS;
+  uint32_t P = 8 * mis + 16 * CS;
   if (status == RPP_OK) {
-    if (16 * CS > lim) status = RPP_TRUNCATED_INPUT;
-    last0 = __builtin_amdgcn_readfirstlane(peek32(0) & 0xFFFFu);
-    if (CS > 1) last1 = __builtin_amdgcn_readfirstlane(peek32(16) & 0xFFFFu);
+    if (P > lim) status = RPP_TRUNCATED_INPUT;
+    last0 = __builtin_amdgcn_readfirstlane(peek32(8 * mis) & 0xFFFFu);
+    if (CS > 1) last1 = __builtin_amdgcn_readfirstlane(peek32(8 * mis + 16) & 0xFFFFu);
   }
   // this lane's 64 bits from bit sb of the stream (its 24-bit segment of a
   // window and what follows it)
@@ -1583,6 +1586,375 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
 #endif
 }
 
+
+// ===========================================================================
+// DECODE, PARSE PASS (rpp_decode_batch stage 1 of 2)
+// ===========================================================================
+// The serial part of decoding a stream is finding where each sub-block
+// starts: sub-block k+1 begins where the n-th code of sub-block k ends
+// (codec.h:103-140, decode.h:42-83).  rpp_parse_kernel does only that, with
+// the exact table-driven parse of rpp_decode_kernel (window map scan, count
+// scan, the lane holding code n-1) and none of its value extraction, and
+// records the start bit of every sub-block's header (plus the end of the last
+// one) in sb_pos.  The values are then produced by rpp_extract_kernel
+// (ricepp_decode2.hip) with all sub-blocks of all streams in parallel.
+//
+// Bit positions are relative to the 4-byte-aligned word containing the
+// stream's first byte (streams may start at any byte offset): the stream's bit
+// 0 is at 8 * (in_off & 3).
+struct ParseParams {
+  const uint8_t* in;
+  const uint64_t* in_off;
+  const uint64_t* in_bytes;
+  const uint64_t* n_samples;
+  const uint64_t* sb_base;  // [nblocks] first sb_pos entry of stream b
+  uint32_t* sb_pos;         // [sum(nsb_b + 1)] header start bits, then the end
+  int32_t* status;
+  uint32_t nblocks;
+  uint32_t bs;
+  uint32_t waves;  // waves (streams) per workgroup
+};
+
+template <uint32_t CS>
+__global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParseParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
+  {
+    const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
+    for (uint32_t i = threadIdx.x; i < kMapEntries; i += blockDim.x) dsm[i] = gt[i];
+  }
+  __syncthreads();
+  const uint4* tab = dsm;
+  const uint32_t lane = lane_id();
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint32_t ring_w = kTabBytes / 4 + wv * kWaveLdsWords;
+  asm("" : "+s"(ring_w));
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + ring_w;
+  const uint32_t bs = p.bs;
+  const uint32_t lane24 = kSegBits * lane;
+  const uint32_t b = blockIdx.x * p.waves + wv;
+  if (b >= p.nblocks) return;  // no barrier below this point
+
+  // ---- per-stream setup (wave-uniform) ----
+  int32_t status = RPP_OK;
+  uint32_t N = 0, nbytes = 0, mis = 0;
+  const uint8_t* in = p.in;
+  {
+    const uint64_t n64 = p.n_samples[b];
+    const uint64_t ioff = p.in_off[b];
+    const uint64_t nb64 = p.in_bytes[b];
+    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
+      status = RPP_INVALID_ARGUMENT;
+    } else {
+      N = (uint32_t)n64;
+      mis = (uint32_t)(ioff & 3u);
+      nbytes = (uint32_t)nb64 + mis;  // bytes from the aligned base
+      in = p.in + (ioff - mis);
+    }
+  }
+  uint32_t* const pos_out = p.sb_pos + p.sb_base[b];
+  const bool aligned16 = ((uintptr_t)in & 15u) == 0;
+  // last readable bit + 1: the reader pulls whole 8-byte packets of the
+  // stream (bitstream_reader.h:149-183), zero past its last byte
+  const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
+  const uint32_t chunk_len = CS * bs;
+  const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
+
+  // ---- LDS ring of the stream's words (as rpp_decode_kernel) ----
+  uint32_t fill_w = 0;
+  bool pend = false;
+  auto retire = [&]() {
+    if (pend) {
+      vm_drain();
+      fill_w += kChunkWords;
+      pend = false;
+    }
+  };
+  auto refill_sync = [&]() {
+    const uint32_t w = fill_w + 4 * lane;
+    uint4 v;
+    if (aligned16 && 4 * w + 16 <= nbytes) {
+      v = *reinterpret_cast<const uint4*>(in + 4 * w);
+    } else {
+      v = make_uint4(stream_word(in, nbytes, w), stream_word(in, nbytes, w + 1), stream_word(in, nbytes, w + 2),
+                     stream_word(in, nbytes, w + 3));
+    }
+    *reinterpret_cast<uint4*>(&ring[w & kRingMask]) = v;
+    if ((w & kRingMask) < kRingPad) *reinterpret_cast<uint4*>(&ring[kRingWords + (w & kRingMask)]) = v;
+    fill_w += kChunkWords;
+  };
+  auto request = [&]() {
+    if (4u * (fill_w + kChunkWords) > nbytes) return;
+    const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[fill_w & kRingMask]);
+    const uint8_t* src = in + 4u * fill_w;
+    if (aligned16) {
+      glds16(src + 16u * lane, slot);
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) glds4(src + 256u * q + 4u * lane, slot + 256u * q);
+    }
+    if ((fill_w & kRingMask) == 0)
+      glds4(src + 4u * lane, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[kRingWords]));
+    pend = true;
+  };
+  refill_sync();
+  refill_sync();
+  lds_fence();
+  auto ensure = [&](uint32_t w) {
+    if (fill_w < w + kAhead) {
+      retire();
+      while (fill_w < w + kAhead) refill_sync();
+      lds_fence();
+    }
+  };
+  auto wptr = [&](uint32_t w) -> const uint32_t* { return ring + (w & kRingMask); };
+  auto load_x = [&](uint32_t sb, uint32_t& xl) {
+    const uint32_t* q = wptr(sb >> 5);
+    xl = __builtin_amdgcn_alignbit(q[1], q[0], sb & 31u);
+  };
+  auto ring_keep = [&](uint32_t q) {
+    if (pend && fill_w < (q >> 5) + kAhead + 128) retire();
+    if (!pend && fill_w <= (q >> 5) + 766) request();
+  };
+
+  // ---- sub-block start positions, buffered 64 at a time in one VGPR ----
+  uint32_t pbuf = 0, pcnt = 0, pstart = 0;
+  auto flush = [&]() {
+    if (lane < pcnt) pos_out[pstart + lane] = pbuf;
+    pstart += pcnt;
+    pcnt = 0;
+  };
+  auto record = [&](uint32_t pos) {
+    pbuf = lane == pcnt ? pos : pbuf;
+    if (++pcnt == kWave) flush();
+  };
+
+  uint32_t P = 8u * mis + 16u * CS;  // codec.h:81-86: the initial values
+  if (status == RPP_OK && P > lim) status = RPP_TRUNCATED_INPUT;
+  const uint32_t nsb = nchunks * CS;
+  const bool fast_bs = bs == 2 * kWave || bs == 16 || bs == 32 || bs == 64;
+  const uint32_t nsb_fast = fast_bs ? (N / chunk_len) * CS : 0u;
+  ScanRegs sreg;
+
+  uint32_t s = 0;
+  while (s < nsb && status == RPP_OK) {
+    // ---- fast loop: Rice sub-blocks of bs codes with fs in [LO, HI] lying
+    //      in one window, ring resident; the parse of sub-block s+1 is issued
+    //      as soon as the end of s is known ----
+    auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI>() {
+      const uint32_t n = bs;
+      auto seg_bits = [&](uint32_t q) {
+        const uint32_t o = lane24 + (q & 31u);
+        uint32_t oi = o >> 5;
+        asm("" : "+v"(oi));
+        const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
+        return __builtin_amdgcn_alignbit(w[1], w[0], o);
+      };
+      auto fs_of = [](uint32_t h) {
+        uint32_t r;
+        asm("s_and_b32 %0, %1, 15\n\ts_max_u32 %0, %0, %2\n\ts_min_u32 %0, %0, %3\n\ts_sub_u32 %0, %0, 1"
+            : "=&s"(r)
+            : "s"(h), "n"(LO + 1), "n"(HI + 1)
+            : "scc");
+        return r;
+      };
+      auto header_ok = [](uint32_t h) { return (h & 15u) - (LO + 1) <= HI - LO; };
+      // end (next header) of the sub-block at bit q, if it lies in the window
+      auto parse = [&](uint32_t q, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
+        const uint32_t k = fs + 1;
+        const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});
+        Map8 M = comp8(Map8{e2.x, e2.y}, M01);
+        M = scan8_shr1(M, sreg.r1);
+        M = scan8_shr2(M, sreg.r2);
+        M = scan8_shr4(M, sreg.r4);
+        M = scan8_shr8(M, sreg.r8);
+        M = scan8_bc15(M, sreg.b15);
+        M = scan8_bc31(M, sreg.b31);
+        const Map8 X = shift8_wave(M, sreg.w1);
+        const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
+        const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+        const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
+        const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
+        uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
+        const uint32_t cnt = __builtin_popcount(tm);
+        const uint32_t incl = wave_incl_sum(cnt);
+        const uint64_t finm = __ballot(incl >= n);
+        const uint32_t excl = incl - cnt;
+        uint32_t t[MT];
+#pragma unroll
+        for (uint32_t j = 0; j < MT; ++j) {
+          t[j] = ffbl(tm);
+          tm &= tm - 1;
+        }
+        const uint32_t r = n - 1 - excl;
+        uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
+        if constexpr (MT > 4) {
+          const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
+          tpk = r < 4 ? tpk : tpk1;
+        }
+        const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
+        const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
+        Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
+        return finm != 0;
+      };
+      auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2) {
+        const uint4* tb = tab + 256u * fs;
+        e0 = tb[xl & 0xFFu];
+        e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
+        e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+      };
+      uint32_t pn_limit, trig_w;
+      auto ring_bounds = [&]() {
+        pn_limit = min(lim - 4u, 32u * (fill_w - kAhead) + 31u);
+        trig_w = pend ? fill_w - (kAhead + 127u) : (fill_w > 766u ? fill_w - 766u : 0u);
+      };
+      ring_bounds();
+      uint32_t Pn;
+      const uint32_t xl = seg_bits(P);
+      const uint32_t h = __builtin_amdgcn_readfirstlane(xl);
+      uint32_t fs = fs_of(h);
+      uint4 e0, e1, e2;
+      lookups(xl, fs, e0, e1, e2);
+      bool ok = parse(P, fs, e0, e1, e2, Pn) && header_ok(h);
+      while (ok) {
+        // sub-block s at P ends at Pn; parse s+1 at Pn
+        const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
+        const uint32_t xlB = seg_bits(Pn);
+        const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
+        const uint32_t fsB = fs_of(hB);
+        lookups(xlB, fsB, e0, e1, e2);
+        uint32_t PnB;
+        ok = parse(Pn, fsB, e0, e1, e2, PnB) && header_ok(hB) && nxt;
+        record(P);
+        ++s;
+        P = Pn;
+        if (!ok) {
+          if (P > lim) status = RPP_TRUNCATED_INPUT;
+          break;
+        }
+        Pn = PnB;
+        fs = fsB;
+        if ((Pn >> 5) >= trig_w) {
+          ring_keep(Pn);
+          ring_bounds();
+        }
+      }
+    };
+    while (s < nsb_fast && status == RPP_OK && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
+      const uint32_t* w = ring + ((P >> 5) & kRingMask);
+      const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
+      const uint32_t s0 = s;
+      if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
+      else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
+      if (s == s0) break;  // the general path takes this sub-block
+    }
+    if (s >= nsb || status != RPP_OK) break;
+    // ---- general path: one sub-block of any kind ----
+    const uint32_t cbase = (s / CS) * chunk_len;
+    const uint32_t n = min(N - cbase, chunk_len) / CS;
+    ensure(P >> 5);
+    if (P + 4 > lim) {  // decode.h:60: the 4-bit header
+      status = RPP_TRUNCATED_INPUT;
+      break;
+    }
+    record(P);
+    uint32_t xl;
+    load_x(P + kSegBits * lane, xl);
+    const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
+    if (fsp1 == 0) {  // decode.h:79-80
+      P += 4;
+    } else if (fsp1 == 15) {  // decode.h:72-77: n raw 16-bit values
+      if ((uint64_t)P + 4 + 16ull * n > lim) {
+        status = RPP_TRUNCATED_INPUT;
+        break;
+      }
+      P += 4 + 16 * n;
+    } else {  // decode.h:62-71: n Rice codes; find the end of code n-1
+      const uint32_t fs = fsp1 - 1;
+      const uint4* tb = tab + 256u * fs;
+      uint32_t q0 = P, s0 = 4, done = 0;
+      for (;;) {
+        const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
+                    e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+        uint32_t tm, xexit;
+        if (fs < 8) {
+          Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
+          M = scan_step8<kDppRowShr1>(M);
+          M = scan_step8<kDppRowShr2>(M);
+          M = scan_step8<kDppRowShr4>(M);
+          M = scan_step8<kDppRowShr8>(M);
+          M = scan_step8<kDppRowBcast15, 0xA>(M);
+          M = scan_step8<kDppRowBcast31, 0xC>(M);
+          const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
+          uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
+          const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+          sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+          const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+          sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+          const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+          xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
+          tm = t0 | (t1 << 8) | (t2 << 16);
+        } else {
+          const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
+          Map16 M = comp16(b2, comp16(b1, b0));
+          M = scan_step16<kDppRowShr1>(M);
+          M = scan_step16<kDppRowShr2>(M);
+          M = scan_step16<kDppRowShr4>(M);
+          M = scan_step16<kDppRowShr8>(M);
+          M = scan_step16<kDppRowBcast15, 0xA>(M);
+          M = scan_step16<kDppRowBcast31, 0xC>(M);
+          const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
+                         dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
+          uint32_t st = sel16(X, s0) & 0xFFu;
+          uint32_t t[3];
+          const uint4 ee[3] = {e0, e1, e2};
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const uint32_t sel = st | kSelByte0;
+            const bool skip = st >= 8;
+            t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
+            st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
+          }
+          tm = t[0] | (t[1] << 8) | (t[2] << 16);
+          xexit = st;
+        }
+        const uint32_t cnt = __builtin_popcount(tm);
+        const uint32_t incl = wave_incl_sum(cnt);
+        const uint32_t need = n - done;
+        const uint64_t fin = __ballot(incl >= need);
+        if (fin) {
+          // terminator need-1-excl of the first lane reaching need
+          const uint32_t lz = (uint32_t)__builtin_ctzll(fin);
+          uint32_t tmv = readlane(tm, (int)lz);
+          const uint32_t r = need - 1 - (readlane(incl, (int)lz) - readlane(cnt, (int)lz));
+          for (uint32_t j = 0; j < r; ++j) tmv &= tmv - 1;
+          P = q0 + kSegBits * lz + (uint32_t)__builtin_ctz(tmv) + fsp1;
+          break;
+        }
+        done += wave_last(incl);
+        s0 = wave_last(xexit);
+        q0 += kWinBits;
+        if (q0 >= lim) {  // the open unary search would read past the input
+          status = RPP_TRUNCATED_INPUT;
+          break;
+        }
+        ensure(q0 >> 5);
+        load_x(q0 + kSegBits * lane, xl);
+      }
+      if (status != RPP_OK) break;
+      if (P > lim) {
+        status = RPP_TRUNCATED_INPUT;
+        break;
+      }
+    }
+    ++s;
+    ring_keep(P);
+  }
+  retire();
+  if (status == RPP_OK) record(P);  // the end of the last sub-block
+  flush();
+  if (lane == 0) p.status[b] = status;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1640,10 +2012,13 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
-int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
-                     const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
-                     const uint64_t* d_out_offsets, const uint64_t* d_n_samples, int32_t* d_status,
-                     void* stream) {
+}  // extern "C"
+
+namespace rpp_internal {
+
+int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                        const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
+                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
   if (nblocks == 0) return RPP_OK;
@@ -1669,8 +2044,31 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count, W};
   const auto k = kernels[2 * (cfg->component_stream_count - 1) + (cfg->unused_lsb_count ? 1 : 0)];
-  hipLaunchKernelGGL(k, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(k, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
-}  // extern "C"
+int launch_parse(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets, const uint64_t* d_in_bytes,
+                 uint32_t nblocks, const uint64_t* d_n_samples, const uint64_t* d_sb_base, uint32_t* d_sb_pos,
+                 int32_t* d_status, hipStream_t stream) {
+  if (nblocks == 0) return RPP_OK;
+  uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
+  const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
+  static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1>, rpp_parse_kernel<2>};
+  static std::once_flag attr_once;
+  static hipError_t attr_err = hipSuccess;
+  std::call_once(attr_once, [] {
+    const int mx = (int)(kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4);
+    for (auto k : kernels)
+      if (attr_err == hipSuccess)
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+  });
+  if (attr_err != hipSuccess) return RPP_HIP_ERROR;
+  ParseParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_sb_base, d_sb_pos, d_status, nblocks,
+                cfg->block_size, W};
+  hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3((nblocks + W - 1) / W), dim3(kWave * W), lds,
+                     stream, p);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
+}  // namespace rpp_internal

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native as N
-from .codec import CodecConfig, _check, _raise_status
+from .codec import CodecConfig, _check, _raise_status, decode_workspace
 
 
 def partition_blocks(block_bytes: Sequence[int], world: int) -> List[Tuple[int, int]]:
@@ -152,6 +152,8 @@ class ShardPipeline:
         self.d_dec_off = torch.as_tensor(dec_off, device=dev)
         self.decoded = torch.empty(max(int(n_samples.sum()), 8), dtype=torch.int16, device=dev)
         self.dec_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
+        self.total_samples = int(n_samples.sum())
+        self.workspace = decode_workspace(config, self.total_samples, self.nblocks, dev)
         self.all_sizes: Optional[torch.Tensor] = None
         self.image_offsets: Optional[torch.Tensor] = None
         self.size_gather = SizeGather(self.nblocks, dev, group)
@@ -173,11 +175,12 @@ class ShardPipeline:
             C.c_void_p(self.enc_status.data_ptr()), self._stream()))
 
     def decode(self) -> None:
-        _raise_status(N.lib().rpp_decode_batch(
+        _raise_status(N.lib().rpp_decode_batch_ws(
             C.byref(self.cfg), C.c_void_p(self.data.data_ptr()), C.c_void_p(self.d_out_off.data_ptr()),
             C.c_void_p(self.sizes.data_ptr()), self.nblocks, C.c_void_p(self.decoded.data_ptr()),
             C.c_void_p(self.d_dec_off.data_ptr()), C.c_void_p(self.d_n.data_ptr()),
-            C.c_void_p(self.dec_status.data_ptr()), self._stream()))
+            C.c_void_p(self.dec_status.data_ptr()), self.total_samples, C.c_void_p(self.workspace.data_ptr()),
+            self.workspace.numel(), self._stream()))
 
     def gather(self) -> None:
         self.all_sizes = self.size_gather(self.sizes)

@@ -16,7 +16,8 @@
  *                            (ricepp/ricepp_cpuspecific.cpp:68-72,101-108), one
  *                            call per DwarFS block in src/compression/ricepp.cpp:136-137,
  *                            batched over many independent blocks
- *   rpp_decode_batch      <- decoder_interface::decode(span<u16>, span<u8 const>)
+ *   rpp_decode_batch /    <- decoder_interface::decode(span<u16>, span<u8 const>)
+ *   rpp_decode_batch_ws
  *                            (ricepp/include/ricepp/decoder_interface.h:37-50,
  *                            ricepp/ricepp_cpuspecific.cpp:127-144), called by
  *                            src/compression/ricepp.cpp:215-232
@@ -34,7 +35,7 @@
  *                            (:107-127 write, :186-201,237-249 read)
  *
  * Errors: C++ exceptions cannot cross this boundary.  Status codes map back to
- * the reference's exceptions in the C++ facade (dwarfs_amd/csrc/ricepp_host.hpp):
+ * the reference's exceptions in the C++ facade (include/ricepp_amd.hpp):
  *   RPP_UNSUPPORTED_CONFIG -> std::runtime_error("Unsupported configuration")
  *   RPP_TRUNCATED_INPUT    -> std::out_of_range (bitstream_reader.h:150-152)
  *
@@ -100,18 +101,41 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
 /*
  * Decode `nblocks` independent ricepp streams.
  *   d_in          encoded bytes
- *   d_in_offsets  [nblocks] byte offset of block b's stream, 4-aligned
+ *   d_in_offsets  [nblocks] byte offset of block b's stream (any alignment: a
+ *                 DwarFS payload right after its varint + thrift header)
  *   d_in_bytes    [nblocks] encoded size of block b
  *   d_out         decoded stored uint16 samples
  *   d_out_offsets [nblocks] start of block b's output, in samples, 8-aligned
  *   d_n_samples   [nblocks] samples to decode (multiple of cs)
  *   d_status      [nblocks] RPP_OK, RPP_TRUNCATED_INPUT (the reference's
  *                 std::out_of_range) or RPP_INVALID_ARGUMENT
+ * For bs 16/32/64/128 the decode runs in two passes over a device workspace
+ * (rpp_decode_batch_ws); this convenience form sizes it by reading
+ * d_n_samples back, i.e. it synchronises `stream` once, and allocates it
+ * stream-ordered (hipMallocAsync).
  */
 int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
                      const uint64_t* d_out_offsets, const uint64_t* d_n_samples,
                      int32_t* d_status, void* stream);
+
+/*
+ * Device workspace rpp_decode_batch_ws needs for a batch of `nblocks` streams
+ * holding `total_samples` samples in all (0 for an unsupported config).
+ */
+uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks);
+
+/*
+ * rpp_decode_batch with a caller-owned device workspace of at least
+ * rpp_decode_workspace_bytes(cfg, total_samples, nblocks) bytes, where
+ * total_samples >= the sum of d_n_samples.  Fully asynchronous on `stream`
+ * (graph-capturable).  Stage 1 finds every sub-block's start bit (one wave
+ * per stream), stage 2 decodes all sub-blocks in parallel (one lane each).
+ */
+int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                        const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
+                        const uint64_t* d_out_offsets, const uint64_t* d_n_samples, int32_t* d_status,
+                        uint64_t total_samples, void* d_workspace, uint64_t workspace_bytes, void* stream);
 
 /*
  * Unused least-significant bits of 16-bit images (the FITS categorizer's
