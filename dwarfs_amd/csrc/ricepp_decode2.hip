@@ -123,6 +123,7 @@ struct ExtractParams {
   uint32_t* counter;
   uint32_t nblocks;
   uint32_t bs, be, ulsb;
+  uint32_t dbg;  // diagnostics (RICEPP_DEC2_DBG): 1 no fast lanes, 2 fast lanes store sample by sample
 };
 
 // pixel traits (ricepp/ricepp_cpuspecific_traits.h:63-75)
@@ -300,8 +301,13 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
     // ---- fast lanes: Rice, a full sub-block, staged, every code <= 32 bits ----
     uint32_t hdr = 0;
     if (active) hdr = rd.peek32(start) & 15u;
-    bool fast = active && hdr != 0 && hdr != 15 && n == BS && (end >> 5) + 1 < w0 + nst;
-    if (CS == 2) fast = fast && __shfl_xor((int)fast, 1);  // pairs share one store path
+    bool fast = active && hdr != 0 && hdr != 15 && n == BS && (end >> 5) + 1 < w0 + nst && !(p.dbg & 1);
+    // pairs share one store path (the shuffle outside any condition: a
+    // short-circuit && would run it on the fast lanes only)
+    if (CS == 2) {
+      const int pf = __shfl_xor((int)fast, 1);
+      fast = fast && pf;
+    }
     uint32_t r[BS / 2];
     uint32_t agg = 0;
     if (fast) {
@@ -330,7 +336,10 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
       if (maxq > 31 - fs || pos != end - 32 * w0) fast = false;
       agg = acc & 0xFFFFu;
     }
-    if (CS == 2) fast = fast && __shfl_xor((int)fast, 1);
+    if (CS == 2) {
+      const int pf = __shfl_xor((int)fast, 1);
+      fast = fast && pf;
+    }
     // ---- general lanes: the element by the exact runtime loop ----
     if (active && !fast) agg = decode_general<false>(rd, start, n, 0, nullptr, CS, be, ulsb);
 
@@ -390,7 +399,13 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
         r[i] = px_write2<SH>(__builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, r[i]) + __builtin_bit_cast(us2, c2)),
                              selbe, ulsb);
       }
-      if constexpr (CS == 1) {
+      if (p.dbg & 2) {
+#pragma unroll
+        for (uint32_t i = 0; i < BS / 2; ++i) {
+          out[cbase + comp + CS * 2 * i] = (uint16_t)r[i];
+          out[cbase + comp + CS * (2 * i + 1)] = (uint16_t)(r[i] >> 16);
+        }
+      } else if constexpr (CS == 1) {
         uint4* o = reinterpret_cast<uint4*>(out + (size_t)k * BS);
 #pragma unroll
         for (uint32_t i = 0; i < BS / 8; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
@@ -483,7 +498,8 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
                                     : extract_kernel_for<2, false>(cfg->block_size));
   ExtractParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_out, d_out_offsets, d_status, w.sb_pos, w.sb_base,
                   w.tile_base, w.tile_map, w.tile_state, w.counter, nblocks, cfg->block_size,
-                  cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count};
+                  cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count, 0u};
+  if (const char* e = getenv("RICEPP_DEC2_DBG")) p.dbg = (uint32_t)atoi(e);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(w.max_tiles, kMaxExtractGrid);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kTile), 0, s, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
