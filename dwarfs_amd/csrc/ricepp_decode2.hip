@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "ricepp_amd.h"
 #include "ricepp_internal.h"
@@ -61,6 +62,15 @@ struct Workspace {
 };
 
 uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+// diagnostics (RICEPP_DEC2_DBG & 4): per-phase cycle sums of the extraction
+// tiles (wave 0 of each workgroup), read by rpp_diag_read
+__device__ unsigned long long g_dec2_diag[8];
+__device__ __forceinline__ uint64_t clk() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 
 Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks, uint8_t* base) {
   const uint64_t B = nblocks;
@@ -242,7 +252,7 @@ __device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t sel, uint32_t
 
 template <uint32_t CS, uint32_t BS, bool SH>
 __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
-  __shared__ uint32_t stage[kStageWords + kStagePad];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kStageWords + kStagePad];
   __shared__ uint32_t scan_buf[kTile];
   __shared__ uint32_t sh_tile, sh_carry[2], sh_min;
   const uint32_t tid = threadIdx.x;
@@ -252,6 +262,15 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
   const uint32_t chunk_len = CS * BS;
   const uint64_t total_tiles = p.tile_base[p.nblocks];
 
+  const bool timing = (p.dbg & 4) && tid < 64;
+  uint64_t tp = timing ? clk() : 0;
+  auto stamp = [&](int i) {
+    if (timing) {
+      const uint64_t now = clk();
+      if (tid == 0) atomicAdd(&g_dec2_diag[i], (unsigned long long)(now - tp));
+      tp = now;
+    }
+  };
   for (;;) {
     if (tid == 0) sh_tile = atomicAdd(p.counter, 1u);
     __syncthreads();
@@ -283,19 +302,39 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
     const uint32_t n = active ? min(N - cbase, chunk_len) / CS : 0u;
     uint16_t* const out = p.out + p.out_off[b];
 
-    // ---- stage the tile's words (zero past the stream) ----
+    stamp(0);
+    // ---- stage the tile's words: 16-byte loads, several in flight per
+    //      lane; the group holding the stream's end word by word (zero past
+    //      the last byte) ----
     const uint32_t w0 = pos_tab[k0] >> 5;
     const uint32_t wend = (pos_tab[k0 + kcount] >> 5) + 2;
     const uint32_t nst = min(wend - w0, kStageWords);
     {
-      const uint32_t* g = reinterpret_cast<const uint32_t*>(base);
-      const uint32_t full = nbytes / 4;  // whole words inside the stream
-      for (uint32_t i = tid; i < nst; i += kTile) {
-        const uint32_t w = w0 + i;
-        stage[i] = w < full ? g[w] : stream_word(base, nbytes, w);
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      const uint32_t nq = (nst + 3) / 4;  // 16-byte groups
+      constexpr uint32_t kInFlight = 4;
+      for (uint32_t q0 = 0; q0 < nq; q0 += kInFlight * kTile) {
+        u4 v[kInFlight];
+#pragma unroll
+        for (uint32_t j = 0; j < kInFlight; ++j) {
+          const uint32_t q = q0 + j * kTile + tid;
+          const uint32_t wq = w0 + 4 * q;
+          if (q < nq && 4 * wq + 16 <= nbytes) {
+            v[j] = *reinterpret_cast<const u4*>(base + 4 * wq);  // (4-byte aligned)
+          } else {
+            v[j] = u4{stream_word(base, nbytes, wq), stream_word(base, nbytes, wq + 1), stream_word(base, nbytes, wq + 2),
+                      stream_word(base, nbytes, wq + 3)};
+          }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kInFlight; ++j) {
+          const uint32_t q = q0 + j * kTile + tid;
+          if (q < nq) *reinterpret_cast<u4*>(&stage[4 * q]) = v[j];
+        }
       }
     }
     __syncthreads();
+    stamp(1);
     const Reader rd{stage, w0, nst, base, nbytes};
 
     // ---- fast lanes: Rice, a full sub-block, staged, every code <= 32 bits ----
@@ -343,6 +382,7 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
     // ---- general lanes: the element by the exact runtime loop ----
     if (active && !fast) agg = decode_general<false>(rd, start, n, 0, nullptr, CS, be, ulsb);
 
+    stamp(2);
     // ---- scan of the elements within the tile (per component: stride CS) ----
     scan_buf[tid] = agg;
     __syncthreads();
@@ -390,6 +430,7 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
     const uint32_t excl = tid >= CS ? scan_buf[tid - CS] : 0u;
     const uint32_t carry = combine(sh_carry[comp], excl) & 0xFFFFu;
 
+    stamp(3);
     // ---- stores ----
     if (fast) {
       const uint32_t c2 = carry * 0x10001u;
@@ -433,6 +474,8 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
       decode_general<true>(rd, start, n, carry, out + cbase + comp, CS, be, ulsb);
     }
     __syncthreads();  // (stage and scan_buf are reused by the next tile)
+    stamp(4);
+    if (timing && tid == 0) atomicAdd(&g_dec2_diag[7], 1ull);
   }
 }
 
@@ -449,14 +492,33 @@ ExtractKernel extract_kernel_for(uint32_t bs) {
   }
 }
 
+// The two-stage decode is selected by RICEPP_DECODE=two-stage; the default is
+// the fused one-wave-per-stream kernel (rpp_decode_kernel).  Measured on MI355X
+// (DESIGN.md section 4): the parse pass alone costs 86 VALU per 128-sample
+// sub-block and is VALU-bound at 74 % (196 us for 4096 x 64 KiB), about what
+// the fused kernel needs for parse AND values (258 us), whose value work
+// hides in the parse chain's latency; so splitting the passes does not pay
+// on this hardware.  The path stays for unaligned-offset and long-stream
+// experiments.
 bool two_stage(const rpp_config* cfg) {
-  if (const char* e = getenv("RICEPP_DECODE_FUSED")) return atoi(e) == 0;  // diagnostics
+  const char* e = getenv("RICEPP_DECODE");
+  if (!e || std::string(e) != "two-stage") return false;
   return cfg->block_size == 16 || cfg->block_size == 32 || cfg->block_size == 64 || cfg->block_size == 128;
 }
 
 }  // namespace
 
 extern "C" {
+
+// diagnostics only (not in the C ABI header): the extraction phase timers
+int rpp_diag_read(unsigned long long* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_dec2_diag), sizeof(g_dec2_diag)) != hipSuccess) return RPP_HIP_ERROR;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dec2_diag), z, sizeof(z)) != hipSuccess) return RPP_HIP_ERROR;
+  }
+  return RPP_OK;
+}
 
 uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks) {
   if (rpp_check_config(cfg) != RPP_OK) return 0;

@@ -294,14 +294,17 @@ def test_configs3_block_mix_in_one_launch(cs):
     run_batch(codec.CodecConfig(128, cs, "big", 0), blocks)
 
 
-def _decode_oracle_streams(cfg, blocks):
-    """Decode-only (BASELINE configs[2]): streams produced by the CPU oracle, decoded on the GPU."""
+def _decode_oracle_streams(cfg, blocks, ragged=False):
+    """Decode-only (BASELINE configs[2]): streams produced by the CPU oracle, decoded on the GPU.
+    ragged: streams start at arbitrary byte offsets (a DwarFS payload follows a 13-18 byte header)."""
     oc = ocfg(cfg)
     streams = [O.encode(oc, b) for b in blocks]
     offs, pos = [], 0
-    for s in streams:
+    for i, s in enumerate(streams):
+        if ragged:
+            pos += 1 + (7 * i) % 15
         offs.append(pos)
-        pos += (len(s) + 15) // 16 * 16
+        pos += len(s) if ragged else (len(s) + 15) // 16 * 16
     buf = np.zeros(pos + 16, np.uint8)
     for o, s in zip(offs, streams):
         buf[o:o + len(s)] = np.frombuffer(s, np.uint8)
@@ -331,3 +334,74 @@ def test_decode_oracle_encoded_32mib_frame():
     """configs[2] with one stream per frame: a whole 4096x4096 frame (32 MiB) encoded by the CPU oracle."""
     frame = datagen.poisson_data(np.random.default_rng(42), 4096 * 4096)
     _decode_oracle_streams(codec.CodecConfig(128, 1, "big", 0), [frame])
+
+
+# ---- the two-stage decode (RICEPP_DECODE=two-stage: parse pass + lane-per-sub-block extraction) ----
+
+class _two_stage:
+    def __enter__(self):
+        import os
+        self.old = os.environ.get("RICEPP_DECODE")
+        os.environ["RICEPP_DECODE"] = "two-stage"
+
+    def __exit__(self, *a):
+        import os
+        if self.old is None:
+            os.environ.pop("RICEPP_DECODE", None)
+        else:
+            os.environ["RICEPP_DECODE"] = self.old
+
+
+@pytest.mark.parametrize("bs", [16, 32, 64, 128])
+@pytest.mark.parametrize("cs", [1, 2])
+def test_two_stage_decode_config_matrix(bs, cs):
+    rng = np.random.default_rng(7000 + bs + cs)
+    with _two_stage():
+        for be, ulsb in ((True, 0), (False, 3)):
+            cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
+            blocks = []
+            for kind in ("poisson", "benchmark", "codec_test", "constant", "full_range", "spiky", "zeros"):
+                n = int(rng.integers(1, 6000)) // cs * cs
+                if kind == "poisson":
+                    blocks.append(datagen.poisson_data(rng, n, ulsb=ulsb, big_endian=be))
+                elif kind == "benchmark":
+                    blocks.append(datagen.benchmark_data(rng, n, ulsb=ulsb, big_endian=be))
+                elif kind == "codec_test":
+                    blocks.append(datagen.codec_test_data(rng, n, ulsb=ulsb, big_endian=be))
+                elif kind == "constant":
+                    blocks.append(datagen.constant_data(n, ulsb=ulsb, big_endian=be))
+                elif kind == "full_range":
+                    blocks.append(datagen.full_range_data(rng, n, ulsb=ulsb, big_endian=be))
+                elif kind == "spiky":
+                    blocks.append(datagen.spiky_data(rng, n, ulsb=ulsb, big_endian=be))
+                else:
+                    blocks.append(np.zeros(n, np.uint16))
+            run_batch(cfg, blocks)
+            _decode_oracle_streams(cfg, blocks)
+
+
+def test_two_stage_decode_long_streams_and_mix():
+    rng = np.random.default_rng(77)
+    blocks = [datagen.poisson_data(rng, m * (1 << 19)) for m in (1, 4, 1)] + [datagen.benchmark_data(rng, 300000)]
+    with _two_stage():
+        run_batch(codec.CodecConfig(128, 1, "big", 0), blocks)
+        run_batch(codec.CodecConfig(128, 2, "big", 0), blocks[:2])
+
+
+def test_two_stage_decode_errors_match_oracle():
+    with _two_stage():
+        test_truncated_input_status_matches_oracle()
+        for bs, cs in ((128, 1), (16, 2)):
+            test_corrupt_streams_match_oracle(bs, cs)
+
+
+@pytest.mark.parametrize("two_stage", [False, True])
+def test_decode_streams_at_any_byte_offset(two_stage):
+    """rpp_decode_batch takes streams at any byte offset (no repack of DwarFS payloads)."""
+    rng = np.random.default_rng(99)
+    ctx = _two_stage() if two_stage else __import__("contextlib").nullcontext()
+    with ctx:
+        for bs, cs in ((128, 1), (16, 2), (29, 1), (64, 2)):
+            blocks = [datagen.poisson_data(rng, int(n) // cs * cs) for n in rng.integers(0, 40000, 9)]
+            blocks += [datagen.benchmark_data(rng, 3000 // cs * cs), datagen.full_range_data(rng, 1000 // cs * cs)]
+            _decode_oracle_streams(codec.CodecConfig(bs, cs, "big", 0), blocks, ragged=True)

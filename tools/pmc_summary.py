@@ -7,12 +7,13 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(f"{root}/pmc_*/run_counter_collection.csv"):
+for f in glob.glob(f"{root}/pmc_*/run_counter_collection.csv") + glob.glob(f"{root}/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         if "rpp_" not in name:
             continue
-        k = "rpp_encode_kernel" if "encode" in name else "rpp_decode_kernel"
+        k = next((kk for kk in ("rpp_encode_kernel", "rpp_decode_kernel", "rpp_parse_kernel", "rpp_extract_kernel",
+                                "rpp_lsb_or_kernel", "rpp_pcm") if kk in name), name.split("(")[0])
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
 for k, d in sorted(agg.items()):
