@@ -36,6 +36,8 @@ EXPORTED_SYMBOLS = (
     "rpp_check_config",
     "rpp_worst_case_bytes",
     "rpp_encode_batch",
+    "rpp_encode_workspace_bytes",
+    "rpp_encode_batch_ws",
     "rpp_decode_batch",
     "rpp_decode_workspace_bytes",
     "rpp_decode_batch_ws",
@@ -106,6 +108,11 @@ def lib() -> C.CDLL:
         L.rpp_worst_case_bytes.restype = C.c_uint64
         L.rpp_encode_batch.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, P]
         L.rpp_encode_batch.restype = C.c_int
+        L.rpp_encode_workspace_bytes.argtypes = [C.POINTER(RppConfig), C.c_uint64, C.c_uint32]
+        L.rpp_encode_workspace_bytes.restype = C.c_uint64
+        L.rpp_encode_batch_ws.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, C.c_uint64, P,
+                                          C.c_uint64, P]
+        L.rpp_encode_batch_ws.restype = C.c_int
         L.rpp_decode_batch.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, P]
         L.rpp_decode_batch.restype = C.c_int
         L.rpp_decode_workspace_bytes.argtypes = [C.POINTER(RppConfig), C.c_uint64, C.c_uint32]

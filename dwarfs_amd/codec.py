@@ -177,12 +177,26 @@ def encode_batch(
     d_out_off = _dev_u64(out_offsets, dev)
     sizes = torch.empty(nb, dtype=torch.int64, device=dev)
     status = torch.empty(nb, dtype=torch.int32, device=dev)
-    st = N.lib().rpp_encode_batch(
+    total_samples = int(n_samples.sum()) if nb else 0
+    ws = encode_workspace(config, total_samples, nb, dev, stream)
+    st = N.lib().rpp_encode_batch_ws(
         C.byref(c), C.c_void_p(samples.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
         C.c_void_p(d_n.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),
-        C.c_void_p(sizes.data_ptr()), C.c_void_p(status.data_ptr()), _stream_ptr(stream))
+        C.c_void_p(sizes.data_ptr()), C.c_void_p(status.data_ptr()), total_samples, C.c_void_p(ws.data_ptr()),
+        ws.numel(), _stream_ptr(stream))
     _raise_status(st)
     return EncodedBatch(out, np.asarray(out_offsets, np.int64), d_out_off, sizes, status)
+
+
+def encode_workspace(config: CodecConfig, total_samples: int, nblocks: int, device, stream=None) -> torch.Tensor:
+    """Device workspace of ``rpp_encode_batch_ws`` (segment table and scratch for streams encoded by
+    several waves) for ``nblocks`` streams of ``total_samples`` samples."""
+    c = _check(config)
+    nbytes = int(N.lib().rpp_encode_workspace_bytes(C.byref(c), int(total_samples), int(nblocks)))
+    ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+    if stream is not None:
+        ws.record_stream(stream)
+    return ws
 
 
 def decode_batch(
@@ -220,6 +234,8 @@ def decode_batch(
     status = torch.empty(nb, dtype=torch.int32, device=dev)
     total = int(n_samples.sum()) if nb else 0
     ws = decode_workspace(config, total, nb, dev)
+    if stream is not None:
+        ws.record_stream(stream)
     st = N.lib().rpp_decode_batch_ws(
         C.byref(c), C.c_void_p(data.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
         C.c_void_p(d_in_bytes.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),

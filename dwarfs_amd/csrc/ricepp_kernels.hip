@@ -172,7 +172,22 @@ struct EncParams {
   int32_t* status;
   uint32_t nblocks;
   uint32_t bs, cs, be, ulsb;
+  // segment mode (long streams, rpp_encode_batch_ws): work unit u = segment
+  // u - seg_base[b] of stream b = seg_map[u]; null seg_map: unit = stream
+  const uint32_t* seg_map;
+  const uint64_t* seg_base;  // [nblocks + 1]: units before stream b; [nblocks] = total
+  uint64_t* seg_bits;        // [units] bits a segment wrote (multi-segment streams)
+  uint8_t* scratch;          // segments >= 1 of a stream: slot u - b - 1
+  uint64_t slot_bytes;
 };
+
+// Segment mode: a stream of more than kEncSegChunks chunks is encoded by
+// several waves, one per run of kEncSegChunks chunks.  Every sub-block's codes
+// depend only on its samples and the sample before it (encode.h:92-157), so a
+// segment starts from the real preceding sample, at bit 0 of its own scratch
+// slot (segment 0: after the initial values, in the stream's output), and
+// rpp_enc_concat_kernel then places each segment at its bit offset.
+constexpr uint32_t kEncSegChunks = 256;
 
 // Compile-time shape of an encode launch: SPL samples per lane (8 or 16), a
 // ricepp sub-block owned by an aligned group of G lanes (G = next pow2 of
@@ -542,14 +557,19 @@ template <uint32_t SPL, uint32_t G, uint32_t CS, bool SH>
 __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t win[kEncWin];
   constexpr uint32_t spw = kWave / G;  // sub-blocks per iteration
-  const uint32_t b = blockIdx.x;
+  uint32_t b = blockIdx.x, seg = 0;
+  if (p.seg_map) {
+    if (blockIdx.x >= p.seg_base[p.nblocks]) return;
+    b = p.seg_map[blockIdx.x];
+    seg = blockIdx.x - (uint32_t)p.seg_base[b];
+  }
   const uint32_t lane = lane_id();
   const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
   const uint64_t n64 = p.n_samples[b];
   const uint64_t ooff = p.out_off[b];
   if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || (ooff & 15u)) {
-    if (lane == 0) {
+    if (lane == 0 && seg == 0) {
       p.status[b] = RPP_INVALID_ARGUMENT;
       p.out_bytes[b] = 0;
     }
@@ -557,7 +577,13 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   }
   const uint32_t N = (uint32_t)n64;
   const uint16_t* in = p.in + p.in_off[b];
-  uint8_t* out8 = p.out + ooff;
+  const uint32_t chunk_len = CS * bs;
+  const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
+  const bool multi = p.seg_map && nchunks > kEncSegChunks;
+  // this unit's chunks [c_lo, c_hi)
+  const uint32_t c_lo = multi ? seg * kEncSegChunks : 0u;
+  const uint32_t c_hi = multi ? min(nchunks, c_lo + kEncSegChunks) : nchunks;
+  uint8_t* out8 = seg == 0 ? p.out + ooff : p.scratch + (size_t)(blockIdx.x - b - 1) * p.slot_bytes;
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
   unsigned long long tprev_;
@@ -567,20 +593,21 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   for (uint32_t i = lane; i < kEncWin; i += kWave) win[i] = 0;
   __syncthreads();
 
-  EncState st{win, reinterpret_cast<uint32_t*>(out8), 0u, 16 * CS, 16 * CS, 0u};
+  const uint32_t bit0 = seg == 0 ? 16 * CS : 0u;
+  EncState st{win, reinterpret_cast<uint32_t*>(out8), 0u, bit0, bit0, 0u};
   // codec.h:69-74,81-86: 16-bit initial value read(in[i]) per component.
-  if (lane < CS) emit_bits(win, 16 * lane, N ? px_read(in[lane], be, ulsb) : 0u);
-  // DPP-prev mode: the first sample is its own reference
-  st.carry = N ? px_read(in[0], be, ulsb) : 0u;
+  if (seg == 0 && lane < CS) emit_bits(win, 16 * lane, N ? px_read(in[lane], be, ulsb) : 0u);
+  // DPP-prev mode: the reference of the unit's first sample (the stream's
+  // first sample is its own reference)
+  st.carry = N ? px_read(in[c_lo ? c_lo * chunk_len - 1 : 0], be, ulsb) : 0u;
 
-  const uint32_t chunk_len = CS * bs;
-  const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
-  const uint32_t nsb = nchunks * CS;
+  const uint32_t nsb = c_hi * CS;     // sub-blocks [s_lo, nsb) are this unit's
+  const uint32_t s_lo = c_lo * CS;
   const uint32_t g = lane / G, j = lane % G;
   // full iterations: every sub-block complete, lanes own 0 or SPL samples
   const bool vec_ok = bs % SPL == 0 && ((uintptr_t)in & 15u) == 0;
-  const uint32_t nsb_full = vec_ok ? (N / chunk_len) * CS : 0u;
-  const uint32_t nfull = nsb_full / spw;
+  const uint32_t nsb_full = vec_ok ? min(N / chunk_len, c_hi) * CS : 0u;
+  const uint32_t nfull = nsb_full > s_lo ? (nsb_full - s_lo) / spw : 0u;
   const bool empty_lanes = G * SPL != bs;
   const bool dpp_prev = CS == 1 && !empty_lanes && !(RPP_EABLATE & 4);
 
@@ -592,16 +619,16 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   //      samples stay in place (no register copies) ----
   uint32_t it = 0;
   if (nfull) {
-    EncGeom g0 = enc_geom<SPL, CS>(g, j, nsb, N, bs);
+    EncGeom g0 = enc_geom<SPL, CS>(s_lo + g, j, nsb, N, bs);
     EncRaw<SPL> r0 = enc_load_vec<SPL, CS>(in, g0, !dpp_prev);
-    EncGeom g1 = enc_geom<SPL, CS>(spw + g, j, nsb, N, bs);
+    EncGeom g1 = enc_geom<SPL, CS>(s_lo + spw + g, j, nsb, N, bs);
     EncRaw<SPL> r1 = enc_load_vec<SPL, CS>(in, g1, !dpp_prev);
     EncPlan<SPL> P, Q;
     enc_plan_a<SPL, G, CS, SH>(P, st, r0, g0, selbe, be, ulsb, empty_lanes, dpp_prev);
     // (loads are unconditional: past the last group the geometry is empty
     // and the load reads the stream start; a conditional load would make
     // every later wait cover it)
-    g0 = enc_geom<SPL, CS>(2 * spw + g, j, nsb, N, bs);
+    g0 = enc_geom<SPL, CS>(s_lo + 2 * spw + g, j, nsb, N, bs);
     r0 = enc_load_vec<SPL, CS>(in, g0, !dpp_prev);
     enc_plan_b<SPL, G>(P, st, j);
     // emits group `it` (plan E) while planning group it+1 (into F, from rn,
@@ -610,7 +637,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
       RPP_STAT(0, 1);
       RPP_TSTAMP(1);
       enc_plan_a<SPL, G, CS, SH>(F, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
-      gn = enc_geom<SPL, CS>((it + 3) * spw + g, j, nsb, N, bs);
+      gn = enc_geom<SPL, CS>(s_lo + (it + 3) * spw + g, j, nsb, N, bs);
       rn = enc_load_vec<SPL, CS>(in, gn, !dpp_prev);
       RPP_TSTAMP(2);
       enc_emit<SPL>(E, st, j, empty_lanes);
@@ -632,7 +659,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
     ++it;
   }
   // ---- ragged tail / unaligned streams: per-sample loads ----
-  for (uint32_t s0 = it * spw; s0 < nsb; s0 += spw) {
+  for (uint32_t s0 = s_lo + it * spw; s0 < nsb; s0 += spw) {
     const EncGeom geo = enc_geom<SPL, CS>(s0 + g, j, nsb, N, bs);
     const EncRaw<SPL> r = enc_load_scalar<SPL, CS>(in, geo);
     enc_iteration<SPL, G, CS, SH>(st, r, geo, j, selbe, be, ulsb, true, false);
@@ -644,17 +671,115 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   //      (bitstream_writer.h:110-120,139-145) ----
   const uint32_t total_bytes = (st.base + 7) >> 3;
   const uint32_t full_end = st.base >> 5;
-  for (uint32_t w = st.win_w0 + lane; w < full_end; w += kWave) st.out32[w] = win[w - st.win_w0];
-  const uint32_t tail_bytes = total_bytes - 4 * full_end;
-  if (lane < tail_bytes) out8[4 * full_end + lane] = (uint8_t)(win[full_end - st.win_w0] >> (8 * lane));
+  if (multi && seg != 0) {
+    // a segment slot: whole words (the last one zero-padded) for the concat
+    for (uint32_t w = st.win_w0 + lane; w <= full_end; w += kWave) st.out32[w] = win[w - st.win_w0];
+  } else {
+    for (uint32_t w = st.win_w0 + lane; w < full_end; w += kWave) st.out32[w] = win[w - st.win_w0];
+    const uint32_t tail_bytes = total_bytes - 4 * full_end;
+    if (lane < tail_bytes) out8[4 * full_end + lane] = (uint8_t)(win[full_end - st.win_w0] >> (8 * lane));
+  }
   if (lane == 0) {
-    p.out_bytes[b] = total_bytes;
-    p.status[b] = RPP_OK;
+    if (multi) {
+      p.seg_bits[blockIdx.x] = st.base;  // (the concat kernel writes size and status)
+    } else {
+      p.out_bytes[b] = total_bytes;
+      p.status[b] = RPP_OK;
+    }
   }
 #ifdef RPP_STATS
   if (lane == 0)
     for (int i = 0; i < 16; ++i) atomicAdd(&g_rpp_stats[i], (unsigned long long)stat_acc[i]);
 #endif
+}
+
+// Units of each stream (nseg: one per kEncSegChunks chunks for a stream of
+// more than kEncSegChunks chunks, else 1); entry nblocks is 0 so the
+// exclusive scan ends in the total.
+__global__ void rpp_enc_units_kernel(const uint64_t* n_samples, uint32_t nblocks, uint32_t chunk_len, uint64_t* units) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nblocks) return;
+  uint64_t u = 0;
+  if (i < nblocks) {
+    const uint64_t n = n_samples[i];
+    const uint64_t nch = (n + chunk_len - 1) / chunk_len;
+    u = nch > kEncSegChunks && n < RPP_MAX_STREAM_SAMPLES ? (nch + kEncSegChunks - 1) / kEncSegChunks : 1;
+  }
+  units[i] = u;
+}
+
+__global__ void rpp_enc_unit_map_kernel(const uint64_t* seg_base, uint32_t nblocks, uint32_t* seg_map) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nblocks) return;
+  for (uint64_t u = seg_base[i]; u < seg_base[i + 1]; ++u) seg_map[u] = i;
+}
+
+// Places segment k >= 1 of a multi-segment stream at its bit offset o_k in the
+// stream's output (seg_off = exclusive scan of seg_bits over all units).  An
+// output word belongs to the segment holding its first bit and takes the
+// following segment's first bits above that segment's end; the word holding
+// o_1 (partly written by segment 0 in place) is merged by segment 1.  The
+// last word is written byte by byte up to ceil(bits / 8)
+// (bitstream_writer.h:139-145); the last segment writes size and status.
+__global__ __launch_bounds__(256) void rpp_enc_concat_kernel(EncParams p, const uint64_t* seg_off) {
+  const uint32_t u = blockIdx.x;
+  if (u >= p.seg_base[p.nblocks]) return;
+  const uint32_t b = p.seg_map[u];
+  const uint32_t first = (uint32_t)p.seg_base[b], nseg = (uint32_t)(p.seg_base[b + 1] - first);
+  const uint32_t k = u - first;
+  if (nseg < 2 || k == 0) return;
+  const uint64_t base = seg_off[first];
+  const uint32_t o_k = (uint32_t)(seg_off[u] - base);
+  const uint32_t L_k = (uint32_t)p.seg_bits[u];
+  const uint32_t total_bits = (uint32_t)(seg_off[first + nseg - 1] - base) + (uint32_t)p.seg_bits[first + nseg - 1];
+  const uint32_t total_bytes = (total_bits + 7) >> 3;
+  const bool last = k + 1 == nseg;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(p.scratch + (size_t)(u - b - 1) * p.slot_bytes);
+  const uint32_t* nxt = last ? nullptr : reinterpret_cast<const uint32_t*>(p.scratch + (size_t)(u - b) * p.slot_bytes);
+  const uint32_t o_n = o_k + L_k;  // next segment's offset
+  uint8_t* out8 = p.out + p.out_off[b];
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
+  // bits [x, x + 32) of this segment (zero past its end)
+  auto seg_bits32 = [&](uint32_t x) -> uint32_t {
+    if (x >= L_k) return 0u;
+    const uint32_t i = x >> 5, sh = x & 31u;
+    const uint32_t lo = src[i];
+    const uint32_t hi = (32 * (i + 1) < L_k) ? src[i + 1] : 0u;
+    uint32_t v = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+    const uint32_t have = L_k - x;
+    if (have < 32) v &= (1u << have) - 1u;
+    return v;
+  };
+  auto put = [&](uint32_t w, uint32_t v) {
+    if (4 * w + 4 <= total_bytes) {
+      out32[w] = v;
+    } else {
+      for (uint32_t c = 0; 4 * w + c < total_bytes; ++c) out8[4 * w + c] = (uint8_t)(v >> (8 * c));
+    }
+  };
+  // words whose first bit lies in this segment
+  const uint32_t w_begin = (o_k + 31) >> 5, w_end = (o_n + 31) >> 5;
+  for (uint32_t w = w_begin + threadIdx.x; w < w_end; w += blockDim.x) {
+    uint32_t v = seg_bits32(32 * w - o_k);
+    if (!last && 32 * w + 32 > o_n) v |= nxt[0] << (o_n - 32 * w);  // (the next segment is >= 1024 bits)
+    put(w, v);
+  }
+  // the word holding o_1: segment 0's bits below it, segment 1's above
+  if (k == 1 && (o_k & 31u) && threadIdx.x == 0) {
+    const uint32_t w = o_k >> 5, sh = o_k & 31u;
+    const uint32_t have = 4 * w < total_bytes ? min(4u, total_bytes - 4 * w) : 0u;
+    uint32_t old = 0;
+    for (uint32_t c = 0; c < 4; ++c)
+      if (8 * c < sh) old |= (uint32_t)out8[4 * w + c] << (8 * c);
+    old &= (1u << sh) - 1u;
+    uint32_t v = old | (src[0] << sh);
+    if (nseg == 2 && o_n < 32 * w + 32 && L_k < 32 - sh) v &= (1u << (sh + L_k)) - 1u;
+    for (uint32_t c = 0; c < have; ++c) out8[4 * w + c] = (uint8_t)(v >> (8 * c));
+  }
+  if (last && threadIdx.x == 0) {
+    p.out_bytes[b] = total_bytes;
+    p.status[b] = RPP_OK;
+  }
 }
 
 // Host-side kernel choice: SPL 16 for bs > 64 (8 sub-blocks of 128 per
@@ -673,6 +798,48 @@ EncKernel enc_kernel_for(uint32_t bs) {
   if (m <= 2) return rpp_encode_kernel<8, 2, CS, SH>;
   if (m <= 4) return rpp_encode_kernel<8, 4, CS, SH>;
   return rpp_encode_kernel<8, 8, CS, SH>;
+}
+
+EncKernel enc_kernel(const rpp_config* cfg) {
+  const bool sh = cfg->unused_lsb_count != 0;
+  return cfg->component_stream_count == 1
+             ? (sh ? enc_kernel_for<1, true>(cfg->block_size) : enc_kernel_for<1, false>(cfg->block_size))
+             : (sh ? enc_kernel_for<2, true>(cfg->block_size) : enc_kernel_for<2, false>(cfg->block_size));
+}
+
+// rpp_encode_batch_ws workspace: unit counts and bases, the unit -> stream
+// map, per-unit bit counts and offsets, and one worst-case scratch slot per
+// segment after a stream's first
+struct EncWorkspace {
+  uint64_t* units;     // [B + 1]
+  uint64_t* seg_base;  // [B + 1]
+  uint32_t* seg_map;   // [max_units]
+  uint64_t* seg_bits;  // [max_units]
+  uint64_t* seg_off;   // [max_units]
+  uint8_t* scratch;    // [(max_units - B) * slot_bytes]
+  uint64_t slot_bytes, max_units, bytes;
+};
+
+EncWorkspace enc_layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks, uint8_t* base) {
+  const uint64_t B = nblocks;
+  const uint64_t seg_samples = (uint64_t)kEncSegChunks * cfg->block_size * cfg->component_stream_count;
+  EncWorkspace w{};
+  w.max_units = B + total_samples / seg_samples;
+  w.slot_bytes = (rpp_worst_case_bytes(cfg, seg_samples) + 16 + 15) & ~uint64_t{15};
+  uint64_t off = 0;
+  auto take = [&](uint64_t bytes) {
+    uint8_t* q = base ? base + off : nullptr;
+    off = (off + bytes + 255) & ~uint64_t{255};
+    return q;
+  };
+  w.units = reinterpret_cast<uint64_t*>(take((B + 1) * 8));
+  w.seg_base = reinterpret_cast<uint64_t*>(take((B + 1) * 8));
+  w.seg_map = reinterpret_cast<uint32_t*>(take(w.max_units * 4));
+  w.seg_bits = reinterpret_cast<uint64_t*>(take(w.max_units * 8));
+  w.seg_off = reinterpret_cast<uint64_t*>(take(w.max_units * 8));
+  w.scratch = take((w.max_units - B) * w.slot_bytes);
+  w.bytes = off;
+  return w;
 }
 
 // ===========================================================================
@@ -2003,12 +2170,43 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
     return RPP_INVALID_ARGUMENT;
   EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count};
-  const bool sh = cfg->unused_lsb_count != 0;
-  const EncKernel k = cfg->component_stream_count == 1
-                          ? (sh ? enc_kernel_for<1, true>(cfg->block_size) : enc_kernel_for<1, false>(cfg->block_size))
-                          : (sh ? enc_kernel_for<2, true>(cfg->block_size) : enc_kernel_for<2, false>(cfg->block_size));
-  hipLaunchKernelGGL(k, dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
+              cfg->unused_lsb_count, nullptr, nullptr, nullptr, nullptr, 0};
+  hipLaunchKernelGGL(enc_kernel(cfg), dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
+uint64_t rpp_encode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks) {
+  if (rpp_check_config(cfg) != RPP_OK) return 0;
+  return enc_layout(cfg, total_samples, nblocks, nullptr).bytes;
+}
+
+int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint64_t* d_in_offsets,
+                        const uint64_t* d_n_samples, uint32_t nblocks, uint8_t* d_out, const uint64_t* d_out_offsets,
+                        uint64_t* d_out_bytes, int32_t* d_status, uint64_t total_samples, void* d_workspace,
+                        uint64_t workspace_bytes, void* stream) {
+  int st = rpp_check_config(cfg);
+  if (st != RPP_OK) return st;
+  if (nblocks == 0) return RPP_OK;
+  if (!d_in || !d_in_offsets || !d_n_samples || !d_out || !d_out_offsets || !d_out_bytes || !d_status)
+    return RPP_INVALID_ARGUMENT;
+  const EncWorkspace w = enc_layout(cfg, total_samples, nblocks, static_cast<uint8_t*>(d_workspace));
+  if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t chunk_len = cfg->block_size * cfg->component_stream_count;
+  hipLaunchKernelGGL(rpp_enc_units_kernel, dim3((nblocks + 256) / 256), dim3(256), 0, s, d_n_samples, nblocks,
+                     chunk_len, w.units);
+  if ((st = rpp_exclusive_scan_u64(w.units, (uint64_t)nblocks + 1, w.seg_base, s)) != RPP_OK) return st;
+  hipLaunchKernelGGL(rpp_enc_unit_map_kernel, dim3((nblocks + 255) / 256), dim3(256), 0, s, w.seg_base, nblocks,
+                     w.seg_map);
+  EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
+              cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
+              cfg->unused_lsb_count, w.seg_map, w.seg_base, w.seg_bits, w.scratch, w.slot_bytes};
+  hipLaunchKernelGGL(enc_kernel(cfg), dim3((uint32_t)w.max_units), dim3(kWave), 0, s, p);
+  if (w.max_units > nblocks) {  // streams long enough to be split: place the segments
+    if ((st = rpp_exclusive_scan_u64(w.seg_bits, w.max_units, w.seg_off, s)) != RPP_OK) return st;
+    hipLaunchKernelGGL(rpp_enc_concat_kernel, dim3((uint32_t)w.max_units), dim3(256), 0, s, p,
+                       (const uint64_t*)w.seg_off);
+  }
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 

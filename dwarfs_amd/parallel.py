@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native as N
-from .codec import CodecConfig, _check, _raise_status, decode_workspace
+from .codec import CodecConfig, _check, _raise_status, decode_workspace, encode_workspace
 
 
 def partition_blocks(block_bytes: Sequence[int], world: int) -> List[Tuple[int, int]]:
@@ -154,6 +154,7 @@ class ShardPipeline:
         self.dec_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
         self.total_samples = int(n_samples.sum())
         self.workspace = decode_workspace(config, self.total_samples, self.nblocks, dev)
+        self.enc_workspace = encode_workspace(config, self.total_samples, self.nblocks, dev)
         self.all_sizes: Optional[torch.Tensor] = None
         self.image_offsets: Optional[torch.Tensor] = None
         self.size_gather = SizeGather(self.nblocks, dev, group)
@@ -168,11 +169,12 @@ class ShardPipeline:
         return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def encode(self) -> None:
-        _raise_status(N.lib().rpp_encode_batch(
+        _raise_status(N.lib().rpp_encode_batch_ws(
             C.byref(self.cfg), C.c_void_p(self.samples.data_ptr()), C.c_void_p(self.d_in_off.data_ptr()),
             C.c_void_p(self.d_n.data_ptr()), self.nblocks, C.c_void_p(self.data.data_ptr()),
             C.c_void_p(self.d_out_off.data_ptr()), C.c_void_p(self.sizes.data_ptr()),
-            C.c_void_p(self.enc_status.data_ptr()), self._stream()))
+            C.c_void_p(self.enc_status.data_ptr()), self.total_samples, C.c_void_p(self.enc_workspace.data_ptr()),
+            self.enc_workspace.numel(), self._stream()))
 
     def decode(self) -> None:
         _raise_status(N.lib().rpp_decode_batch_ws(

@@ -405,3 +405,29 @@ def test_decode_streams_at_any_byte_offset(two_stage):
             blocks = [datagen.poisson_data(rng, int(n) // cs * cs) for n in rng.integers(0, 40000, 9)]
             blocks += [datagen.benchmark_data(rng, 3000 // cs * cs), datagen.full_range_data(rng, 1000 // cs * cs)]
             _decode_oracle_streams(codec.CodecConfig(bs, cs, "big", 0), blocks, ragged=True)
+
+
+@pytest.mark.parametrize("bs,cs", [(128, 1), (16, 1), (32, 2), (13, 2), (512, 1)])
+def test_segmented_encode_of_long_streams(bs, cs):
+    """rpp_encode_batch_ws splits streams of more than 256 chunks into segments encoded by separate waves
+    and then places their bits; the result must be the oracle's stream byte for byte, at every segment
+    count and tail shape: exactly 256 chunks (one segment), 257 (a one-chunk last segment), a ragged
+    last chunk, a last segment of a single sample, and data that makes raw / zero / Rice sub-blocks."""
+    rng = np.random.default_rng(bs * 10 + cs)
+    seg = 256 * bs * cs
+    sizes = [seg, seg + bs * cs, seg + cs, 2 * seg + 5 * cs, 3 * seg - cs, 5 * seg + 7 * cs]
+    blocks = []
+    for i, n in enumerate(sizes):
+        kind = i % 4
+        if kind == 0:
+            blocks.append(datagen.poisson_data(rng, n))
+        elif kind == 1:
+            blocks.append(datagen.mixed_data(rng, n))
+        elif kind == 2:
+            blocks.append(datagen.full_range_data(rng, n))
+        else:
+            blocks.append(datagen.benchmark_data(rng, n))
+    blocks.append(datagen.constant_data(2 * seg + cs))
+    run_batch(codec.CodecConfig(bs, cs, "big", 0), blocks)
+    run_batch(codec.CodecConfig(bs, cs, "little", 2), [datagen.poisson_data(rng, 2 * seg + 3 * cs, lam=300,
+                                                                             ulsb=2, big_endian=False)])
