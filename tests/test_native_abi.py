@@ -130,3 +130,13 @@ def test_plugin_callsites_compile_against_facade():
     r = subprocess.run(["g++", "-std=c++20", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I", str(ROOT / "include"),
                         str(ROOT / "tests" / "cpp" / "plugin_callsites.cpp")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_host_code_under_asan_ubsan():
+    """SURVEY.md section 5 (reference CMakeLists.txt:67-69 sanitizer builds): the DwarFS frame parser of the
+    product library and the CPU oracle under AddressSanitizer + UBSan, fed hostile headers and streams."""
+    r = subprocess.run(["bash", str(ROOT / "tests" / "cpp" / "build_sanitize.sh")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run([str(ROOT / "tests" / "cpp" / "build" / "fuzz_host"), "200000"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "fuzz_host: OK" in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])
