@@ -178,21 +178,25 @@ def encode_batch(
     sizes = torch.empty(nb, dtype=torch.int64, device=dev)
     status = torch.empty(nb, dtype=torch.int32, device=dev)
     total_samples = int(n_samples.sum()) if nb else 0
-    ws = encode_workspace(config, total_samples, nb, dev, stream)
+    max_samples = int(n_samples.max()) if nb else 0
+    ws = encode_workspace(config, total_samples, max_samples, nb, dev, stream)
     st = N.lib().rpp_encode_batch_ws(
         C.byref(c), C.c_void_p(samples.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
         C.c_void_p(d_n.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),
-        C.c_void_p(sizes.data_ptr()), C.c_void_p(status.data_ptr()), total_samples, C.c_void_p(ws.data_ptr()),
-        ws.numel(), _stream_ptr(stream))
+        C.c_void_p(sizes.data_ptr()), C.c_void_p(status.data_ptr()), total_samples, max_samples,
+        C.c_void_p(ws.data_ptr()), ws.numel(), _stream_ptr(stream))
     _raise_status(st)
     return EncodedBatch(out, np.asarray(out_offsets, np.int64), d_out_off, sizes, status)
 
 
-def encode_workspace(config: CodecConfig, total_samples: int, nblocks: int, device, stream=None) -> torch.Tensor:
+def encode_workspace(config: CodecConfig, total_samples: int, max_stream_samples: int, nblocks: int, device,
+                     stream=None) -> torch.Tensor:
     """Device workspace of ``rpp_encode_batch_ws`` (segment table and scratch for streams encoded by
-    several waves) for ``nblocks`` streams of ``total_samples`` samples."""
+    several waves) for ``nblocks`` streams of ``total_samples`` samples, none longer than
+    ``max_stream_samples``."""
     c = _check(config)
-    nbytes = int(N.lib().rpp_encode_workspace_bytes(C.byref(c), int(total_samples), int(nblocks)))
+    nbytes = int(N.lib().rpp_encode_workspace_bytes(C.byref(c), int(total_samples), int(max_stream_samples),
+                                                    int(nblocks)))
     ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
     if stream is not None:
         ws.record_stream(stream)

@@ -800,6 +800,11 @@ EncKernel enc_kernel_for(uint32_t bs) {
   return rpp_encode_kernel<8, 8, CS, SH>;
 }
 
+// streams of more than kEncSegChunks chunks are split
+bool enc_segmented(const rpp_config* cfg, uint64_t max_stream_samples) {
+  return max_stream_samples > (uint64_t)kEncSegChunks * cfg->block_size * cfg->component_stream_count;
+}
+
 EncKernel enc_kernel(const rpp_config* cfg) {
   const bool sh = cfg->unused_lsb_count != 0;
   return cfg->component_stream_count == 1
@@ -2175,20 +2180,25 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
-uint64_t rpp_encode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks) {
+uint64_t rpp_encode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                                    uint32_t nblocks) {
   if (rpp_check_config(cfg) != RPP_OK) return 0;
+  if (!enc_segmented(cfg, max_stream_samples)) return 0;
   return enc_layout(cfg, total_samples, nblocks, nullptr).bytes;
 }
 
 int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_n_samples, uint32_t nblocks, uint8_t* d_out, const uint64_t* d_out_offsets,
-                        uint64_t* d_out_bytes, int32_t* d_status, uint64_t total_samples, void* d_workspace,
-                        uint64_t workspace_bytes, void* stream) {
+                        uint64_t* d_out_bytes, int32_t* d_status, uint64_t total_samples,
+                        uint64_t max_stream_samples, void* d_workspace, uint64_t workspace_bytes, void* stream) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
   if (nblocks == 0) return RPP_OK;
   if (!d_in || !d_in_offsets || !d_n_samples || !d_out || !d_out_offsets || !d_out_bytes || !d_status)
     return RPP_INVALID_ARGUMENT;
+  if (!enc_segmented(cfg, max_stream_samples))  // no stream to split: one wave per stream
+    return rpp_encode_batch(cfg, d_in, d_in_offsets, d_n_samples, nblocks, d_out, d_out_offsets, d_out_bytes,
+                            d_status, stream);
   const EncWorkspace w = enc_layout(cfg, total_samples, nblocks, static_cast<uint8_t*>(d_workspace));
   if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
   hipStream_t s = (hipStream_t)stream;

@@ -154,7 +154,8 @@ class ShardPipeline:
         self.dec_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
         self.total_samples = int(n_samples.sum())
         self.workspace = decode_workspace(config, self.total_samples, self.nblocks, dev)
-        self.enc_workspace = encode_workspace(config, self.total_samples, self.nblocks, dev)
+        self.max_samples = int(n_samples.max()) if self.nblocks else 0
+        self.enc_workspace = encode_workspace(config, self.total_samples, self.max_samples, self.nblocks, dev)
         self.all_sizes: Optional[torch.Tensor] = None
         self.image_offsets: Optional[torch.Tensor] = None
         self.size_gather = SizeGather(self.nblocks, dev, group)
@@ -173,7 +174,8 @@ class ShardPipeline:
             C.byref(self.cfg), C.c_void_p(self.samples.data_ptr()), C.c_void_p(self.d_in_off.data_ptr()),
             C.c_void_p(self.d_n.data_ptr()), self.nblocks, C.c_void_p(self.data.data_ptr()),
             C.c_void_p(self.d_out_off.data_ptr()), C.c_void_p(self.sizes.data_ptr()),
-            C.c_void_p(self.enc_status.data_ptr()), self.total_samples, C.c_void_p(self.enc_workspace.data_ptr()),
+            C.c_void_p(self.enc_status.data_ptr()), self.total_samples, self.max_samples,
+            C.c_void_p(self.enc_workspace.data_ptr()),
             self.enc_workspace.numel(), self._stream()))
 
     def decode(self) -> None:

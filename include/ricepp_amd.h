@@ -101,23 +101,28 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
 
 /*
  * Device workspace rpp_encode_batch_ws needs for `nblocks` streams holding
- * `total_samples` samples in all (0 for an unsupported config).
+ * `total_samples` samples in all, none longer than `max_stream_samples`
+ * (0: no workspace needed; also for an unsupported config).
  */
-uint64_t rpp_encode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks);
+uint64_t rpp_encode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                                    uint32_t nblocks);
 
 /*
  * rpp_encode_batch with a caller-owned device workspace of at least
- * rpp_encode_workspace_bytes(cfg, total_samples, nblocks) bytes
- * (total_samples >= the sum of d_n_samples).  Streams longer than 256 chunks
- * of cs * bs samples are encoded by several waves in parallel (a segment per
- * 256 chunks, then the segments' bits are placed at their offsets), so a
- * 16 MiB DwarFS block no longer encodes at one wave's speed.  Same output as
- * rpp_encode_batch, byte for byte.  Fully asynchronous on `stream`.
+ * rpp_encode_workspace_bytes(cfg, total_samples, max_stream_samples, nblocks)
+ * bytes (total_samples >= the sum and max_stream_samples >= the maximum of
+ * d_n_samples).  Streams longer than 256 chunks of cs * bs samples are encoded
+ * by several waves in parallel (a segment per 256 chunks, then the segments'
+ * bits are placed at their offsets), so a 16 MiB DwarFS block no longer
+ * encodes at one wave's speed; a batch without such streams is exactly
+ * rpp_encode_batch.  Same output as rpp_encode_batch, byte for byte.  Fully
+ * asynchronous on `stream`.
  */
 int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_n_samples, uint32_t nblocks, uint8_t* d_out,
                         const uint64_t* d_out_offsets, uint64_t* d_out_bytes, int32_t* d_status,
-                        uint64_t total_samples, void* d_workspace, uint64_t workspace_bytes, void* stream);
+                        uint64_t total_samples, uint64_t max_stream_samples, void* d_workspace,
+                        uint64_t workspace_bytes, void* stream);
 
 /*
  * Decode `nblocks` independent ricepp streams.
