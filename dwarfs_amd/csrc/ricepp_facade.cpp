@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cctype>
 #include <charconv>
@@ -94,6 +95,7 @@ class device_ctx {
   int device() const { return dev_; }
   hipStream_t stream() const { return stream_; }
   uint8_t* dev(size_t bytes) { return grow(dbuf_, dcap_, bytes, false); }
+  uint8_t* workspace(size_t bytes) { return grow(wbuf_, wcap_, bytes, false); }
   uint8_t* pin_in(size_t bytes) { return grow(hin_, hin_cap_, bytes, true); }
   uint8_t* pin_out(size_t bytes) { return grow(hout_, hout_cap_, bytes, true); }
   void sync() { hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
@@ -122,6 +124,8 @@ class device_ctx {
   hipStream_t stream_ = nullptr;
   uint8_t* dbuf_ = nullptr;
   size_t dcap_ = 0;
+  uint8_t* wbuf_ = nullptr;
+  size_t wcap_ = 0;
   uint8_t* hin_ = nullptr;
   size_t hin_cap_ = 0;
   uint8_t* hout_ = nullptr;
@@ -206,7 +210,7 @@ struct request {
 
 constexpr size_t kMaxBatchBlocks = 8192;
 constexpr size_t kMaxBatchBytes = size_t{512} << 20;  // input bytes per launch
-constexpr int kMaxActive = 2;                         // launches in flight per queue
+constexpr int kMaxActive = 4;                         // launches in flight per queue
 
 class batch_queue {
  public:
@@ -358,8 +362,17 @@ class batch_queue {
     hipStream_t s = ctx.stream();
     if (in_total) hip_check(hipMemcpyAsync(d, pin, in_total, hipMemcpyHostToDevice, s), "H2D encode input");
     hip_check(hipMemcpyAsync(d64, h64, 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode params");
-    int st = rpp_encode_batch(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
-                              d + in_total, d64 + 2 * nb, d64 + 3 * nb, dst, s);
+    // long blocks (16 MiB DwarFS blocks) are encoded by several waves
+    uint64_t total_samples = 0, max_samples = 0;
+    for (request* q : b) {
+      total_samples += q->n_samples;
+      max_samples = std::max<uint64_t>(max_samples, q->n_samples);
+    }
+    const uint64_t ws_bytes = rpp_encode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
+    uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
+    int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
+                                 d + in_total, d64 + 2 * nb, d64 + 3 * nb, dst, total_samples, max_samples, ws,
+                                 ws_bytes, s);
     if (st != RPP_OK) throw_status(st);
     st = rpp_pack_batch(d + in_total, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb),
                         d + in_total + out_total, d64 + 4 * nb, d64 + 5 * nb, s);
