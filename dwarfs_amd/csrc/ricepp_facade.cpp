@@ -18,6 +18,7 @@
 #include <charconv>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -186,8 +187,9 @@ class ctx_lease {
 enum req_state { QUEUED, TAKEN, ASSIGNED, STAGED, RESULT, DONE };
 
 struct batch_counts {
-  size_t to_stage = 0;  // requests not yet STAGED
+  size_t to_stage = 0;   // requests not yet STAGED
   size_t to_finish = 0;  // requests not yet DONE
+  std::condition_variable cv;  // the leader waits here
 };
 
 struct request {
@@ -206,6 +208,7 @@ struct request {
   std::string error;  // HIP failure text
   req_state state = QUEUED;
   batch_counts* counts = nullptr;
+  std::condition_variable cv;  // its caller waits here (woken individually: no notify_all storms)
 };
 
 constexpr size_t kMaxBatchBlocks = 8192;
@@ -232,7 +235,7 @@ class batch_queue {
           break;
         default: break;
       }
-      cv_.wait(lk);
+      r.cv.wait(lk);
     }
   }
 
@@ -242,7 +245,7 @@ class batch_queue {
     if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
     lk.lock();
     r.state = STAGED;
-    if (--r.counts->to_stage == 0) cv_.notify_all();
+    if (--r.counts->to_stage == 0) r.counts->cv.notify_one();
   }
   void copy_out(std::unique_lock<std::mutex>& lk, request& r) {
     lk.unlock();
@@ -250,7 +253,7 @@ class batch_queue {
     lk.lock();
     r.state = DONE;
     batch_counts* c = r.counts;  // (r may be gone once DONE is seen)
-    if (--c->to_finish == 0) cv_.notify_all();
+    if (--c->to_finish == 0) c->cv.notify_one();
   }
 
   // Takes a batch from the queue and drives it (lk held on entry and exit).
@@ -261,23 +264,24 @@ class batch_queue {
     while (!pending_.empty() && b.size() < kMaxBatchBlocks &&
            (b.empty() || bytes + pending_.front()->in_bytes <= kMaxBatchBytes)) {
       request* q = pending_.front();
-      pending_.erase(pending_.begin());
+      pending_.pop_front();
       bytes += q->in_bytes;
       q->state = TAKEN;
       b.push_back(q);
     }
-    batch_counts counts{b.size(), b.size()};
+    batch_counts counts;
+    counts.to_stage = counts.to_finish = b.size();
     for (request* q : b) q->counts = &counts;
     ++active_;
+    // another caller may lead the next batch meanwhile
+    if (!pending_.empty() && active_ < kMaxActive) pending_.front()->cv.notify_one();
     lk.unlock();
     {
       ctx_lease ctx{dev_};
-      bool published = false;
       try {
         device_guard g{dev_};
         if (encode_) launch_encode(lk, b, self, *ctx.operator->());
         else launch_decode(lk, b, self, *ctx.operator->());
-        published = true;
       } catch (std::exception const& e) {
         lk.lock();
         // requests still waiting for their slot: nothing to copy in
@@ -286,28 +290,26 @@ class batch_queue {
             q->state = STAGED;
             --counts.to_stage;
           }
-        // wait for callers copying in, then report the error to everyone
-        cv_.wait(lk, [&] { return counts.to_stage == 0; });
+        counts.cv.wait(lk, [&] { return counts.to_stage == 0; });
         for (request* q : b) {
           q->status = RPP_HIP_ERROR;
           q->error = e.what();
           q->result_bytes = 0;
           q->state = RESULT;
+          q->cv.notify_one();
         }
-        cv_.notify_all();
         lk.unlock();
       }
-      (void)published;
       lk.lock();
       // the leader copies its own result out, then waits for the others
       // before the staging buffers go back to the pool
       if (self.state == RESULT && self.counts == &counts) copy_out(lk, self);
-      cv_.wait(lk, [&] { return counts.to_finish == 0; });
+      counts.cv.wait(lk, [&] { return counts.to_finish == 0; });
       lk.unlock();
     }
     lk.lock();
     --active_;
-    cv_.notify_all();
+    if (!pending_.empty()) pending_.front()->cv.notify_one();  // the next leader
   }
 
   // Hands out the pinned input slots and waits until every caller copied in
@@ -318,19 +320,21 @@ class batch_queue {
     for (size_t i = 0; i < b.size(); ++i) {
       b[i]->pin_in = pin + off[i];
       b[i]->state = ASSIGNED;
+      if (b[i] != &self) b[i]->cv.notify_one();
     }
-    cv_.notify_all();
-    if (self.state == ASSIGNED && self.counts == b.front()->counts) copy_in(lk, self);
     batch_counts* c = b.front()->counts;
-    cv_.wait(lk, [&] { return c->to_stage == 0; });
+    if (self.state == ASSIGNED && self.counts == c) copy_in(lk, self);
+    c->cv.wait(lk, [&] { return c->to_stage == 0; });
     lk.unlock();
   }
 
   // Publishes the results (lk not held on entry or exit).
   void publish(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b) {
     lk.lock();
-    for (request* q : b) q->state = RESULT;
-    cv_.notify_all();
+    for (request* q : b) {
+      q->state = RESULT;
+      q->cv.notify_one();
+    }
     lk.unlock();
   }
 
@@ -447,8 +451,7 @@ class batch_queue {
   rpp_config cfg_;
   bool encode_;
   std::mutex mu_;
-  std::condition_variable cv_;
-  std::vector<request*> pending_;
+  std::deque<request*> pending_;
   int active_ = 0;
 };
 
