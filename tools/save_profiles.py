@@ -17,7 +17,12 @@ dst.mkdir(exist_ok=True)
 shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / f"{tag}_bench_kernel_stats.csv")
 shutil.copy(src / "pmc_summary.txt", dst / f"{tag}_pmc_summary.txt")
 pmc = json.loads((src / "pmc_summary.json").read_text())
-latest = {"source": f"profiles/{tag}_pmc_summary.txt", "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+sys.path.insert(0, str(ROOT))
+from bench import kernel_source_sha256  # noqa: E402
+
+latest = {"source": f"profiles/{tag}_pmc_summary.txt", "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024",
+          # the HIP sources the counters were taken of: bench.py reports `traffic` only while they match
+          "kernel_source_sha256": kernel_source_sha256()}
 for k, v in pmc.items():
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         latest[k] = {"hbm_bytes_per_launch": int((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024),
