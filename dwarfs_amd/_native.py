@@ -115,10 +115,10 @@ def lib() -> C.CDLL:
         L.rpp_encode_batch_ws.restype = C.c_int
         L.rpp_decode_batch.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, P]
         L.rpp_decode_batch.restype = C.c_int
-        L.rpp_decode_workspace_bytes.argtypes = [C.POINTER(RppConfig), C.c_uint64, C.c_uint32]
+        L.rpp_decode_workspace_bytes.argtypes = [C.POINTER(RppConfig), C.c_uint64, C.c_uint64, C.c_uint32]
         L.rpp_decode_workspace_bytes.restype = C.c_uint64
-        L.rpp_decode_batch_ws.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, C.c_uint64, P,
-                                          C.c_uint64, P]
+        L.rpp_decode_batch_ws.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, C.c_uint64,
+                                          C.c_uint64, P, C.c_uint64, P]
         L.rpp_decode_batch_ws.restype = C.c_int
         L.rpp_unused_lsb_batch.argtypes = [P, P, P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P]
         L.rpp_unused_lsb_batch.restype = C.c_int

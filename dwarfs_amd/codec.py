@@ -237,23 +237,36 @@ def decode_batch(
     d_out_off = _dev_u64(out_offsets, dev)
     status = torch.empty(nb, dtype=torch.int32, device=dev)
     total = int(n_samples.sum()) if nb else 0
-    ws = decode_workspace(config, total, nb, dev)
+    longest = int(n_samples.max()) if nb else 0
+    ws = decode_workspace(config, total, nb, dev, longest)
     if stream is not None:
         ws.record_stream(stream)
     st = N.lib().rpp_decode_batch_ws(
         C.byref(c), C.c_void_p(data.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
         C.c_void_p(d_in_bytes.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),
-        C.c_void_p(d_n.data_ptr()), C.c_void_p(status.data_ptr()), total, C.c_void_p(ws.data_ptr()), ws.numel(),
-        _stream_ptr(stream))
+        C.c_void_p(d_n.data_ptr()), C.c_void_p(status.data_ptr()), total, longest, C.c_void_p(ws.data_ptr()),
+        ws.numel(), _stream_ptr(stream))
     _raise_status(st)
     return out, status
 
 
-def decode_workspace(config: CodecConfig, total_samples: int, nblocks: int, device) -> torch.Tensor:
-    """Device workspace of ``rpp_decode_batch_ws`` (sub-block start positions, tile scan state) for a
-    batch of ``nblocks`` streams of ``total_samples`` samples."""
+def segmented_decode_stats(reset: bool = True) -> dict:
+    """Counters of the segmented decode since the last reset (diagnostics): units whose guessed chain met
+    the exact one at once, reruns from a known header, serial passes, streams left to the fused kernel, and
+    failed units that had found no guess at all."""
+    buf = (C.c_ulonglong * 8)()
+    _raise_status(N.lib().rpp_seg_diag_read(buf, int(reset)))
+    return dict(zip(("met", "reruns", "serial", "fallback", "no_guess"), map(int, buf)))
+
+
+def decode_workspace(config: CodecConfig, total_samples: int, nblocks: int, device,
+                     max_stream_samples: Optional[int] = None) -> torch.Tensor:
+    """Device workspace of ``rpp_decode_batch_ws`` for a batch of ``nblocks`` streams of ``total_samples``
+    samples, the longest ``max_stream_samples`` (default: ``total_samples``, i.e. sized for the segmented
+    decode of long streams whenever the batch could need it)."""
     c = _check(config)
-    nbytes = int(N.lib().rpp_decode_workspace_bytes(C.byref(c), int(total_samples), int(nblocks)))
+    mx = int(total_samples if max_stream_samples is None else max_stream_samples)
+    nbytes = int(N.lib().rpp_decode_workspace_bytes(C.byref(c), int(total_samples), mx, int(nblocks)))
     return torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
 
 

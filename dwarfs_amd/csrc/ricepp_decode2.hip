@@ -57,22 +57,42 @@ struct Workspace {
   uint32_t* tile_map;   // [max_tiles]
   uint32_t* sb_pos;     // [max_sb + B]
   uint32_t* counter;    // [1]
+  // segmented decode (L != 0)
+  uint64_t* ucnt;       // [B + 1] units per stream
+  uint64_t* unit_base;  // [B + 1]
+  uint32_t* unit_map;   // [U_max]
+  uint64_t* bm_cnt;     // [U_max + 1] bitmap words per unit
+  uint64_t* bm_base;    // [U_max + 1]
+  uint32_t* bitmap;     // [bm_words]
+  uint32_t* ovr;        // [U_max * kSegOvr]
+  uint32_t* ustate;     // [U_max * 4]
+  uint32_t* ulo;        // [U_max]
+  uint32_t* uov;        // [U_max]
+  uint32_t* uhit;       // [U_max]
+  uint32_t* sst;        // [B]
+  uint32_t* sflags;     // [B]
+  uint64_t* cnt2;       // [U_max + 1] exact positions per unit
+  uint64_t* off2;       // [U_max + 1]
   uint64_t bytes;
   uint64_t max_tiles;
+  uint64_t units_max;
 };
 
-uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+__host__ __device__ inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
 // diagnostics (RICEPP_DEC2_DBG & 4): per-phase cycle sums of the extraction
 // tiles (wave 0 of each workgroup), read by rpp_diag_read
 __device__ unsigned long long g_dec2_diag[8];
+// segmented decode counters (rpp_seg_diag_read): units that met the exact
+// chain at once, reruns requested, serial passes, streams left to the fused kernel
+__device__ unsigned long long g_seg_diag[8];
 __device__ __forceinline__ uint64_t clk() {
   uint64_t t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
 
-Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks, uint8_t* base) {
+Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks, uint32_t L, uint8_t* base) {
   const uint64_t B = nblocks;
   const uint64_t max_sb = total_samples / cfg->block_size + B * cfg->component_stream_count;
   const uint64_t max_tiles = max_sb / kTile + B;
@@ -91,8 +111,30 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks
   w.tile_map = reinterpret_cast<uint32_t*>(take(max_tiles * 4));
   w.sb_pos = reinterpret_cast<uint32_t*>(take((max_sb + B) * 4));
   w.counter = reinterpret_cast<uint32_t*>(take(256));
-  w.bytes = off;
   w.max_tiles = max_tiles;
+  if (L) {
+    // header bits of all streams: at most their worst-case sizes (seg_last_bit)
+    const uint64_t bits = 8 * rpp_worst_case_bytes(cfg, total_samples) + 128 * B;
+    const uint64_t U = B + (bits >> L) + 1;
+    const uint64_t words = (bits >> 5) + 8 * U;
+    w.units_max = U;
+    w.ucnt = reinterpret_cast<uint64_t*>(take((B + 1) * 8));
+    w.unit_base = reinterpret_cast<uint64_t*>(take((B + 1) * 8));
+    w.unit_map = reinterpret_cast<uint32_t*>(take(U * 4));
+    w.bm_cnt = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
+    w.bm_base = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
+    w.bitmap = reinterpret_cast<uint32_t*>(take(words * 4));
+    w.ovr = reinterpret_cast<uint32_t*>(take(U * rpp_internal::kSegOvr * 4));
+    w.ustate = reinterpret_cast<uint32_t*>(take(U * 16));
+    w.ulo = reinterpret_cast<uint32_t*>(take(U * 4));
+    w.uov = reinterpret_cast<uint32_t*>(take(U * 4));
+    w.uhit = reinterpret_cast<uint32_t*>(take(U * 4));
+    w.sst = reinterpret_cast<uint32_t*>(take(B * 4));
+    w.sflags = reinterpret_cast<uint32_t*>(take(B * 4));
+    w.cnt2 = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
+    w.off2 = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
+  }
+  w.bytes = off;
   return w;
 }
 
@@ -169,6 +211,10 @@ __device__ __forceinline__ uint32_t combine(uint32_t a, uint32_t b) {
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62;
 __device__ __forceinline__ uint64_t pack_state(uint32_t c0, uint32_t c1, uint64_t flag) {
   return flag | (uint64_t)(c0 & 0x1FFFFu) | ((uint64_t)(c1 & 0x1FFFFu) << 17);
+}
+
+__device__ __forceinline__ uint32_t readlane(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
 __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
@@ -392,9 +438,11 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
       scan_buf[tid] = v;
       __syncthreads();
     }
-    // ---- tile carry: decoupled look-back over the stream's earlier tiles ----
-    if (tid == 0) {
-      uint32_t a0 = scan_buf[kcount - CS], a1 = CS == 2 ? scan_buf[kcount - 1] : 0u;  // tile aggregates
+    // ---- tile carry: decoupled look-back over the stream's earlier tiles,
+    //      64 predecessors at a time (one per lane of wave 0): a long stream
+    //      has thousands of tiles in flight at once ----
+    if (tid < 64) {
+      const uint32_t a0 = scan_buf[kcount - CS], a1 = CS == 2 ? scan_buf[kcount - 1] : 0u;  // tile aggregates
       uint32_t e0, e1;  // exclusive prefix of this tile
       if (lt == 0) {
         // codec.h:81-86: the 16-bit initial value of each component
@@ -403,27 +451,43 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
         e0 = kSet | (uint32_t)(x & 0xFFFFu);
         e1 = kSet | (uint32_t)((x >> 16) & 0xFFFFu);
       } else {
-        __hip_atomic_store(&p.tile_state[t], pack_state(a0, a1, kFlagAgg), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t x0 = 0, x1 = 0;  // identity
-        for (uint32_t j = t - 1;; --j) {
-          uint64_t s;
-          do {
-            s = __hip_atomic_load(&p.tile_state[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (!(s >> 62)) __builtin_amdgcn_s_sleep(1);
-          } while (!(s >> 62));
-          const uint32_t s0 = (uint32_t)(s & 0x1FFFFu), s1 = (uint32_t)((s >> 17) & 0x1FFFFu);
-          x0 = combine(s0, x0);
-          x1 = combine(s1, x1);
-          if ((s >> 62) == 2) break;
+        if (tid == 0)
+          __hip_atomic_store(&p.tile_state[t], pack_state(a0, a1, kFlagAgg), __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t x0 = 0, x1 = 0;  // identity: the tiles after the current window
+        const uint32_t tfirst = t - lt;  // the stream's first tile (publishes its inclusive prefix)
+        for (uint32_t jt = t - 1;; jt -= 64) {
+          const bool valid = tid <= jt - tfirst;
+          uint64_t s = 0;
+          if (valid) {
+            do {
+              s = __hip_atomic_load(&p.tile_state[jt - tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+              if (!(s >> 62)) __builtin_amdgcn_s_sleep(1);
+            } while (!(s >> 62));
+          }
+          const uint64_t incl = __ballot(valid && (s >> 62) == 2);
+          const uint64_t vm = __ballot(valid);
+          const int k = incl ? __builtin_ctzll(incl) : 63 - __builtin_clzll(vm);
+          uint32_t y0 = 0, y1 = 0;  // the window, oldest tile (lane k) first
+          const uint32_t slo = (uint32_t)s, shi = (uint32_t)(s >> 32);
+          for (int l = k; l >= 0; --l) {
+            const uint64_t sl = ((uint64_t)readlane(shi, l) << 32) | readlane(slo, l);
+            y0 = combine(y0, (uint32_t)(sl & 0x1FFFFu));
+            y1 = combine(y1, (uint32_t)((sl >> 17) & 0x1FFFFu));
+          }
+          x0 = combine(y0, x0);
+          x1 = combine(y1, x1);
+          if (incl) break;
         }
         e0 = x0;
         e1 = x1;
       }
-      __hip_atomic_store(&p.tile_state[t], pack_state(combine(e0, a0), combine(e1, a1), kFlagIncl),
-                         __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      sh_carry[0] = e0;
-      sh_carry[1] = e1;
+      if (tid == 0) {
+        __hip_atomic_store(&p.tile_state[t], pack_state(combine(e0, a0), combine(e1, a1), kFlagIncl),
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        sh_carry[0] = e0;
+        sh_carry[1] = e1;
+      }
     }
     __syncthreads();
     // value before this lane's sub-block
@@ -479,6 +543,361 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
   }
 }
 
+// ===========================================================================
+// Segmented decode of long streams: units, stitch, positions, ragged tail
+// (the scheme: ricepp_internal.h; the parse of the units: rpp_parse_kernel
+// with SEG = true in ricepp_kernels.hip).
+// ===========================================================================
+using rpp_internal::kSegNone;
+using rpp_internal::kSegOvr;
+
+struct SegArgs {
+  rpp_internal::SegView sv;
+  const uint8_t* in;
+  const uint64_t* in_off;
+  const uint64_t* in_bytes;
+  const uint64_t* n_samples;
+  const uint64_t* sb_base;
+  uint32_t* sb_pos;
+  int32_t* status;
+  uint64_t* cnt;  // [U_max + 1] exact positions per unit
+  uint64_t* off;  // [U_max + 1] their exclusive scan
+  uint32_t* uhit; // [U_max] first overshoot header of the unit before that is a header of the unit
+  uint32_t nblocks, bs, cs;
+};
+
+__device__ __forceinline__ bool seg_stream_ok(uint64_t n, uint64_t nb, uint32_t cs) {
+  return n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES && nb < (UINT64_C(1) << 29);
+}
+
+// units of each stream: 1, or one per 2^L bits of its header range
+__global__ void rpp_seg_units_kernel(SegArgs a, uint64_t* ucnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > a.nblocks) return;
+  if (i == a.nblocks) {
+    ucnt[i] = 0;
+    return;
+  }
+  const uint64_t n = a.n_samples[i], nb = a.in_bytes[i];
+  uint64_t c = 1;
+  if (seg_stream_ok(n, nb, a.cs))
+    c = (rpp_internal::seg_last_bit((uint32_t)(a.in_off[i] & 3u), nb, n, a.bs, a.cs) >> a.sv.seg_log2) + 1;
+  ucnt[i] = c;
+}
+
+// unit -> stream, and the bitmap words of each unit of a split stream
+// (its region [j 2^L, min((j+1) 2^L, last bit + 1)), a multiple of 4 words)
+__global__ void rpp_seg_map_kernel(SegArgs a, uint32_t* unit_map, uint64_t* bm_cnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nblocks) return;
+  const uint64_t u0 = a.sv.unit_base[i], nu = a.sv.unit_base[i + 1] - u0;
+  const uint32_t L = a.sv.seg_log2;
+  uint32_t Eend = 0;
+  if (nu > 1)
+    Eend = rpp_internal::seg_last_bit((uint32_t)(a.in_off[i] & 3u), a.in_bytes[i], a.n_samples[i], a.bs, a.cs);
+  for (uint64_t k = 0; k < nu; ++k) {
+    unit_map[u0 + k] = i;
+    uint64_t words = 0;
+    if (nu > 1) {
+      const uint64_t S = k << L, E = k + 1 == nu ? (uint64_t)Eend + 1 : S + (1ull << L);
+      words = align_up((E - S + 31) / 32, 4);
+    }
+    bm_cnt[u0 + k] = words;
+  }
+}
+
+struct UnitGeo {
+  uint32_t b, u0, nu, S, E;
+};
+__device__ __forceinline__ UnitGeo unit_geo(const SegArgs& a, uint32_t u) {
+  UnitGeo g;
+  g.b = a.sv.unit_map[u];
+  g.u0 = (uint32_t)a.sv.unit_base[g.b];
+  g.nu = (uint32_t)a.sv.unit_base[g.b + 1] - g.u0;
+  const uint32_t j = u - g.u0, L = a.sv.seg_log2;
+  g.S = j << L;
+  g.E = g.S + (1u << L);
+  if (g.nu > 1 && j + 1 == g.nu)
+    g.E = rpp_internal::seg_last_bit((uint32_t)(a.in_off[g.b] & 3u), a.in_bytes[g.b], a.n_samples[g.b], a.bs, a.cs) + 1;
+  return g;
+}
+
+__device__ __forceinline__ bool bm_test(const SegArgs& a, uint32_t u, uint32_t S, uint32_t pos) {
+  const uint32_t* bm = a.sv.bitmap + a.sv.bm_base[u];
+  return (bm[(pos - S) >> 5] >> (pos & 31u)) & 1u;
+}
+
+// One thread per unit of a split stream (not yet resolved): the first of the
+// previous unit's overshoot headers that is also a header of this unit.
+__global__ void rpp_seg_hit_kernel(SegArgs a) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= a.sv.units_max || u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
+  const uint32_t b = a.sv.unit_map[u];
+  const uint32_t u0 = (uint32_t)a.sv.unit_base[b], nu = (uint32_t)a.sv.unit_base[b + 1] - u0;
+  const uint32_t j = u - u0;
+  if (nu <= 1 || j == 0 || j < a.sv.sst[b]) return;
+  const uint32_t L = a.sv.seg_log2, prev = u - 1;
+  const uint32_t S = j << L;
+  const uint32_t E = j + 1 == nu ? rpp_internal::seg_last_bit((uint32_t)(a.in_off[b] & 3u), a.in_bytes[b],
+                                                              a.n_samples[b], a.bs, a.cs) + 1
+                                 : S + (1u << L);
+  const uint32_t np = a.sv.ustate[4 * prev + rpp_internal::kUsNovr];
+  uint32_t hit = kSegNone;
+  for (uint32_t i = 0; i < np && hit == kSegNone; ++i) {
+    const uint32_t o = a.sv.ovr[kSegOvr * prev + i];
+    if (o >= S && o < E && bm_test(a, u, S, o)) hit = i;
+  }
+  a.uhit[u] = hit;
+}
+
+// One wave per split stream, 64 units at a time from the first unresolved
+// one: where does the exact chain (the previous unit's, by induction) meet
+// the unit's own chain?  At the previous unit's overshoot header uhit: from
+// there on the unit's positions are exact.  The first unit without a meeting
+// decides the rest: if the previous chain stopped early the stream ended
+// there; else the unit is parsed again from the last overshoot header (a
+// rerun pass) and the stitch resumes there next time.
+__global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
+  using namespace rpp_internal;
+  const uint32_t b = blockIdx.x, lane = threadIdx.x;
+  if (b >= a.nblocks) return;
+  const uint32_t u0 = (uint32_t)a.sv.unit_base[b], nu = (uint32_t)a.sv.unit_base[b + 1] - u0;
+  uint32_t j0 = a.sv.sst[b];
+  if (nu <= 1 || j0 >= nu) return;
+  if (j0 == 0) {
+    if (lane == 0) a.sv.ulo[u0] = a.sv.ustate[4 * u0 + kUsStart];
+    j0 = 1;
+  }
+  enum { kOk, kEnd, kFail };
+  for (; j0 < nu; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const bool in = j < nu;
+    const uint32_t u = u0 + j, prev = u - 1;
+    uint32_t cls = kOk, lo = 0, uovp = 0;
+    if (in) {
+      const uint32_t np = a.sv.ustate[4 * prev + kUsNovr];
+      const uint32_t h = a.uhit[u];
+      if (a.sv.ustate[4 * u + kUsFlags] & kUfRerunDone) {  // parsed from the previous unit's last overshoot header
+        lo = a.sv.ustate[4 * u + kUsStart];
+        uovp = kSegOvr - 1;
+      } else if (h != kSegNone) {
+        lo = a.sv.ovr[kSegOvr * prev + h];
+        uovp = h;
+      } else {
+        cls = np < kSegOvr ? kEnd : kFail;
+        uovp = np;
+      }
+    }
+    const uint64_t ev = __ballot(in && cls != kOk);
+    const uint32_t e = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
+    if (in && lane < e) {
+      a.sv.ulo[u] = lo;
+      a.sv.uov[prev] = uovp;
+    }
+    if (lane < e && in) atomicAdd(&g_seg_diag[0], 1ull);
+    if (e == 64) continue;
+    const uint32_t ce = __shfl((int)cls, (int)e);
+    if (ce == kFail) {
+      if (lane == e) {
+        a.sv.ustate[4 * u + kUsRerun] = a.sv.ovr[kSegOvr * prev + kSegOvr - 1];
+        a.sv.sst[b] = j;
+        atomicAdd(&g_seg_diag[a.sv.pass == 2 ? 2 : 1], 1ull);
+        if (a.sv.ustate[4 * u + kUsFlags] & kUfNoGuess) atomicAdd(&g_seg_diag[4], 1ull);
+      }
+      return;
+    }
+    // the chain ended before unit j0 + e: no later unit has exact positions
+    if (lane == e) a.sv.uov[prev] = uovp;
+    for (uint32_t k = j0 + e + lane; k < nu; k += 64) {
+      a.sv.ulo[u0 + k] = kSegNone;
+      if (k > j0 + e) a.sv.uov[u0 + k - 1] = 0;
+    }
+    break;
+  }
+  if (lane == 0) {
+    a.sv.uov[u0 + nu - 1] = 0;
+    a.sv.sst[b] = nu;
+  }
+}
+
+// exact positions of a unit in its bitmap: the words [wlo, whi), the first
+// masked below bit `lo`
+struct UnitSpan {
+  const uint32_t* bm;
+  uint32_t wlo, whi, lomask;
+};
+__device__ __forceinline__ UnitSpan unit_span(const SegArgs& a, uint32_t u, const UnitGeo& g, uint32_t lo) {
+  UnitSpan s{a.sv.bitmap + a.sv.bm_base[u], 0, 0, 0};
+  if (lo != kSegNone && lo < g.E) {
+    s.wlo = (lo - g.S) >> 5;
+    s.whi = (g.E - g.S + 31) >> 5;
+    s.lomask = ~0u << ((lo - g.S) & 31u);
+  }
+  return s;
+}
+
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* red) {
+  const uint32_t tid = threadIdx.x;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (uint32_t i = 0; i < blockDim.x / 64; ++i) t += red[i];
+  return t;
+}
+
+constexpr uint32_t kSegThreads = 256;
+
+// exact positions per unit of a split stream (0 for other units)
+__global__ __launch_bounds__(kSegThreads) void rpp_seg_count_kernel(SegArgs a) {
+  __shared__ uint32_t red[kSegThreads / 64];
+  const uint32_t u = blockIdx.x;
+  if (u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
+  const UnitGeo g = unit_geo(a, u);
+  if (g.nu <= 1) {
+    if (threadIdx.x == 0) a.cnt[u] = 0;
+    return;
+  }
+  const uint32_t lo = a.sv.ulo[u];
+  const UnitSpan sp = unit_span(a, u, g, lo);
+  uint32_t c = 0;
+  for (uint32_t w = sp.wlo + threadIdx.x; w < sp.whi; w += kSegThreads) {
+    uint32_t x = sp.bm[w];
+    if (w == sp.wlo) x &= sp.lomask;
+    c += __builtin_popcount(x);
+  }
+  c = block_sum_u32(c, red);
+  if (threadIdx.x == 0) a.cnt[u] = c + (lo != kSegNone ? a.sv.uov[u] : 0u);
+}
+
+// positions of each unit into the stream's sb_pos: the bitmap's set bits in
+// order (rounds of 4 consecutive words per thread, a block scan of their
+// counts per round), then its own overshoot entries; entries past the
+// stream's nsb + 1 are dropped
+__global__ __launch_bounds__(kSegThreads) void rpp_seg_write_kernel(SegArgs a) {
+  __shared__ uint32_t wsum[kSegThreads / 64];
+  const uint32_t u = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  if (u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
+  const UnitGeo g = unit_geo(a, u);
+  if (g.nu <= 1) return;
+  const uint32_t lo = a.sv.ulo[u];
+  if (lo == kSegNone) return;
+  const UnitSpan sp = unit_span(a, u, g, lo);
+  const uint64_t N = a.n_samples[g.b];
+  const uint32_t chunk_len = a.bs * a.cs;
+  const uint64_t cap = (N + chunk_len - 1) / chunk_len * a.cs + 1;
+  uint32_t* dst = a.sb_pos + a.sb_base[g.b];
+  const uint64_t idx0 = a.off[u] - a.off[g.u0];
+  const uint32_t nw = sp.whi - sp.wlo;
+  uint64_t run = idx0;
+  for (uint32_t r0 = 0; r0 < nw && run < cap; r0 += 4 * kSegThreads) {
+    uint32_t x[4], c = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t w = r0 + 4 * tid + q;
+      x[q] = w < nw ? sp.bm[sp.wlo + w] : 0u;
+      if (w == 0) x[q] &= sp.lomask;
+      c += __builtin_popcount(x[q]);
+    }
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t i = 0; i < kSegThreads / 64; ++i) {
+      before += i < wv ? wsum[i] : 0u;
+      total += wsum[i];
+    }
+    uint64_t idx = run + before + incl - c;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t w = r0 + 4 * tid + q;
+      uint32_t v = x[q];
+      while (v && idx < cap) {
+        dst[idx++] = g.S + 32u * (sp.wlo + w) + (uint32_t)__builtin_ctz(v);
+        v &= v - 1;
+      }
+    }
+    run += total;
+    __syncthreads();  // (wsum is reused)
+  }
+  const uint64_t bits_total = run - idx0;  // (all of them unless the cap cut the rounds short)
+  const uint32_t nov = a.sv.uov[u];
+  if (run < cap)
+    for (uint32_t i = tid; i < nov; i += kSegThreads) {
+      const uint64_t k = idx0 + bits_total + i;
+      if (k < cap) dst[k] = a.sv.ovr[kSegOvr * u + i];
+    }
+}
+
+// One sub-block of n samples from bit `pos` (decode.h:42-83, positions only);
+// false when it reads past the stream (the fused kernel's TRUNCATED cases).
+__device__ bool seg_parse_one(const uint8_t* in, uint32_t nbytes, uint32_t lim, uint32_t& pos, uint32_t n) {
+  auto peek = [&](uint32_t q) {
+    return __builtin_amdgcn_alignbit(stream_word(in, nbytes, (q >> 5) + 1), stream_word(in, nbytes, q >> 5), q & 31u);
+  };
+  if (pos + 4 > lim) return false;
+  const uint32_t h = peek(pos) & 15u;
+  pos += 4;
+  if (h == 0) return true;
+  if (h == 15) {
+    if ((uint64_t)pos + 16ull * n > lim) return false;
+    pos += 16 * n;
+    return true;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    for (;;) {
+      if (pos >= lim) return false;
+      const uint32_t x = peek(pos);
+      if (x) {
+        pos += ffbl(x) + 1;
+        break;
+      }
+      pos += 32;
+    }
+    pos += h - 1;
+  }
+  return pos <= lim;
+}
+
+// One thread per split stream: enough exact positions?  The ragged last
+// chunk (parsed by the units with bs samples) again with its own size; the
+// stream's status.
+__global__ void rpp_seg_tail_kernel(SegArgs a) {
+  using namespace rpp_internal;
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.nblocks) return;
+  const uint32_t u0 = (uint32_t)a.sv.unit_base[b], nu = (uint32_t)a.sv.unit_base[b + 1] - u0;
+  if (nu <= 1) return;
+  const uint64_t T = a.off[u0 + nu] - a.off[u0];
+  const uint32_t N = (uint32_t)a.n_samples[b], cs = a.cs, chunk_len = a.bs * cs;
+  const uint32_t nsb = (N + chunk_len - 1) / chunk_len * cs;
+  const uint32_t rag = N % chunk_len;
+  const uint64_t need = rag ? nsb - cs + 1 : nsb + 1;
+  int32_t st = RPP_OK;
+  if (T < need) {
+    st = (a.sv.sflags[b] & 1u) ? kSegFallback : RPP_TRUNCATED_INPUT;
+    if (st == kSegFallback) atomicAdd(&g_seg_diag[3], 1ull);
+  } else if (rag) {
+    const uint64_t ioff = a.in_off[b];
+    const uint32_t mis = (uint32_t)(ioff & 3u);
+    const uint32_t nbytes = (uint32_t)a.in_bytes[b] + mis;
+    uint32_t* dst = a.sb_pos + a.sb_base[b];
+    const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
+    uint32_t pos = dst[nsb - cs];
+    for (uint32_t c = 0; c < cs && st == RPP_OK; ++c) {
+      if (!seg_parse_one(a.in + (ioff - mis), nbytes, lim, pos, rag / cs)) st = RPP_TRUNCATED_INPUT;
+      else dst[nsb - cs + 1 + c] = pos;
+    }
+  }
+  a.status[b] = st;
+}
+
 using ExtractKernel = void (*)(ExtractParams);
 
 template <uint32_t CS, bool SH>
@@ -492,18 +911,41 @@ ExtractKernel extract_kernel_for(uint32_t bs) {
   }
 }
 
-// The two-stage decode is selected by RICEPP_DECODE=two-stage; the default is
-// the fused one-wave-per-stream kernel (rpp_decode_kernel).  Measured on MI355X
+bool extract_bs(uint32_t bs) { return bs == 16 || bs == 32 || bs == 64 || bs == 128; }
+
+// The two-stage decode of every stream is selected by RICEPP_DECODE=two-stage;
+// the default for batches without long streams is the fused
+// one-wave-per-stream kernel (rpp_decode_kernel).  Measured on MI355X
 // (DESIGN.md section 4): the parse pass alone costs 86 VALU per 128-sample
 // sub-block and is VALU-bound at 74 % (196 us for 4096 x 64 KiB), about what
 // the fused kernel needs for parse AND values (258 us), whose value work
 // hides in the parse chain's latency; so splitting the passes does not pay
-// on this hardware.  The path stays for unaligned-offset and long-stream
-// experiments.
+// when the batch has enough streams to fill the GPU.
 bool two_stage(const rpp_config* cfg) {
   const char* e = getenv("RICEPP_DECODE");
   if (!e || std::string(e) != "two-stage") return false;
-  return cfg->block_size == 16 || cfg->block_size == 32 || cfg->block_size == 64 || cfg->block_size == 128;
+  return extract_bs(cfg->block_size);
+}
+
+// Segmented decode (units of 2^L bits; 0 = off): when the batch's longest
+// stream would take longer to parse serially than the whole batch takes at
+// full occupancy (its samples > 1/1024 of the batch's, and >= 2^18).
+// RICEPP_DECODE=segmented forces it, =fused disables it; RICEPP_SEG_LOG2 sets
+// L (tests use small units to split short streams).
+uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples) {
+  if (!extract_bs(cfg->block_size)) return 0;
+  const char* e = getenv("RICEPP_DECODE");
+  const std::string mode = e ? e : "";
+  if (mode == "fused" || mode == "two-stage") return 0;
+  if (mode != "segmented") {
+    if (max_stream_samples < (1u << 18)) return 0;
+    if (max_stream_samples * 1024 < total_samples) return 0;
+  }
+  // about 4096 units for the batch (16 bits per sample at most), 2^20..2^23 bits
+  uint32_t L = 20;
+  while (L < 23 && ((total_samples * 16) >> L) > 4096) ++L;
+  if (const char* l = getenv("RICEPP_SEG_LOG2")) L = (uint32_t)std::min(26, std::max(10, atoi(l)));
+  return L;
 }
 
 }  // namespace
@@ -511,6 +953,15 @@ bool two_stage(const rpp_config* cfg) {
 extern "C" {
 
 // diagnostics only (not in the C ABI header): the extraction phase timers
+int rpp_seg_diag_read(unsigned long long* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_seg_diag), sizeof(g_seg_diag)) != hipSuccess) return RPP_HIP_ERROR;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_seg_diag), z, sizeof(z)) != hipSuccess) return RPP_HIP_ERROR;
+  }
+  return RPP_OK;
+}
+
 int rpp_diag_read(unsigned long long* out8, int reset) {
   if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_dec2_diag), sizeof(g_dec2_diag)) != hipSuccess) return RPP_HIP_ERROR;
   if (reset) {
@@ -520,38 +971,87 @@ int rpp_diag_read(unsigned long long* out8, int reset) {
   return RPP_OK;
 }
 
-uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks) {
+uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                                    uint32_t nblocks) {
   if (rpp_check_config(cfg) != RPP_OK) return 0;
-  return layout(cfg, total_samples, nblocks, nullptr).bytes;
+  const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples);
+  if (!L && !two_stage(cfg)) return 0;  // the fused kernel needs none
+  return layout(cfg, total_samples, nblocks, L, nullptr).bytes;
 }
 
 int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
-                        const uint64_t* d_n_samples, int32_t* d_status, uint64_t total_samples, void* d_workspace,
-                        uint64_t workspace_bytes, void* stream) {
+                        const uint64_t* d_n_samples, int32_t* d_status, uint64_t total_samples,
+                        uint64_t max_stream_samples, void* d_workspace, uint64_t workspace_bytes, void* stream) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
   if (nblocks == 0) return RPP_OK;
   if (!d_in || !d_in_offsets || !d_in_bytes || !d_out || !d_out_offsets || !d_n_samples || !d_status)
     return RPP_INVALID_ARGUMENT;
   hipStream_t s = (hipStream_t)stream;
-  if (!two_stage(cfg))
+  const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples);
+  if (!L && !two_stage(cfg))
     return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
                                              d_n_samples, d_status, s);
-  const Workspace w = layout(cfg, total_samples, nblocks, static_cast<uint8_t*>(d_workspace));
+  const Workspace w = layout(cfg, total_samples, nblocks, L, static_cast<uint8_t*>(d_workspace));
   if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
   const uint32_t chunk_len = cfg->block_size * cfg->component_stream_count;
-  hipLaunchKernelGGL(rpp_dec_count_kernel, dim3((nblocks + 256) / 256), dim3(256), 0, s, d_n_samples, nblocks,
-                     chunk_len, cfg->component_stream_count, w.sb_cnt, w.tile_cnt);
+  const uint32_t g256 = (nblocks + 256) / 256;
+  hipLaunchKernelGGL(rpp_dec_count_kernel, dim3(g256), dim3(256), 0, s, d_n_samples, nblocks, chunk_len,
+                     cfg->component_stream_count, w.sb_cnt, w.tile_cnt);
   if ((st = rpp_exclusive_scan_u64(w.sb_cnt, (uint64_t)nblocks + 1, w.sb_base, s)) != RPP_OK) return st;
   if ((st = rpp_exclusive_scan_u64(w.tile_cnt, (uint64_t)nblocks + 1, w.tile_base, s)) != RPP_OK) return st;
-  hipLaunchKernelGGL(rpp_dec_tile_map_kernel, dim3((nblocks + 255) / 256), dim3(256), 0, s, w.tile_base, nblocks,
-                     w.tile_map);
+  hipLaunchKernelGGL(rpp_dec_tile_map_kernel, dim3(g256), dim3(256), 0, s, w.tile_base, nblocks, w.tile_map);
   if (hipMemsetAsync(w.tile_state, 0, w.max_tiles * 8, s) != hipSuccess) return RPP_HIP_ERROR;
   if (hipMemsetAsync(w.counter, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
-  st = rpp_internal::launch_parse(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base, w.sb_pos,
-                                  d_status, s);
-  if (st != RPP_OK) return st;
+  if (!L) {
+    st = rpp_internal::launch_parse(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base, w.sb_pos,
+                                    d_status, s);
+    if (st != RPP_OK) return st;
+  } else {
+    const uint64_t U = w.units_max;
+    SegArgs a{};
+    a.sv = rpp_internal::SegView{w.unit_map, w.unit_base, w.bm_base, w.bitmap, w.ovr, w.ustate, w.ulo, w.uov,
+                                 w.sst, w.sflags, L, 0, (uint32_t)U};
+    a.in = d_in;
+    a.in_off = d_in_offsets;
+    a.in_bytes = d_in_bytes;
+    a.n_samples = d_n_samples;
+    a.sb_base = w.sb_base;
+    a.sb_pos = w.sb_pos;
+    a.status = d_status;
+    a.cnt = w.cnt2;
+    a.off = w.off2;
+    a.uhit = w.uhit;
+    a.nblocks = nblocks;
+    a.bs = cfg->block_size;
+    a.cs = cfg->component_stream_count;
+    hipLaunchKernelGGL(rpp_seg_units_kernel, dim3(g256), dim3(256), 0, s, a, w.ucnt);
+    if ((st = rpp_exclusive_scan_u64(w.ucnt, (uint64_t)nblocks + 1, w.unit_base, s)) != RPP_OK) return st;
+    if (hipMemsetAsync(w.bm_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
+    if (hipMemsetAsync(w.cnt2, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
+    if (hipMemsetAsync(w.sst, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
+    if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
+    hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.bm_cnt);
+    if ((st = rpp_exclusive_scan_u64(w.bm_cnt, U + 1, w.bm_base, s)) != RPP_OK) return st;
+    // pass 0: every unit; two rerun passes; a serial pass for what is left
+    if (hipMemsetAsync(w.ustate, 0xFF, U * 16, s) != hipSuccess) return RPP_HIP_ERROR;
+    const uint32_t gu = (uint32_t)((U + 255) / 256);
+    for (uint32_t pass : {0u, 1u, 1u, 2u}) {
+      a.sv.pass = pass;  // (the stitch counts the reruns it asks this pass for)
+      if (pass != 0) {
+        hipLaunchKernelGGL(rpp_seg_hit_kernel, dim3(gu), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(rpp_seg_stitch_kernel, dim3(nblocks), dim3(64), 0, s, a);
+      }
+      st = rpp_internal::launch_parse_seg(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base,
+                                          w.sb_pos, d_status, a.sv, s);
+      if (st != RPP_OK) return st;
+    }
+    hipLaunchKernelGGL(rpp_seg_count_kernel, dim3((uint32_t)U), dim3(kSegThreads), 0, s, a);
+    if ((st = rpp_exclusive_scan_u64(w.cnt2, U + 1, w.off2, s)) != RPP_OK) return st;
+    hipLaunchKernelGGL(rpp_seg_write_kernel, dim3((uint32_t)U), dim3(kSegThreads), 0, s, a);
+    hipLaunchKernelGGL(rpp_seg_tail_kernel, dim3(g256), dim3(256), 0, s, a);
+  }
   const bool sh = cfg->unused_lsb_count != 0;
   const ExtractKernel k = cfg->component_stream_count == 1
                               ? (sh ? extract_kernel_for<1, true>(cfg->block_size)
@@ -564,9 +1064,16 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
   if (const char* e = getenv("RICEPP_DEC2_DBG")) p.dbg = (uint32_t)atoi(e);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(w.max_tiles, kMaxExtractGrid);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kTile), 0, s, p);
-  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+  if (hipGetLastError() != hipSuccess) return RPP_HIP_ERROR;
+  if (L)  // streams whose exact chain left the region the units cover (malformed input)
+    return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
+                                             d_n_samples, d_status, s, true);
+  return RPP_OK;
 }
 
+// Without a workspace: the fused kernel (no host synchronisation), or, with
+// RICEPP_DECODE set to two-stage / segmented, the sample counts are read back
+// to size a temporary workspace (this call then synchronises the stream).
 int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                      const uint64_t* d_n_samples, int32_t* d_status, void* stream) {
@@ -576,27 +1083,31 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   if (!d_in || !d_in_offsets || !d_in_bytes || !d_out || !d_out_offsets || !d_n_samples || !d_status)
     return RPP_INVALID_ARGUMENT;
   hipStream_t s = (hipStream_t)stream;
-  if (!two_stage(cfg))
+  const char* e = getenv("RICEPP_DECODE");
+  const std::string mode = e ? e : "";
+  if ((mode != "two-stage" && mode != "segmented") || !extract_bs(cfg->block_size))
     return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
                                              d_n_samples, d_status, s);
-  // the workspace size needs the batch's sample count: read the counts
-  // (this call synchronises the stream; rpp_decode_batch_ws does not)
   uint64_t* h = nullptr;
   if (hipHostMalloc(reinterpret_cast<void**>(&h), (size_t)nblocks * 8, hipHostMallocDefault) != hipSuccess)
     return RPP_HIP_ERROR;
-  uint64_t total = 0;
+  uint64_t total = 0, mx = 0;
   bool ok = hipMemcpyAsync(h, d_n_samples, (size_t)nblocks * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
             hipStreamSynchronize(s) == hipSuccess;
   if (ok)
-    for (uint32_t i = 0; i < nblocks; ++i) total += h[i] < RPP_MAX_STREAM_SAMPLES ? h[i] : 0;
+    for (uint32_t i = 0; i < nblocks; ++i)
+      if (h[i] < RPP_MAX_STREAM_SAMPLES) {
+        total += h[i];
+        mx = std::max<uint64_t>(mx, h[i]);
+      }
   (void)hipHostFree(h);
   if (!ok) return RPP_HIP_ERROR;
-  const uint64_t bytes = rpp_decode_workspace_bytes(cfg, total, nblocks);
+  const uint64_t bytes = rpp_decode_workspace_bytes(cfg, total, mx, nblocks);
   void* ws = nullptr;
-  if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (bytes && hipMallocAsync(&ws, bytes, s) != hipSuccess) return RPP_HIP_ERROR;
   st = rpp_decode_batch_ws(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets, d_n_samples, d_status,
-                           total, ws, bytes, s);
-  (void)hipFreeAsync(ws, s);
+                           total, mx, ws, bytes, s);
+  if (ws) (void)hipFreeAsync(ws, s);
   return st;
 }
 

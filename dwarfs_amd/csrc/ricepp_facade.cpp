@@ -3,7 +3,7 @@
 // The DwarFS plugin semantics follow src/compression/ricepp.cpp (file:line
 // cited at each method).  Encode / decode calls go through a per-(device,
 // config) combining queue: concurrent calls are coalesced into one
-// rpp_encode_batch / rpp_decode_batch launch on a pooled device context
+// rpp_encode_batch_ws / rpp_decode_batch_ws launch on a pooled device context
 // (stream + grow-only device arena + grow-only pinned staging), so the
 // worker_group threads of the DwarFS writer (src/writer/filesystem_writer.cpp:
 // 255-287) and block cache (src/reader/internal/block_cache.cpp:628-706) feed
@@ -429,8 +429,17 @@ class batch_queue {
     hipStream_t s = ctx.stream();
     if (in_total) hip_check(hipMemcpyAsync(d, pin, in_total, hipMemcpyHostToDevice, s), "H2D decode input");
     hip_check(hipMemcpyAsync(d64, h64, 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode params");
-    int st = rpp_decode_batch(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb), reinterpret_cast<uint16_t*>(d + in_total),
-                              d64 + 2 * nb, d64 + 3 * nb, dst, s);
+    // long blocks (16 MiB DwarFS blocks) are parsed in segments by several waves
+    uint64_t total_samples = 0, max_samples = 0;
+    for (request* q : b) {
+      total_samples += q->n_samples;
+      max_samples = std::max<uint64_t>(max_samples, q->n_samples);
+    }
+    const uint64_t ws_bytes = rpp_decode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
+    uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
+    int st = rpp_decode_batch_ws(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb),
+                                 reinterpret_cast<uint16_t*>(d + in_total), d64 + 2 * nb, d64 + 3 * nb, dst,
+                                 total_samples, max_samples, ws, ws_bytes, s);
     if (st != RPP_OK) throw_status(st);
     g_dec_launches.fetch_add(1, std::memory_order_relaxed);
     g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);

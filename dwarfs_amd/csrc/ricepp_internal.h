@@ -1,5 +1,5 @@
-// ricepp_internal.h -- launchers shared between the kernel translation units
-// (not part of the C ABI).
+// ricepp_internal.h -- launchers and data shared between the kernel
+// translation units (not part of the C ABI).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -9,15 +9,72 @@
 
 namespace rpp_internal {
 
+// ---------------------------------------------------------------------------
+// Segmented decode of long streams (ricepp_decode2.hip, DESIGN.md "Segmented
+// decode").  A stream longer than 2^L bits is cut into units of 2^L bits;
+// every unit is parsed by its own wave from a guessed first header (unit 0
+// from the true start), recording the header positions it visits in a bitmap
+// of its region and the first kSegOvr headers past the region in a list.  A
+// guessed chain that meets the previous unit's exact chain is exact from the
+// meeting point on (the parse is deterministic), so the stitch pass keeps each
+// unit's positions from there; a unit whose chain never meets is parsed again
+// from a known header (rerun passes, then one serial pass): the result is the
+// serial parse's, whatever the guesses were.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSegOvr = 16;             // headers recorded past a unit's region
+constexpr uint32_t kSegNone = 0xFFFFFFFFu;   // no position
+constexpr uint32_t kSpecSteps = 14;          // sub-blocks a guessed first header must chain through
+constexpr int32_t kSegFallback = 0x7F5E0001;  // internal status: decode this stream with the fused kernel
+
+// per-unit state words (SegView::ustate[4 u + i])
+enum : uint32_t { kUsNovr = 0, kUsStart = 1, kUsRerun = 2, kUsFlags = 3 };
+enum : uint32_t { kUfRerunDone = 1, kUfNoGuess = 2, kUfTrunc = 4 };
+
+struct SegView {
+  const uint32_t* unit_map;   // [U] stream of unit u
+  const uint64_t* unit_base;  // [B + 1] first unit of stream b (entry B: the number of units)
+  const uint64_t* bm_base;    // [U_max + 1] first bitmap word of unit u
+  uint32_t* bitmap;           // header positions, one bit per stream bit of the unit's region
+  uint32_t* ovr;              // [U_max * kSegOvr] first headers past the region
+  uint32_t* ustate;           // [U_max * 4]
+  uint32_t* ulo;              // [U_max] the unit's exact positions start here (stitch)
+  uint32_t* uov;              // [U_max] overshoot entries of the unit that are its own (stitch)
+  uint32_t* sst;              // [B] first unresolved unit of stream b
+  uint32_t* sflags;           // [B] bit 0: the exact chain ran past the stream's region
+  uint32_t seg_log2;          // L
+  uint32_t pass;              // 0 all units; 1 pending reruns; 2 pending reruns, serial to the end
+  uint32_t units_max;         // grid bound (U_max)
+};
+
+// Last bit position a header (or the end) of a well-formed stream can take,
+// relative to the 4-aligned base (bit 0 at 8 * mis): the stream's bytes,
+// clamped to rpp_worst_case_bytes of its sample count (codec.h:45-55 bound).
+__host__ __device__ inline uint32_t seg_last_bit(uint32_t mis, uint64_t in_bytes, uint64_t n, uint32_t bs,
+                                                  uint32_t cs) {
+  const uint64_t per = n / cs;
+  const uint64_t num = 16 + 4 * ((per + bs - 1) / bs) + 16 * per;
+  const uint64_t wc = (num * cs + 7) / 8;
+  const uint64_t nb = in_bytes < wc ? in_bytes : wc;
+  return (uint32_t)(8u * mis + 8u * nb);
+}
+
 // rpp_decode_kernel: one wave per stream, parse and values fused (any bs).
+// only_fallback: decode only the streams whose status is kSegFallback.
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
-                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream);
+                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback = false);
 
 // rpp_parse_kernel: sub-block start positions of every stream into sb_pos
 // (stream b's entries from sb_base[b]: nsb_b header positions, then the end).
 int launch_parse(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets, const uint64_t* d_in_bytes,
                  uint32_t nblocks, const uint64_t* d_n_samples, const uint64_t* d_sb_base, uint32_t* d_sb_pos,
                  int32_t* d_status, hipStream_t stream);
+
+// The same kernel over units (SegView): single-unit streams exactly as
+// launch_parse; units of split streams into the bitmaps and overshoot lists.
+int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                     const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples,
+                     const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,
+                     hipStream_t stream);
 
 }  // namespace rpp_internal

@@ -884,7 +884,8 @@ struct DecParams {
   int32_t* status;
   uint32_t nblocks;
   uint32_t bs, cs, be, ulsb;
-  uint32_t waves;  // waves (streams) per workgroup
+  uint32_t waves;          // waves (streams) per workgroup
+  uint32_t only_fallback;  // decode only streams whose status is kSegFallback
 };
 
 // ---- transfer tables (built at compile time) ----
@@ -1149,6 +1150,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint32_t lane24 = kSegBits * lane, lane24m4 = lane24 - 4u;
   const uint32_t b = blockIdx.x * p.waves + wv;
   if (b >= p.nblocks) return;  // no barrier below this point
+  if (p.only_fallback && p.status[b] != rpp_internal::kSegFallback) return;
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
   unsigned long long tprev_;
@@ -1784,12 +1786,139 @@ struct ParseParams {
   int32_t* status;
   uint32_t nblocks;
   uint32_t bs;
-  uint32_t waves;  // waves (streams) per workgroup
+  uint32_t waves;  // waves (streams or units) per workgroup
+  rpp_internal::SegView sv;  // SEG: the units of the segmented decode
 };
 
-template <uint32_t CS>
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+
+// Segmented decode, the first header of a unit (ricepp_internal.h): the
+// first candidate bit c in [0, 4 + 16 bs) of the staged words `st` whose
+// chain of kSpecSteps sub-blocks (each parsed exactly as decode.h:42-83 would
+// from there) keeps its header values within a range of 4 -- ricepp output
+// does (the Rice parameter follows the local noise level), a chain through
+// random bits does with probability ~13 * 4^-14.  Candidates are parsed lane by
+// lane out of LDS, up to four chains per lane, 256 at a time; after every
+// sub-block the survivors are compacted into `list` (512 words of LDS).  A
+// wrong guess costs a rerun, never a wrong result.
+__device__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_rel, uint32_t bs, uint32_t lane) {
+  using rpp_internal::kSegNone;
+  using rpp_internal::kSpecSteps;
+  constexpr uint32_t kSlots = 4;
+  const uint32_t maxsb = 4u + 16u * bs;
+  auto peek = [&](uint32_t r) {
+    const uint32_t* w = st + (r >> 5);
+    return __builtin_amdgcn_alignbit(w[1], w[0], r & 31u);
+  };
+  for (uint32_t c0 = 0; c0 < maxsb; c0 += kSlots * kWave) {
+    uint32_t cur[kSlots], org[kSlots], rng[kSlots];  // rng: lowest header | highest << 4
+    bool alive[kSlots];
+    uint32_t nslots = kSlots;
+#pragma unroll
+    for (uint32_t i = 0; i < kSlots; ++i) {
+      org[i] = c0 + lane + kWave * i;
+      alive[i] = org[i] < maxsb && org[i] + 4 <= end_rel;
+      cur[i] = alive[i] ? org[i] : 0u;
+      rng[i] = 0x0Fu;
+    }
+    for (uint32_t step = 0; step < kSpecSteps; ++step) {
+      uint32_t fsv[kSlots];
+      bool rice[kSlots];
+#pragma unroll
+      for (uint32_t i = 0; i < kSlots; ++i) {
+        rice[i] = false;
+        fsv[i] = 0;
+        if (i < nslots) {
+          const uint32_t v = peek(cur[i]) & 15u;
+          const uint32_t lo = min(rng[i] & 15u, v), hi = max(rng[i] >> 4, v);
+          rng[i] = lo | (hi << 4);
+          const uint32_t nc = cur[i] + (v == 15 ? 4u + 16u * bs : 4u);
+          alive[i] = alive[i] && hi - lo <= 3 && nc + 4 <= end_rel;
+          rice[i] = alive[i] && v - 1u < 14u;
+          fsv[i] = v - 1;
+          cur[i] = alive[i] ? nc : 0u;
+        }
+      }
+      // the codes of the Rice sub-blocks
+      for (uint32_t k = 0; k < bs; ++k) {
+#pragma unroll
+        for (uint32_t i = 0; i < kSlots; ++i) {
+          if (i < nslots) {
+            uint32_t at = cur[i];
+            uint32_t x = peek(at);
+            if (x == 0 && rice[i]) {  // a unary run past 32 bits (rare): scan on
+              do {
+                at += 32;
+                if (at + 4 > end_rel) break;
+                x = peek(at);
+              } while (x == 0);
+            }
+            const uint32_t nc = at + ffbl(x) + 1 + fsv[i];
+            const bool bad = rice[i] && (x == 0 || nc + 4 > end_rel);
+            cur[i] = bad ? 0u : (rice[i] ? nc : cur[i]);
+            rice[i] = rice[i] && !bad;
+            alive[i] = alive[i] && !bad;
+          }
+        }
+      }
+      // compact the survivors (in candidate order) into the first slots
+      uint32_t cnt = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kSlots; ++i) {
+        if (i < nslots) {
+          const uint64_t m = __ballot(alive[i]);
+          const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (alive[i]) {
+            list[2 * at] = cur[i];
+            list[2 * at + 1] = org[i] | (rng[i] << 16);
+          }
+          cnt += (uint32_t)__builtin_popcountll(m);
+        }
+      }
+      lds_fence();
+      if (cnt == 0) break;
+      nslots = (cnt + kWave - 1) / kWave;
+#pragma unroll
+      for (uint32_t i = 0; i < kSlots; ++i) {
+        const uint32_t idx = kWave * i + lane;
+        alive[i] = idx < cnt;
+        cur[i] = alive[i] ? list[2 * idx] : 0u;
+        const uint32_t o = alive[i] ? list[2 * idx + 1] : 0u;
+        org[i] = o & 0xFFFFu;
+        rng[i] = o >> 16;
+      }
+      lds_fence();
+    }
+    uint32_t m = kSegNone;
+#pragma unroll
+    for (uint32_t i = 0; i < kSlots; ++i)
+      if (alive[i]) m = min(m, org[i]);
+    m = wave_min_u32(m);
+    if (m != kSegNone) return m;
+  }
+  return kSegNone;
+}
+
+// SEG = false: one wave per stream (launch_parse).  SEG = true: one wave per
+// unit of rpp_internal::SegView; a stream of one unit is parsed exactly as
+// with SEG = false, a unit of a split stream (ricepp_internal.h) records into
+// the bitmaps / overshoot list instead of sb_pos.
+template <uint32_t CS, bool SEG>
 __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParseParams p) {
+  using namespace rpp_internal;
   extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
+  if constexpr (SEG) {
+    // rerun passes (one wave per workgroup): most units have nothing to do;
+    // leave before loading the tables
+    if (p.sv.pass != 0) {
+      const uint32_t w = blockIdx.x * p.waves + threadIdx.x / kWave;
+      if (w >= (uint32_t)p.sv.unit_base[p.nblocks] || p.sv.ustate[4 * w + kUsRerun] == kSegNone) return;
+    }
+  }
   {
     const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
     for (uint32_t i = threadIdx.x; i < kMapEntries; i += blockDim.x) dsm[i] = gt[i];
@@ -1803,8 +1932,22 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + ring_w;
   const uint32_t bs = p.bs;
   const uint32_t lane24 = kSegBits * lane;
-  const uint32_t b = blockIdx.x * p.waves + wv;
-  if (b >= p.nblocks) return;  // no barrier below this point
+  const uint32_t wid = blockIdx.x * p.waves + wv;
+  // ---- the stream (and, SEG, the unit) of this wave ----
+  uint32_t b = wid, u = 0, u0 = 0, ju = 0, nunits = 1;
+  if constexpr (SEG) {
+    if (wid >= p.sv.units_max) return;
+    if (wid >= (uint32_t)p.sv.unit_base[p.nblocks]) return;
+    u = wid;
+    b = __builtin_amdgcn_readfirstlane(p.sv.unit_map[u]);
+    u0 = (uint32_t)p.sv.unit_base[b];
+    nunits = (uint32_t)p.sv.unit_base[b + 1] - u0;
+    ju = u - u0;
+    if (p.sv.pass != 0 && (nunits == 1 || p.sv.ustate[4 * u + kUsRerun] == kSegNone)) return;
+  } else {
+    if (b >= p.nblocks) return;  // no barrier below this point
+  }
+  const bool multi = SEG && nunits > 1;
 
   // ---- per-stream setup (wave-uniform) ----
   int32_t status = RPP_OK;
@@ -1823,7 +1966,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       in = p.in + (ioff - mis);
     }
   }
-  uint32_t* const pos_out = p.sb_pos + p.sb_base[b];
+  uint32_t* const pos_out = multi ? nullptr : p.sb_pos + p.sb_base[b];
   const bool aligned16 = ((uintptr_t)in & 15u) == 0;
   // last readable bit + 1: the reader pulls whole 8-byte packets of the
   // stream (bitstream_reader.h:149-183), zero past its last byte
@@ -1831,8 +1974,65 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
   const uint32_t chunk_len = CS * bs;
   const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
 
+  // ---- SEG: the unit's region [S, E) of header positions ----
+  const uint32_t L = p.sv.seg_log2;
+  const bool serial = multi && p.sv.pass == 2;
+  uint32_t S = 0, E = 0, Eend = 0;
+  bool last = false;
+  if (multi) {
+    Eend = seg_last_bit(mis, nbytes - mis, N, bs, CS);
+    S = ju << L;
+    last = ju + 1 == nunits;
+    E = last ? Eend + 1 : S + (1u << L);
+    if (serial) E = Eend + 1;
+  }
+
+  // ---- SEG: the first header of the unit ----
+  uint32_t P = 8u * mis + 16u * CS;  // codec.h:81-86: the initial values
+  if (multi) {
+    uint32_t* us = p.sv.ustate + 4 * u;
+    uint32_t flags = 0;
+    if (p.sv.pass != 0) {
+      P = us[kUsRerun];  // a header of the exact chain (stitch)
+      flags = kUfRerunDone;
+    } else if (ju != 0) {
+      // A guess: the first candidate bit in [S, S + max sub-block) whose
+      // chain of kSpecSteps sub-blocks looks like ricepp output (seg_guess).
+      constexpr uint32_t kStW = kRingWords + kRingPad;
+      const uint32_t w0 = S >> 5;
+      for (uint32_t i = lane; i < kStW; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
+      lds_fence();
+      const uint32_t g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane);
+      P = g == kSegNone ? kSegNone : S + g;
+      if (P == kSegNone) flags = kUfNoGuess;
+    }
+    // the unit's bitmap words (serial: also those of every later unit)
+    const uint64_t bw0 = p.sv.bm_base[u];
+    const uint64_t bw1 = p.sv.bm_base[serial ? u0 + nunits : u + 1];
+    for (uint64_t i = bw0 / 4 + lane; i < bw1 / 4; i += kWave)
+      reinterpret_cast<uint4*>(p.sv.bitmap)[i] = make_uint4(0, 0, 0, 0);
+    vm_drain();
+    if (lane == 0) {
+      us[kUsNovr] = 0;
+      us[kUsStart] = P;
+      us[kUsRerun] = kSegNone;
+      us[kUsFlags] = flags;
+    }
+    if (serial && lane == 0) {  // the stitch bookkeeping of the rest of the stream
+      p.sv.uov[u - 1] = kSegOvr - 1;
+      p.sv.ulo[u] = P;
+      for (uint32_t k = ju + 1; k < nunits; ++k) {
+        p.sv.ulo[u0 + k] = k << L;
+        p.sv.uov[u0 + k - 1] = 0;
+      }
+      p.sv.uov[u0 + nunits - 1] = 0;
+      p.sv.sst[b] = nunits;
+    }
+    if (P == kSegNone) return;
+  }
+
   // ---- LDS ring of the stream's words (as rpp_decode_kernel) ----
-  uint32_t fill_w = 0;
+  uint32_t fill_w = multi ? (P >> 5) & ~(kChunkWords - 1) : 0u;
   bool pend = false;
   auto retire = [&]() {
     if (pend) {
@@ -1890,25 +2090,46 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
 
   // ---- sub-block start positions, buffered 64 at a time in one VGPR ----
   uint32_t pbuf = 0, pcnt = 0, pstart = 0;
+  uint32_t novr = 0;
+  bool stop = false;
   auto flush = [&]() {
-    if (lane < pcnt) pos_out[pstart + lane] = pbuf;
-    pstart += pcnt;
+    if (multi) {  // into the bitmap of the unit holding the position
+      if (lane < pcnt) {
+        const uint32_t k = pbuf >> L;
+        const uint64_t w = p.sv.bm_base[u0 + k] + ((pbuf - (k << L)) >> 5);
+        atomicOr(p.sv.bitmap + w, 1u << (pbuf & 31u));
+      }
+    } else {
+      if (lane < pcnt) pos_out[pstart + lane] = pbuf;
+      pstart += pcnt;
+    }
     pcnt = 0;
   };
   auto record = [&](uint32_t pos) {
+    if (multi && pos >= E) {  // past the region: the overshoot list, or the end
+      if (last || serial) {
+        stop = true;
+        if (lane == 0) atomicOr(p.sv.sflags + b, 1u);
+      } else {
+        if (lane == 0 && novr < kSegOvr) p.sv.ovr[kSegOvr * u + novr] = pos;
+        if (++novr >= kSegOvr) stop = true;
+      }
+      return;
+    }
     pbuf = lane == pcnt ? pos : pbuf;
     if (++pcnt == kWave) flush();
   };
 
-  uint32_t P = 8u * mis + 16u * CS;  // codec.h:81-86: the initial values
-  if (status == RPP_OK && P > lim) status = RPP_TRUNCATED_INPUT;
-  const uint32_t nsb = nchunks * CS;
+  if (!multi && status == RPP_OK && P > lim) status = RPP_TRUNCATED_INPUT;
+  // a unit of a split stream parses bs-sample sub-blocks until its region
+  // ends (the ragged last chunk is re-parsed by rpp_seg_tail_kernel)
+  const uint32_t nsb = multi ? 0xFFFFFFFFu : nchunks * CS;
   const bool fast_bs = bs == 2 * kWave || bs == 16 || bs == 32 || bs == 64;
-  const uint32_t nsb_fast = fast_bs ? (N / chunk_len) * CS : 0u;
+  const uint32_t nsb_fast = multi ? 0xFFFFFFFFu : fast_bs ? (N / chunk_len) * CS : 0u;
   ScanRegs sreg;
 
   uint32_t s = 0;
-  while (s < nsb && status == RPP_OK) {
+  while (s < nsb && status == RPP_OK && !stop) {
     // ---- fast loop: Rice sub-blocks of bs codes with fs in [LO, HI] lying
     //      in one window, ring resident; the parse of sub-block s+1 is issued
     //      as soon as the end of s is known ----
@@ -1989,7 +2210,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       bool ok = parse(P, fs, e0, e1, e2, Pn) && header_ok(h);
       while (ok) {
         // sub-block s at P ends at Pn; parse s+1 at Pn
-        const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
+        const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit && !stop;
         const uint32_t xlB = seg_bits(Pn);
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
         const uint32_t fsB = fs_of(hB);
@@ -2011,7 +2232,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
         }
       }
     };
-    while (s < nsb_fast && status == RPP_OK && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
+    while (s < nsb_fast && status == RPP_OK && !stop && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
       const uint32_t* w = ring + ((P >> 5) & kRingMask);
       const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
       const uint32_t s0 = s;
@@ -2019,16 +2240,20 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
       if (s == s0) break;  // the general path takes this sub-block
     }
-    if (s >= nsb || status != RPP_OK) break;
+    if (s >= nsb || status != RPP_OK || stop) break;
     // ---- general path: one sub-block of any kind ----
     const uint32_t cbase = (s / CS) * chunk_len;
-    const uint32_t n = min(N - cbase, chunk_len) / CS;
+    const uint32_t n = multi ? bs : min(N - cbase, chunk_len) / CS;
     ensure(P >> 5);
+    if (multi) {  // (the end of the stream's last sub-block is a position too)
+      record(P);
+      if (stop) break;
+    }
     if (P + 4 > lim) {  // decode.h:60: the 4-bit header
       status = RPP_TRUNCATED_INPUT;
       break;
     }
-    record(P);
+    if (!multi) record(P);
     uint32_t xl;
     load_x(P + kSegBits * lane, xl);
     const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
@@ -2122,6 +2347,15 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     ring_keep(P);
   }
   retire();
+  if (multi) {
+    flush();
+    vm_drain();
+    if (lane == 0) {
+      p.sv.ustate[4 * u + kUsNovr] = min(novr, kSegOvr);
+      if (status != RPP_OK) p.sv.ustate[4 * u + kUsFlags] |= kUfTrunc;
+    }
+    return;
+  }
   if (status == RPP_OK) record(P);  // the end of the last sub-block
   flush();
   if (lane == 0) p.status[b] = status;
@@ -2226,7 +2460,7 @@ namespace rpp_internal {
 
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
-                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream) {
+                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
   if (nblocks == 0) return RPP_OK;
@@ -2250,7 +2484,7 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
   if (attr_err != hipSuccess) return RPP_HIP_ERROR;
   DecParams p{d_in, d_in_offsets, d_in_bytes, d_out, d_out_offsets, d_n_samples, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count, W};
+              cfg->unused_lsb_count, W, only_fallback ? 1u : 0u};
   const auto k = kernels[2 * (cfg->component_stream_count - 1) + (cfg->unused_lsb_count ? 1 : 0)];
   hipLaunchKernelGGL(k, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
@@ -2262,7 +2496,7 @@ int launch_parse(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_i
   if (nblocks == 0) return RPP_OK;
   uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
-  static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1>, rpp_parse_kernel<2>};
+  static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1, false>, rpp_parse_kernel<2, false>};
   static std::once_flag attr_once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(attr_once, [] {
@@ -2276,6 +2510,32 @@ int launch_parse(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_i
                 cfg->block_size, W};
   hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3((nblocks + W - 1) / W), dim3(kWave * W), lds,
                      stream, p);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
+int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                     const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples,
+                     const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,
+                     hipStream_t stream) {
+  if (nblocks == 0 || sv.units_max == 0) return RPP_OK;
+  // rerun passes have a few units to do: fewer waves per workgroup spread them
+  const uint32_t W = sv.pass == 0 ? std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (sv.units_max + 255) / 256))
+                                  : 1u;
+  const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
+  static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1, true>, rpp_parse_kernel<2, true>};
+  static std::once_flag attr_once;
+  static hipError_t attr_err = hipSuccess;
+  std::call_once(attr_once, [] {
+    const int mx = (int)(kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4);
+    for (auto k : kernels)
+      if (attr_err == hipSuccess)
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+  });
+  if (attr_err != hipSuccess) return RPP_HIP_ERROR;
+  ParseParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_sb_base, d_sb_pos, d_status, nblocks,
+                cfg->block_size, W, sv};
+  hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3((sv.units_max + W - 1) / W), dim3(kWave * W),
+                     lds, stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .codec import CodecConfig, _check, _raise_status, decode_workspace
+from .codec import CodecConfig, _check, _raise_status
 
 
 def _ptr(t: torch.Tensor) -> C.c_void_p:
@@ -120,9 +120,9 @@ class HostDecodePipeline:
             d_in = [torch.empty(cap_in, dtype=torch.uint8, device=self.dev) for _ in range(2)]
             d_out = [torch.empty(cap_out, dtype=torch.int16, device=self.dev) for _ in range(2)]
             # one decode workspace: the chunk decodes are ordered on self.comp
-            ws_samples = max(int(n[lo:hi].sum()) for lo, hi in chunks)
-            ws_blocks = max(hi - lo for lo, hi in chunks)
-            ws = decode_workspace(self.config, ws_samples, ws_blocks, self.dev)
+            ws_bytes = max(int(N.lib().rpp_decode_workspace_bytes(
+                C.byref(self.cfg), int(n[lo:hi].sum()), int(n[lo:hi].max()), hi - lo)) for lo, hi in chunks)
+            ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=self.dev)
         for s in (self.h2d, self.comp, self.d2h):
             s.wait_stream(cur)
         ev_h2d = [torch.cuda.Event() for _ in range(2)]
@@ -144,7 +144,8 @@ class HostDecodePipeline:
                 _raise_status(N.lib().rpp_decode_batch_ws(
                     C.byref(self.cfg), _ptr(d_in[slot]), _ptr(d_rel_in[lo:hi]), _ptr(d_len[lo:hi]), hi - lo,
                     _ptr(d_out[slot]), _ptr(d_rel_out[lo:hi]), _ptr(d_n[lo:hi]), _ptr(status[lo:hi]),
-                    int(n[lo:hi].sum()), _ptr(ws), ws.numel(), C.c_void_p(self.comp.cuda_stream)))
+                    int(n[lo:hi].sum()), int(n[lo:hi].max()), _ptr(ws), ws.numel(),
+                    C.c_void_p(self.comp.cuda_stream)))
                 ev_dec[slot].record(self.comp)
             oa, ob = cout[k]
             with torch.cuda.stream(self.d2h):

@@ -153,8 +153,8 @@ class ShardPipeline:
         self.decoded = torch.empty(max(int(n_samples.sum()), 8), dtype=torch.int16, device=dev)
         self.dec_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
         self.total_samples = int(n_samples.sum())
-        self.workspace = decode_workspace(config, self.total_samples, self.nblocks, dev)
         self.max_samples = int(n_samples.max()) if self.nblocks else 0
+        self.workspace = decode_workspace(config, self.total_samples, self.nblocks, dev, self.max_samples)
         self.enc_workspace = encode_workspace(config, self.total_samples, self.max_samples, self.nblocks, dev)
         self.all_sizes: Optional[torch.Tensor] = None
         self.image_offsets: Optional[torch.Tensor] = None
@@ -183,8 +183,8 @@ class ShardPipeline:
             C.byref(self.cfg), C.c_void_p(self.data.data_ptr()), C.c_void_p(self.d_out_off.data_ptr()),
             C.c_void_p(self.sizes.data_ptr()), self.nblocks, C.c_void_p(self.decoded.data_ptr()),
             C.c_void_p(self.d_dec_off.data_ptr()), C.c_void_p(self.d_n.data_ptr()),
-            C.c_void_p(self.dec_status.data_ptr()), self.total_samples, C.c_void_p(self.workspace.data_ptr()),
-            self.workspace.numel(), self._stream()))
+            C.c_void_p(self.dec_status.data_ptr()), self.total_samples, self.max_samples,
+            C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), self._stream()))
 
     def gather(self) -> None:
         self.all_sizes = self.size_gather(self.sizes)

@@ -135,10 +135,12 @@ int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint6
  *   d_n_samples   [nblocks] samples to decode (multiple of cs)
  *   d_status      [nblocks] RPP_OK, RPP_TRUNCATED_INPUT (the reference's
  *                 std::out_of_range) or RPP_INVALID_ARGUMENT
- * For bs 16/32/64/128 the decode runs in two passes over a device workspace
- * (rpp_decode_batch_ws); this convenience form sizes it by reading
- * d_n_samples back, i.e. it synchronises `stream` once, and allocates it
- * stream-ordered (hipMallocAsync).
+ * One wave decodes one stream (parse and values fused), asynchronously on
+ * `stream`.  This form does not know the batch's longest stream: batches with
+ * long streams (a few streams of MiBs) should use rpp_decode_batch_ws, which
+ * splits them.  (With RICEPP_DECODE=two-stage or =segmented set, this form
+ * reads d_n_samples back to size a temporary workspace: it then synchronises
+ * `stream` once.)
  */
 int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
@@ -147,21 +149,28 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
 
 /*
  * Device workspace rpp_decode_batch_ws needs for a batch of `nblocks` streams
- * holding `total_samples` samples in all (0 for an unsupported config).
+ * holding `total_samples` samples in all, the longest `max_stream_samples`
+ * (0: none needed, or an unsupported config).
  */
-uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks);
+uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                                    uint32_t nblocks);
 
 /*
- * rpp_decode_batch with a caller-owned device workspace of at least
- * rpp_decode_workspace_bytes(cfg, total_samples, nblocks) bytes, where
- * total_samples >= the sum of d_n_samples.  Fully asynchronous on `stream`
- * (graph-capturable).  Stage 1 finds every sub-block's start bit (one wave
- * per stream), stage 2 decodes all sub-blocks in parallel (one lane each).
+ * rpp_decode_batch with the batch's sample counts and a caller-owned device
+ * workspace of at least rpp_decode_workspace_bytes(cfg, total_samples,
+ * max_stream_samples, nblocks) bytes, where total_samples >= the sum of
+ * d_n_samples and max_stream_samples >= the largest.  Fully asynchronous on
+ * `stream` (graph-capturable).  A batch whose longest stream holds more than
+ * 1/1024 of its samples (and >= 2^18) is decoded segmented (bs 16/32/64/128):
+ * long streams are cut into units of 2^20..2^23 bits parsed by one wave each
+ * from a guessed first header, stitched exactly, then every sub-block of
+ * every stream is decoded by its own lane; other batches one wave per stream.
  */
 int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
                         const uint64_t* d_out_offsets, const uint64_t* d_n_samples, int32_t* d_status,
-                        uint64_t total_samples, void* d_workspace, uint64_t workspace_bytes, void* stream);
+                        uint64_t total_samples, uint64_t max_stream_samples, void* d_workspace,
+                        uint64_t workspace_bytes, void* stream);
 
 /*
  * Unused least-significant bits of 16-bit images (the FITS categorizer's

@@ -338,18 +338,33 @@ def test_decode_oracle_encoded_32mib_frame():
 
 # ---- the two-stage decode (RICEPP_DECODE=two-stage: parse pass + lane-per-sub-block extraction) ----
 
-class _two_stage:
+class _decode_mode:
+    """Selects the decode path for the block (RICEPP_DECODE, and RICEPP_SEG_LOG2 for the unit size of the
+    segmented decode: small units split even short streams into many)."""
+
+    def __init__(self, mode, seg_log2=None):
+        self.env = {"RICEPP_DECODE": mode, "RICEPP_SEG_LOG2": None if seg_log2 is None else str(seg_log2)}
+
     def __enter__(self):
         import os
-        self.old = os.environ.get("RICEPP_DECODE")
-        os.environ["RICEPP_DECODE"] = "two-stage"
+        self.old = {k: os.environ.get(k) for k in self.env}
+        for k, v in self.env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
     def __exit__(self, *a):
         import os
-        if self.old is None:
-            os.environ.pop("RICEPP_DECODE", None)
-        else:
-            os.environ["RICEPP_DECODE"] = self.old
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _two_stage():
+    return _decode_mode("two-stage")
 
 
 @pytest.mark.parametrize("bs", [16, 32, 64, 128])
@@ -431,3 +446,78 @@ def test_segmented_encode_of_long_streams(bs, cs):
     run_batch(codec.CodecConfig(bs, cs, "big", 0), blocks)
     run_batch(codec.CodecConfig(bs, cs, "little", 2), [datagen.poisson_data(rng, 2 * seg + 3 * cs, lam=300,
                                                                              ulsb=2, big_endian=False)])
+
+
+# ---- the segmented decode of long streams (units parsed from guessed headers, stitched exactly) ----
+
+def _kind_blocks(rng, sizes, cs, ulsb=0, be=True):
+    kinds = ("poisson", "benchmark", "mixed", "full_range", "constant", "spiky", "codec_test", "zeros")
+    blocks = []
+    for i, n in enumerate(sizes):
+        n = int(n) // cs * cs
+        k = kinds[i % len(kinds)]
+        if k == "poisson":
+            blocks.append(datagen.poisson_data(rng, n, ulsb=ulsb, big_endian=be))
+        elif k == "benchmark":
+            blocks.append(datagen.benchmark_data(rng, n, ulsb=ulsb, big_endian=be))
+        elif k == "mixed":
+            blocks.append(datagen.mixed_data(rng, n, ulsb=ulsb, big_endian=be))
+        elif k == "full_range":
+            blocks.append(datagen.full_range_data(rng, n, ulsb=ulsb, big_endian=be))
+        elif k == "constant":
+            blocks.append(datagen.constant_data(n, ulsb=ulsb, big_endian=be))
+        elif k == "spiky":
+            blocks.append(datagen.spiky_data(rng, n, ulsb=ulsb, big_endian=be))
+        elif k == "codec_test":
+            blocks.append(datagen.codec_test_data(rng, n, ulsb=ulsb, big_endian=be))
+        else:
+            blocks.append(np.zeros(n, np.uint16))
+    return blocks
+
+
+@pytest.mark.parametrize("bs", [16, 32, 64, 128])
+@pytest.mark.parametrize("cs", [1, 2])
+@pytest.mark.parametrize("seg_log2", [10, 13, 16])
+def test_segmented_decode_config_matrix(bs, cs, seg_log2):
+    """Every stream split into units of 2^seg_log2 bits (1 Kib units make most guesses fail and exercise the
+    rerun and serial passes; 64 Kib units mostly stitch at once): the decode must be the oracle's, for every
+    data kind, byte order, unused-LSB count, ragged last chunk and stream byte offset."""
+    rng = np.random.default_rng(9000 + 100 * seg_log2 + bs + cs)
+    sizes = [rng.integers(1, 400) * cs, 40000, 70001, 123457, 5000, 31, 65536 + 3, 90000, 200000]
+    codec.segmented_decode_stats(reset=True)
+    with _decode_mode("segmented", seg_log2):
+        for be, ulsb in ((True, 0), (False, 3)):
+            cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
+            blocks = _kind_blocks(rng, sizes, cs, ulsb, be)
+            run_batch(cfg, blocks)
+            _decode_oracle_streams(cfg, blocks, ragged=True)
+    stats = codec.segmented_decode_stats(reset=True)
+    assert stats["met"] > 0, stats  # the units were split and stitched
+    if seg_log2 == 10:
+        assert stats["reruns"] + stats["serial"] > 0, stats
+
+
+def test_segmented_decode_errors_match_oracle():
+    """Truncated and corrupt streams, split into 1 Kib units: the status and the output are the oracle's
+    (a corrupt chain that runs past the region a stream's sample count allows is decoded by the fused kernel)."""
+    for log2 in (10, 12):
+        with _decode_mode("segmented", log2):
+            test_truncated_input_status_matches_oracle()
+            for bs, cs in ((128, 1), (16, 2)):
+                test_corrupt_streams_match_oracle(bs, cs)
+
+
+def test_segmented_decode_is_chosen_for_long_streams():
+    """Default mode: a batch whose longest stream dominates (one 16 MiB generator block, a 4 MiB Poisson
+    block and small ones) takes the segmented decode; the result is the oracle's, the same as with the fused
+    kernel forced."""
+    rng = np.random.default_rng(4242)
+    blocks = [datagen.benchmark_data(rng, 8 << 20), datagen.poisson_data(rng, 2 << 20)]
+    blocks += [datagen.poisson_data(rng, int(n)) for n in rng.integers(1, 40000, 5)]
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    codec.segmented_decode_stats(reset=True)
+    run_batch(cfg, blocks)
+    stats = codec.segmented_decode_stats(reset=True)
+    assert stats["met"] > 0 and stats["fallback"] == 0, stats
+    with _decode_mode("fused"):
+        _decode_oracle_streams(cfg, blocks[1:3])

@@ -52,7 +52,7 @@ def main():
     dev = torch.device("cuda:0")
     d = torch.from_numpy(np.frombuffer(data + bytes(64), np.uint8).copy()).to(dev)
     total = len(x)
-    ws = codec.decode_workspace(cfg, total, 1, dev)
+    ws = codec.decode_workspace(cfg, total, 1, dev, total)
     ws.zero_()
     out = torch.zeros(total + 8, dtype=torch.int16, device=dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -62,7 +62,7 @@ def main():
     r = N.lib().rpp_decode_batch_ws(C.byref(c), C.c_void_p(d.data_ptr()), C.c_void_p(keep[0].data_ptr()),
                                     C.c_void_p(keep[1].data_ptr()), 1, C.c_void_p(out.data_ptr()),
                                     C.c_void_p(keep[2].data_ptr()), C.c_void_p(keep[3].data_ptr()),
-                                    C.c_void_p(st.data_ptr()), total, C.c_void_p(ws.data_ptr()), ws.numel(),
+                                    C.c_void_p(st.data_ptr()), total, total, C.c_void_p(ws.data_ptr()), ws.numel(),
                                     C.c_void_p(torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     print("call", r, "status", int(st.item()))
