@@ -1034,10 +1034,10 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
     if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
     hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.bm_cnt);
     if ((st = rpp_exclusive_scan_u64(w.bm_cnt, U + 1, w.bm_base, s)) != RPP_OK) return st;
-    // pass 0: every unit; two rerun passes; a serial pass for what is left
+    // pass 0: every unit; three rerun passes; a serial pass for what is left
     if (hipMemsetAsync(w.ustate, 0xFF, U * 16, s) != hipSuccess) return RPP_HIP_ERROR;
     const uint32_t gu = (uint32_t)((U + 255) / 256);
-    for (uint32_t pass : {0u, 1u, 1u, 2u}) {
+    for (uint32_t pass : {0u, 1u, 1u, 1u, 2u}) {
       a.sv.pass = pass;  // (the stitch counts the reruns it asks this pass for)
       if (pass != 0) {
         hipLaunchKernelGGL(rpp_seg_hit_kernel, dim3(gu), dim3(256), 0, s, a);

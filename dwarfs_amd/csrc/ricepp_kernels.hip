@@ -1790,6 +1790,15 @@ struct ParseParams {
   rpp_internal::SegView sv;  // SEG: the units of the segmented decode
 };
 
+// segmented-decode parse diagnostics (rpp_parse_diag_read): cycles in the
+// guess, cycles in the chain, sub-blocks parsed, units
+__device__ unsigned long long g_parse_diag[8];
+__device__ __forceinline__ uint64_t memtime() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
@@ -1799,13 +1808,21 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // Segmented decode, the first header of a unit (ricepp_internal.h): the
 // first candidate bit c in [0, 4 + 16 bs) of the staged words `st` whose
 // chain of kSpecSteps sub-blocks (each parsed exactly as decode.h:42-83 would
-// from there) keeps its header values within a range of 4 -- ricepp output
-// does (the Rice parameter follows the local noise level), a chain through
-// random bits does with probability ~13 * 4^-14.  Candidates are parsed lane by
-// lane out of LDS, up to four chains per lane, 256 at a time; after every
-// sub-block the survivors are compacted into `list` (512 words of LDS).  A
-// wrong guess costs a rerun, never a wrong result.
-__device__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_rel, uint32_t bs, uint32_t lane) {
+// from there) keeps its header values within a range of 4 (highest - lowest
+// <= 3), with zero headers only in an all-zero chain.  ricepp output does:
+// the Rice parameter follows the local noise level (Poisson data stays on one
+// or two values, 6-bit noise with outliers on fs 11..13).  Random bits do
+// not, except through the zero high bits of small remainders, which read as
+// chains of small headers -- hence the zero rule (a CPU replay of the guess
+// on the generator data: 6 of 60 units unstitchable without it, 0 with it).
+// Candidates a few bits before the true header often land on the true chain
+// after one sub-block; the stitch accepts those.  Candidates are parsed lane
+// by lane out of LDS, up to four chains per lane and three codes per read,
+// 256 candidates at a time; after every sub-block the survivors are
+// compacted into `list` (512 words of LDS).
+// A wrong guess costs a rerun, never a wrong result.
+__device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_rel, uint32_t bs,
+                                              uint32_t lane) {
   using rpp_internal::kSegNone;
   using rpp_internal::kSpecSteps;
   constexpr uint32_t kSlots = 4;
@@ -1814,7 +1831,9 @@ __device__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_r
     const uint32_t* w = st + (r >> 5);
     return __builtin_amdgcn_alignbit(w[1], w[0], r & 31u);
   };
+  uint32_t n_chunks = 0, n_steps = 0, n_slotsteps = 0;
   for (uint32_t c0 = 0; c0 < maxsb; c0 += kSlots * kWave) {
+    ++n_chunks;
     uint32_t cur[kSlots], org[kSlots], rng[kSlots];  // rng: lowest header | highest << 4
     bool alive[kSlots];
     uint32_t nslots = kSlots;
@@ -1826,6 +1845,8 @@ __device__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_r
       rng[i] = 0x0Fu;
     }
     for (uint32_t step = 0; step < kSpecSteps; ++step) {
+      ++n_steps;
+      n_slotsteps += nslots;
       uint32_t fsv[kSlots];
       bool rice[kSlots];
 #pragma unroll
@@ -1837,33 +1858,53 @@ __device__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_r
           const uint32_t lo = min(rng[i] & 15u, v), hi = max(rng[i] >> 4, v);
           rng[i] = lo | (hi << 4);
           const uint32_t nc = cur[i] + (v == 15 ? 4u + 16u * bs : 4u);
-          alive[i] = alive[i] && hi - lo <= 3 && nc + 4 <= end_rel;
+          // (zero sub-blocks only in an all-zero run: chains of small
+          // headers through the zero high bits of small remainders are the
+          // common false survivors)
+          alive[i] = alive[i] && hi - lo <= 3 && (lo != 0 || hi == 0) && nc + 4 <= end_rel;
           rice[i] = alive[i] && v - 1u < 14u;
           fsv[i] = v - 1;
           cur[i] = alive[i] ? nc : 0u;
         }
       }
-      // the codes of the Rice sub-blocks
-      for (uint32_t k = 0; k < bs; ++k) {
+      // the codes of the Rice sub-blocks, branch-free, up to three per LDS
+      // read (a 64-bit window; codes 2 and 3 when the previous one ends in
+      // the first 32 bits).  A window without a terminator (a unary run past
+      // 32 bits, rare) advances 32 bits and consumes no code.
+      uint32_t ncode[kSlots];
 #pragma unroll
-        for (uint32_t i = 0; i < kSlots; ++i) {
-          if (i < nslots) {
-            uint32_t at = cur[i];
-            uint32_t x = peek(at);
-            if (x == 0 && rice[i]) {  // a unary run past 32 bits (rare): scan on
-              do {
-                at += 32;
-                if (at + 4 > end_rel) break;
-                x = peek(at);
-              } while (x == 0);
-            }
-            const uint32_t nc = at + ffbl(x) + 1 + fsv[i];
-            const bool bad = rice[i] && (x == 0 || nc + 4 > end_rel);
-            cur[i] = bad ? 0u : (rice[i] ? nc : cur[i]);
-            rice[i] = rice[i] && !bad;
-            alive[i] = alive[i] && !bad;
-          }
-        }
+      for (uint32_t i = 0; i < kSlots; ++i) ncode[i] = 0;
+      auto codes = [&](uint32_t i) {
+        const uint32_t* w = st + (cur[i] >> 5);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        const uint32_t sh = cur[i] & 31u;
+        const uint32_t x = __builtin_amdgcn_alignbit(w1, w0, sh), xn = __builtin_amdgcn_alignbit(w2, w1, sh);
+        const uint32_t k1 = fsv[i] + 1, left = bs - ncode[i];
+        const uint32_t e1 = ffbl(x) + k1;
+        const uint32_t y = __builtin_amdgcn_alignbit(xn, x, e1 & 31u);
+        const bool c2 = e1 < 32 && y != 0 && left >= 2;
+        const uint32_t e2 = e1 + ffbl(y) + k1;
+        const uint32_t z = __builtin_amdgcn_alignbit(xn, x, e2 & 31u);
+        const bool c3 = c2 && e2 < 32 && z != 0 && left >= 3;
+        const uint32_t e3 = e2 + ffbl(z) + k1;
+        const bool zero = x == 0;
+        const uint32_t adv = zero ? 32u : c3 ? e3 : c2 ? e2 : e1;
+        const uint32_t n = zero ? 0u : 1u + (c2 ? 1u : 0u) + (c3 ? 1u : 0u);
+        const bool r = rice[i];
+        const uint32_t nxt = cur[i] + adv;
+        const bool bad = r && nxt + 4 > end_rel;
+        cur[i] = r ? (bad ? 0u : nxt) : cur[i];
+        ncode[i] += r ? n : 0u;
+        alive[i] = alive[i] && !bad;
+        rice[i] = r && !bad && ncode[i] < bs;
+      };
+      for (;;) {
+        const bool more = rice[0] || rice[1] || rice[2] || rice[3];
+        if (__ballot(more) == 0) break;
+        codes(0);
+        if (nslots > 1) codes(1);
+        if (nslots > 2) codes(2);
+        if (nslots > 3) codes(3);
       }
       // compact the survivors (in candidate order) into the first slots
       uint32_t cnt = 0;
@@ -1898,7 +1939,14 @@ __device__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_r
     for (uint32_t i = 0; i < kSlots; ++i)
       if (alive[i]) m = min(m, org[i]);
     m = wave_min_u32(m);
-    if (m != kSegNone) return m;
+    if (m != kSegNone || c0 + kSlots * kWave >= maxsb) {
+      if (lane == 0) {
+        atomicAdd(&g_parse_diag[4], (unsigned long long)n_chunks);
+        atomicAdd(&g_parse_diag[5], (unsigned long long)n_steps);
+        atomicAdd(&g_parse_diag[6], (unsigned long long)n_slotsteps);
+      }
+      if (m != kSegNone) return m;
+    }
   }
   return kSegNone;
 }
@@ -2002,7 +2050,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       const uint32_t w0 = S >> 5;
       for (uint32_t i = lane; i < kStW; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
       lds_fence();
+      const uint64_t tg = memtime();
       const uint32_t g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane);
+      if (lane == 0) atomicAdd(&g_parse_diag[0], (unsigned long long)(memtime() - tg));
       P = g == kSegNone ? kSegNone : S + g;
       if (P == kSegNone) flags = kUfNoGuess;
     }
@@ -2129,6 +2179,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
   ScanRegs sreg;
 
   uint32_t s = 0;
+  const uint64_t t_chain = multi ? memtime() : 0;
   while (s < nsb && status == RPP_OK && !stop) {
     // ---- fast loop: Rice sub-blocks of bs codes with fs in [LO, HI] lying
     //      in one window, ring resident; the parse of sub-block s+1 is issued
@@ -2351,6 +2402,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     flush();
     vm_drain();
     if (lane == 0) {
+      atomicAdd(&g_parse_diag[1], (unsigned long long)(memtime() - t_chain));
+      atomicAdd(&g_parse_diag[2], (unsigned long long)s);
+      atomicAdd(&g_parse_diag[3], 1ull);
       p.sv.ustate[4 * u + kUsNovr] = min(novr, kSegOvr);
       if (status != RPP_OK) p.sv.ustate[4 * u + kUsFlags] |= kUfTrunc;
     }
@@ -2369,6 +2423,16 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
 extern "C" {
 
 uint32_t rpp_abi_version(void) { return 1; }
+
+// diagnostics only (not in the C ABI header): the segmented parse's counters
+int rpp_parse_diag_read(unsigned long long* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_parse_diag), sizeof(g_parse_diag)) != hipSuccess) return RPP_HIP_ERROR;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_parse_diag), z, sizeof(z)) != hipSuccess) return RPP_HIP_ERROR;
+  }
+  return RPP_OK;
+}
 
 #ifdef RPP_STATS
 // Diagnostic build only: copies (and optionally clears) the loop counters.

@@ -1,0 +1,52 @@
+"""Where the segmented parse spends its time: s_memtime cycles (100 MHz) in the guess and in the unit
+chains, sub-blocks parsed, units -- for one 16 MiB Poisson stream and the block mix.
+
+usage: python tools/seg_parse_diag.py"""
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
+import datagen  # noqa: E402
+from dwarfs_amd import _native as N  # noqa: E402
+from dwarfs_amd import codec  # noqa: E402
+
+MIB = 1 << 20
+
+
+def run(name, blocks):
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    ns = [len(b) for b in blocks]
+    offs = np.zeros(len(ns), np.int64)
+    offs[1:] = np.cumsum(ns)[:-1]
+    x = torch.from_numpy(np.concatenate(blocks).view(np.int16)).cuda()
+    enc = codec.encode_batch(cfg, x, offs, ns)
+    codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns)
+    torch.cuda.synchronize()
+    buf = (C.c_ulonglong * 8)()
+    N.lib().rpp_parse_diag_read(buf, 1)
+    codec.segmented_decode_stats(reset=True)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    out, st = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns)
+    ev[1].record()
+    torch.cuda.synchronize()
+    N.lib().rpp_parse_diag_read(buf, 1)
+    g, ch, sb, un, nch, nst, nsl, _ = map(int, buf)
+    print(f"{name}: {ev[0].elapsed_time(ev[1]):.3f} ms, units {un}, sub-blocks {sb}, "
+          f"guess {g / max(un, 1) / 100:.1f} us/unit, chain {ch / max(un, 1) / 100:.1f} us/unit = "
+          f"{ch / max(sb, 1) * 10:.0f} ns/sub-block; per guess {nch / max(un, 1):.2f} chunks {nst / max(un, 1):.1f} steps "
+          f"{nsl / max(un, 1):.1f} slot-steps, exact {torch.equal(out[:sum(ns)], x)}, "
+          f"{codec.segmented_decode_stats()}", flush=True)
+
+
+rng = np.random.default_rng(3)
+run("one 16 MiB Poisson", [datagen.poisson_data(rng, 8 * MIB)])
+run("one 16 MiB generator", [datagen.benchmark_data(rng, 8 * MIB)])
+sizes = [1] * 84 + [4] * 21 + [16] * 21
+rng.shuffle(sizes)
+run("mix 504 MiB", [datagen.poisson_data(rng, m * MIB // 2, lam=float(rng.integers(200, 3000))) for m in sizes])
