@@ -54,7 +54,10 @@ struct Workspace {
   uint64_t* tile_cnt;   // [B + 1]
   uint64_t* tile_base;  // [B + 1]
   uint64_t* tile_state; // [max_tiles]
-  uint32_t* tile_map;   // [max_tiles]
+  uint32_t* tile_map;   // [max_tiles] stream of the t-th tile handed out
+  uint32_t* tile_lt;    // [max_tiles] its index within the stream
+  uint64_t* lvl_cnt;    // [levels + 1] streams with more than l tiles
+  uint64_t* lvl_base;   // [levels + 1]
   uint32_t* sb_pos;     // [max_sb + B]
   uint32_t* counter;    // [1]
   // segmented decode (L != 0)
@@ -76,6 +79,7 @@ struct Workspace {
   uint64_t bytes;
   uint64_t max_tiles;
   uint64_t units_max;
+  uint32_t levels;      // most tiles a stream can have
 };
 
 __host__ __device__ inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
@@ -92,7 +96,8 @@ __device__ __forceinline__ uint64_t clk() {
   return t;
 }
 
-Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks, uint32_t L, uint8_t* base) {
+Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples, uint32_t nblocks,
+                 uint32_t L, uint8_t* base) {
   const uint64_t B = nblocks;
   const uint64_t max_sb = total_samples / cfg->block_size + B * cfg->component_stream_count;
   const uint64_t max_tiles = max_sb / kTile + B;
@@ -109,6 +114,10 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks
   w.tile_base = reinterpret_cast<uint64_t*>(take((B + 1) * 8));
   w.tile_state = reinterpret_cast<uint64_t*>(take(max_tiles * 8));
   w.tile_map = reinterpret_cast<uint32_t*>(take(max_tiles * 4));
+  w.tile_lt = reinterpret_cast<uint32_t*>(take(max_tiles * 4));
+  w.levels = (uint32_t)((max_stream_samples / cfg->block_size + 2) / kTile + 1);
+  w.lvl_cnt = reinterpret_cast<uint64_t*>(take(((uint64_t)w.levels + 1) * 8));
+  w.lvl_base = reinterpret_cast<uint64_t*>(take(((uint64_t)w.levels + 1) * 8));
   w.sb_pos = reinterpret_cast<uint32_t*>(take((max_sb + B) * 4));
   w.counter = reinterpret_cast<uint32_t*>(take(256));
   w.max_tiles = max_tiles;
@@ -140,23 +149,85 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks
 
 // sub-blocks + 1 (the end entry) and tiles of each stream; entry B is 0 so
 // that the exclusive scans end in the totals
+// (units: the segmented decode's units per stream; streams of one unit are
+// the fused kernel's and get no entries)
 __global__ void rpp_dec_count_kernel(const uint64_t* n_samples, uint32_t nblocks, uint32_t chunk_len, uint32_t cs,
-                                     uint64_t* sb_cnt, uint64_t* tile_cnt) {
+                                     uint64_t* sb_cnt, uint64_t* tile_cnt, const uint64_t* units) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nblocks) return;
   uint64_t nsb = 0;
   if (i < nblocks) {
     const uint64_t n = n_samples[i];
-    if (n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES) nsb = (n + chunk_len - 1) / chunk_len * cs;
+    if (n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES && (!units || units[i] > 1)) nsb = (n + chunk_len - 1) / chunk_len * cs;
   }
   sb_cnt[i] = i < nblocks ? nsb + 1 : 0;
   tile_cnt[i] = (nsb + kTile - 1) / kTile;
 }
 
-__global__ void rpp_dec_tile_map_kernel(const uint64_t* tile_base, uint32_t nblocks, uint32_t* tile_map) {
+// The caller's max_stream_samples bounds the tile levels: a stream longer
+// than it breaks the contract and is reported, not decoded.
+__global__ void rpp_dec_check_max_kernel(const uint64_t* n_samples, uint32_t nblocks, uint64_t max_stream_samples,
+                                         int32_t* status) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nblocks) return;
-  for (uint64_t t = tile_base[i]; t < tile_base[i + 1]; ++t) tile_map[t] = i;
+  if (i < nblocks && n_samples[i] > max_stream_samples) status[i] = RPP_INVALID_ARGUMENT;
+}
+
+// Tiles are handed out level by level: tile l of every stream before tile
+// l + 1 of any (a stream's tiles stay in order, as the look-back needs, and a
+// long stream has few tiles in flight at once, so its inclusive prefixes keep
+// up).  One workgroup per level: streams with more than l tiles, counted, then
+// ranked by a block scan.
+constexpr uint32_t kLvlThreads = 256;
+__device__ __forceinline__ uint32_t block_excl_scan_flag(bool f, uint32_t* sh, uint32_t& total) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint64_t m = __ballot(f);
+  const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (lane == 0) sh[wv] = (uint32_t)__builtin_popcountll(m);
+  __syncthreads();
+  uint32_t off = 0;
+  total = 0;
+  for (uint32_t i = 0; i < kLvlThreads / 64; ++i) {
+    off += i < wv ? sh[i] : 0u;
+    total += sh[i];
+  }
+  __syncthreads();
+  return off + before;
+}
+
+__global__ __launch_bounds__(kLvlThreads) void rpp_dec_level_count_kernel(const uint64_t* tile_cnt, uint32_t nblocks,
+                                                                          uint32_t levels, uint64_t* lvl_cnt) {
+  __shared__ uint32_t sh[kLvlThreads / 64];
+  const uint32_t l = blockIdx.x;
+  if (l > levels) return;
+  uint64_t n = 0;
+  if (l < levels)
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += kLvlThreads) {
+      const uint32_t b = b0 + threadIdx.x;
+      uint32_t total;
+      block_excl_scan_flag(b < nblocks && tile_cnt[b] > l, sh, total);
+      n += total;
+    }
+  if (threadIdx.x == 0) lvl_cnt[l] = n;
+}
+
+__global__ __launch_bounds__(kLvlThreads) void rpp_dec_level_map_kernel(const uint64_t* tile_cnt, uint32_t nblocks,
+                                                                        uint32_t levels, const uint64_t* lvl_base,
+                                                                        uint32_t* tile_map, uint32_t* tile_lt) {
+  __shared__ uint32_t sh[kLvlThreads / 64];
+  const uint32_t l = blockIdx.x;
+  if (l >= levels) return;
+  uint64_t r = lvl_base[l];
+  for (uint32_t b0 = 0; b0 < nblocks; b0 += kLvlThreads) {
+    const uint32_t b = b0 + threadIdx.x;
+    const bool f = b < nblocks && tile_cnt[b] > l;
+    uint32_t total;
+    const uint32_t at = block_excl_scan_flag(f, sh, total);
+    if (f) {
+      tile_map[r + at] = b;
+      tile_lt[r + at] = l;
+    }
+    r += total;
+  }
 }
 
 struct ExtractParams {
@@ -171,6 +242,8 @@ struct ExtractParams {
   const uint64_t* sb_base;
   const uint64_t* tile_base;
   const uint32_t* tile_map;
+  const uint32_t* tile_lt;
+  const uint64_t* n_tiles;  // tiles handed out (the level map's total)
   uint64_t* tile_state;
   uint32_t* counter;
   uint32_t nblocks;
@@ -301,12 +374,13 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t stage[kStageWords + kStagePad];
   __shared__ uint32_t scan_buf[kTile];
   __shared__ uint32_t sh_tile, sh_carry[2], sh_min;
+  __shared__ uint32_t wtot[kTile / 64][2];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = __lane_id();
   const uint32_t be = p.be, ulsb = p.ulsb;
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;  // byte-swap each half
   const uint32_t chunk_len = CS * BS;
-  const uint64_t total_tiles = p.tile_base[p.nblocks];
+  const uint64_t total_tiles = *p.n_tiles;
 
   const bool timing = (p.dbg & 4) && tid < 64;
   uint64_t tp = timing ? clk() : 0;
@@ -320,10 +394,11 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
   for (;;) {
     if (tid == 0) sh_tile = atomicAdd(p.counter, 1u);
     __syncthreads();
-    const uint32_t t = sh_tile;
-    if (t >= total_tiles) return;  // (uniform)
-    const uint32_t b = p.tile_map[t];
-    const uint32_t lt = (uint32_t)(t - p.tile_base[b]);
+    const uint32_t tg = sh_tile;
+    if (tg >= total_tiles) return;  // (uniform)
+    const uint32_t b = p.tile_map[tg];
+    const uint32_t lt = p.tile_lt[tg];
+    const uint32_t t = (uint32_t)p.tile_base[b] + lt;  // the tile's state slot (stream-major)
     if (p.status[b] != RPP_OK) {  // the parse failed: nothing to decode
       if (tid == 0) __hip_atomic_store(&p.tile_state[t], kFlagIncl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
@@ -429,13 +504,21 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
     if (active && !fast) agg = decode_general<false>(rd, start, n, 0, nullptr, CS, be, ulsb);
 
     stamp(2);
-    // ---- scan of the elements within the tile (per component: stride CS) ----
-    scan_buf[tid] = agg;
-    __syncthreads();
-    for (uint32_t d = CS; d < kTile; d <<= 1) {
-      const uint32_t v = tid >= d ? combine(scan_buf[tid - d], scan_buf[tid]) : scan_buf[tid];
+    // ---- scan of the elements within the tile (per component: stride CS):
+    //      a shuffle scan per wave, then the wave totals through LDS ----
+    {
+      const uint32_t l = tid & 63u, wv = tid >> 6;
+      uint32_t v = agg;
+#pragma unroll
+      for (uint32_t d = CS; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)v, d);
+        if (l >= d) v = combine(y, v);
+      }
+      if (l >= 64 - CS) wtot[wv][l - (64 - CS)] = v;
       __syncthreads();
-      scan_buf[tid] = v;
+      uint32_t pre = 0;
+      for (uint32_t w = 0; w < wv; ++w) pre = combine(pre, wtot[w][comp]);
+      scan_buf[tid] = combine(pre, v);
       __syncthreads();
     }
     // ---- tile carry: decoupled look-back over the stream's earlier tiles,
@@ -452,7 +535,7 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
         e1 = kSet | (uint32_t)((x >> 16) & 0xFFFFu);
       } else {
         if (tid == 0)
-          __hip_atomic_store(&p.tile_state[t], pack_state(a0, a1, kFlagAgg), __ATOMIC_RELEASE,
+          __hip_atomic_store(&p.tile_state[t], pack_state(a0, a1, kFlagAgg), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         uint32_t x0 = 0, x1 = 0;  // identity: the tiles after the current window
         const uint32_t tfirst = t - lt;  // the stream's first tile (publishes its inclusive prefix)
@@ -461,7 +544,9 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
           uint64_t s = 0;
           if (valid) {
             do {
-              s = __hip_atomic_load(&p.tile_state[jt - tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+              // (relaxed: the state word carries its payload, no other data is
+              // published with it)
+              s = __hip_atomic_load(&p.tile_state[jt - tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               if (!(s >> 62)) __builtin_amdgcn_s_sleep(1);
             } while (!(s >> 62));
           }
@@ -484,7 +569,7 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
       }
       if (tid == 0) {
         __hip_atomic_store(&p.tile_state[t], pack_state(combine(e0, a0), combine(e1, a1), kFlagIncl),
-                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sh_carry[0] = e0;
         sh_carry[1] = e1;
       }
@@ -496,6 +581,11 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
 
     stamp(3);
     // ---- stores ----
+    // general lanes first: they read the staged words once more
+    if (active && !fast) decode_general<true>(rd, start, n, carry, out + cbase + comp, CS, be, ulsb);
+    // fast lanes: their BS samples, in output order (lane k's BS samples are
+    // output samples [k BS, (k+1) BS) of the tile for either CS)
+    uint32_t o32[BS / 2];
     if (fast) {
       const uint32_t c2 = carry * 0x10001u;
 #pragma unroll
@@ -504,22 +594,14 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
         r[i] = px_write2<SH>(__builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, r[i]) + __builtin_bit_cast(us2, c2)),
                              selbe, ulsb);
       }
-      if (p.dbg & 2) {
+      if constexpr (CS == 1) {
 #pragma unroll
-        for (uint32_t i = 0; i < BS / 2; ++i) {
-          out[cbase + comp + CS * 2 * i] = (uint16_t)r[i];
-          out[cbase + comp + CS * (2 * i + 1)] = (uint16_t)(r[i] >> 16);
-        }
-      } else if constexpr (CS == 1) {
-        uint4* o = reinterpret_cast<uint4*>(out + (size_t)k * BS);
-#pragma unroll
-        for (uint32_t i = 0; i < BS / 8; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+        for (uint32_t i = 0; i < BS / 2; ++i) o32[i] = r[i];
       } else {
         // lane 2c holds component 0 of chunk c, lane 2c+1 component 1; the
-        // chunk interleaves them.  The even lane writes chunk dwords
-        // [0, BS/2), the odd lane [BS/2, BS); dword j = (c0[j], c1[j]).
+        // chunk interleaves them.  The even lane takes chunk dwords [0, BS/2),
+        // the odd lane [BS/2, BS); dword j = (c0[j], c1[j]).
         const bool odd = tid & 1u;
-        uint32_t o32[BS / 2];
 #pragma unroll
         for (uint32_t i = 0; i < BS / 4; ++i) {
           const uint32_t own = odd ? r[BS / 4 + i] : r[i];
@@ -529,13 +611,47 @@ __global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
           o32[2 * i] = __builtin_amdgcn_perm(c1, c0, 0x05040100u);      // (c0.lo, c1.lo)
           o32[2 * i + 1] = __builtin_amdgcn_perm(c1, c0, 0x07060302u);  // (c0.hi, c1.hi)
         }
-        uint4* o = reinterpret_cast<uint4*>(out + (size_t)(k / 2) * chunk_len + (odd ? BS : 0));
-#pragma unroll
-        for (uint32_t i = 0; i < BS / 8; ++i)
-          o[i] = make_uint4(o32[4 * i], o32[4 * i + 1], o32[4 * i + 2], o32[4 * i + 3]);
       }
-    } else if (active) {
-      decode_general<true>(rd, start, n, carry, out + cbase + comp, CS, be, ulsb);
+    }
+    if (p.dbg & 2) {
+      if (fast)
+        for (uint32_t i = 0; i < BS / 2; ++i) {
+          out[(size_t)k * BS + 2 * i] = (uint16_t)o32[i];
+          out[(size_t)k * BS + 2 * i + 1] = (uint16_t)(o32[i] >> 16);
+        }
+    } else if constexpr (BS >= 64) {
+      // Through LDS, so that every store instruction writes whole 128-byte
+      // lines: each wave puts 128 bytes of each lane in a row of its own
+      // quarter of the stage (rows padded to 144 bytes), then eight lanes
+      // store one row.
+      constexpr uint32_t kRow = 36;
+      __syncthreads();  // (the staged words are read no more)
+      const uint32_t l = tid & 63u, wv = tid >> 6;
+      uint32_t* tr = stage + wv * 64 * kRow;
+      const uint64_t fm = __ballot(fast);
+      uint16_t* const wout = out + (size_t)(k0 + 64 * wv) * BS;
+#pragma unroll
+      for (uint32_t h = 0; h < BS / 64; ++h) {
+        if (fast) {
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j)
+            *reinterpret_cast<uint4*>(tr + l * kRow + 4 * j) =
+                make_uint4(o32[32 * h + 4 * j], o32[32 * h + 4 * j + 1], o32[32 * h + 4 * j + 2], o32[32 * h + 4 * j + 3]);
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+          const uint32_t row = 8 * i + (l >> 3), c = l & 7u;
+          if ((fm >> row) & 1u)
+            *reinterpret_cast<uint4*>(wout + (size_t)row * BS + 64 * h + 8 * c) =
+                *reinterpret_cast<const uint4*>(tr + row * kRow + 4 * c);
+        }
+        asm volatile("" ::: "memory");
+      }
+    } else if (fast) {
+      uint4* o = reinterpret_cast<uint4*>(out + (size_t)k * BS);
+#pragma unroll
+      for (uint32_t i = 0; i < BS / 8; ++i) o[i] = make_uint4(o32[4 * i], o32[4 * i + 1], o32[4 * i + 2], o32[4 * i + 3]);
     }
     __syncthreads();  // (stage and scan_buf are reused by the next tile)
     stamp(4);
@@ -941,9 +1057,11 @@ uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t ma
     if (max_stream_samples < (1u << 18)) return 0;
     if (max_stream_samples * 1024 < total_samples) return 0;
   }
-  // about 4096 units for the batch (16 bits per sample at most), 2^20..2^23 bits
+  // about 8192 units for the batch (8 bits per sample: Poisson-like data
+  // compresses to 7-8), 2^20..2^23 bits; streams that fit one unit stay on
+  // the fused kernel
   uint32_t L = 20;
-  while (L < 23 && ((total_samples * 16) >> L) > 4096) ++L;
+  while (L < 23 && ((total_samples * 8) >> L) > 8192) ++L;
   if (const char* l = getenv("RICEPP_SEG_LOG2")) L = (uint32_t)std::min(26, std::max(10, atoi(l)));
   return L;
 }
@@ -976,7 +1094,7 @@ uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_sample
   if (rpp_check_config(cfg) != RPP_OK) return 0;
   const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples);
   if (!L && !two_stage(cfg)) return 0;  // the fused kernel needs none
-  return layout(cfg, total_samples, nblocks, L, nullptr).bytes;
+  return layout(cfg, total_samples, max_stream_samples, nblocks, L, nullptr).bytes;
 }
 
 int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
@@ -993,26 +1111,14 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
   if (!L && !two_stage(cfg))
     return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
                                              d_n_samples, d_status, s);
-  const Workspace w = layout(cfg, total_samples, nblocks, L, static_cast<uint8_t*>(d_workspace));
+  const Workspace w = layout(cfg, total_samples, max_stream_samples, nblocks, L, static_cast<uint8_t*>(d_workspace));
   if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
   const uint32_t chunk_len = cfg->block_size * cfg->component_stream_count;
   const uint32_t g256 = (nblocks + 256) / 256;
-  hipLaunchKernelGGL(rpp_dec_count_kernel, dim3(g256), dim3(256), 0, s, d_n_samples, nblocks, chunk_len,
-                     cfg->component_stream_count, w.sb_cnt, w.tile_cnt);
-  if ((st = rpp_exclusive_scan_u64(w.sb_cnt, (uint64_t)nblocks + 1, w.sb_base, s)) != RPP_OK) return st;
-  if ((st = rpp_exclusive_scan_u64(w.tile_cnt, (uint64_t)nblocks + 1, w.tile_base, s)) != RPP_OK) return st;
-  hipLaunchKernelGGL(rpp_dec_tile_map_kernel, dim3(g256), dim3(256), 0, s, w.tile_base, nblocks, w.tile_map);
-  if (hipMemsetAsync(w.tile_state, 0, w.max_tiles * 8, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (hipMemsetAsync(w.counter, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (!L) {
-    st = rpp_internal::launch_parse(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base, w.sb_pos,
-                                    d_status, s);
-    if (st != RPP_OK) return st;
-  } else {
-    const uint64_t U = w.units_max;
-    SegArgs a{};
+  SegArgs a{};
+  if (L) {
     a.sv = rpp_internal::SegView{w.unit_map, w.unit_base, w.bm_base, w.bitmap, w.ovr, w.ustate, w.ulo, w.uov,
-                                 w.sst, w.sflags, L, 0, (uint32_t)U};
+                                 w.sst, w.sflags, L, 0, (uint32_t)w.units_max};
     a.in = d_in;
     a.in_off = d_in_offsets;
     a.in_bytes = d_in_bytes;
@@ -1028,15 +1134,37 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
     a.cs = cfg->component_stream_count;
     hipLaunchKernelGGL(rpp_seg_units_kernel, dim3(g256), dim3(256), 0, s, a, w.ucnt);
     if ((st = rpp_exclusive_scan_u64(w.ucnt, (uint64_t)nblocks + 1, w.unit_base, s)) != RPP_OK) return st;
+  }
+  hipLaunchKernelGGL(rpp_dec_count_kernel, dim3(g256), dim3(256), 0, s, d_n_samples, nblocks, chunk_len,
+                     cfg->component_stream_count, w.sb_cnt, w.tile_cnt, L ? (const uint64_t*)w.ucnt : nullptr);
+  if ((st = rpp_exclusive_scan_u64(w.sb_cnt, (uint64_t)nblocks + 1, w.sb_base, s)) != RPP_OK) return st;
+  if ((st = rpp_exclusive_scan_u64(w.tile_cnt, (uint64_t)nblocks + 1, w.tile_base, s)) != RPP_OK) return st;
+  hipLaunchKernelGGL(rpp_dec_level_count_kernel, dim3(w.levels + 1), dim3(kLvlThreads), 0, s, w.tile_cnt, nblocks,
+                     w.levels, w.lvl_cnt);
+  if ((st = rpp_exclusive_scan_u64(w.lvl_cnt, (uint64_t)w.levels + 1, w.lvl_base, s)) != RPP_OK) return st;
+  hipLaunchKernelGGL(rpp_dec_level_map_kernel, dim3(w.levels), dim3(kLvlThreads), 0, s, w.tile_cnt, nblocks,
+                     w.levels, w.lvl_base, w.tile_map, w.tile_lt);
+  if (hipMemsetAsync(w.tile_state, 0, w.max_tiles * 8, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (hipMemsetAsync(w.counter, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (!L) {
+    st = rpp_internal::launch_parse(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base, w.sb_pos,
+                                    d_status, s);
+    if (st != RPP_OK) return st;
+  } else {
+    const uint64_t U = w.units_max;
+    // the streams that fit one unit: one wave each, parse and values fused
+    st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
+                                           d_n_samples, d_status, s, false, w.ucnt);
+    if (st != RPP_OK) return st;
     if (hipMemsetAsync(w.bm_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.cnt2, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.sst, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
     hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.bm_cnt);
     if ((st = rpp_exclusive_scan_u64(w.bm_cnt, U + 1, w.bm_base, s)) != RPP_OK) return st;
-    // pass 0: every unit; three rerun passes; a serial pass for what is left
     if (hipMemsetAsync(w.ustate, 0xFF, U * 16, s) != hipSuccess) return RPP_HIP_ERROR;
     const uint32_t gu = (uint32_t)((U + 255) / 256);
+    // pass 0: every unit; three rerun passes; a serial pass for what is left
     for (uint32_t pass : {0u, 1u, 1u, 1u, 2u}) {
       a.sv.pass = pass;  // (the stitch counts the reruns it asks this pass for)
       if (pass != 0) {
@@ -1059,16 +1187,21 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
                               : (sh ? extract_kernel_for<2, true>(cfg->block_size)
                                     : extract_kernel_for<2, false>(cfg->block_size));
   ExtractParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_out, d_out_offsets, d_status, w.sb_pos, w.sb_base,
-                  w.tile_base, w.tile_map, w.tile_state, w.counter, nblocks, cfg->block_size,
+                  w.tile_base, w.tile_map, w.tile_lt, w.lvl_base + w.levels, w.tile_state, w.counter, nblocks,
+                  cfg->block_size,
                   cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count, 0u};
   if (const char* e = getenv("RICEPP_DEC2_DBG")) p.dbg = (uint32_t)atoi(e);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(w.max_tiles, kMaxExtractGrid);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kTile), 0, s, p);
   if (hipGetLastError() != hipSuccess) return RPP_HIP_ERROR;
-  if (L)  // streams whose exact chain left the region the units cover (malformed input)
-    return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                             d_n_samples, d_status, s, true);
-  return RPP_OK;
+  if (L) {  // streams whose exact chain left the region the units cover (malformed input)
+    st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
+                                           d_n_samples, d_status, s, true);
+    if (st != RPP_OK) return st;
+  }
+  hipLaunchKernelGGL(rpp_dec_check_max_kernel, dim3(g256), dim3(256), 0, s, d_n_samples, nblocks, max_stream_samples,
+                     d_status);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
 // Without a workspace: the fused kernel (no host synchronisation), or, with

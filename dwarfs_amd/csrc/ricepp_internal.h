@@ -59,10 +59,12 @@ __host__ __device__ inline uint32_t seg_last_bit(uint32_t mis, uint64_t in_bytes
 }
 
 // rpp_decode_kernel: one wave per stream, parse and values fused (any bs).
-// only_fallback: decode only the streams whose status is kSegFallback.
+// only_fallback: decode only the streams whose status is kSegFallback;
+// d_units (the segmented decode's units per stream): skip split streams.
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
-                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback = false);
+                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback = false,
+                        const uint64_t* d_units = nullptr);
 
 // rpp_parse_kernel: sub-block start positions of every stream into sb_pos
 // (stream b's entries from sb_base[b]: nsb_b header positions, then the end).
@@ -70,8 +72,8 @@ int launch_parse(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_i
                  uint32_t nblocks, const uint64_t* d_n_samples, const uint64_t* d_sb_base, uint32_t* d_sb_pos,
                  int32_t* d_status, hipStream_t stream);
 
-// The same kernel over units (SegView): single-unit streams exactly as
-// launch_parse; units of split streams into the bitmaps and overshoot lists.
+// The same kernel over units (SegView): the units of split streams, into the
+// bitmaps and overshoot lists (single-unit streams are left to the fused kernel).
 int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples,
                      const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,

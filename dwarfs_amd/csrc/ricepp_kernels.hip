@@ -886,6 +886,7 @@ struct DecParams {
   uint32_t bs, cs, be, ulsb;
   uint32_t waves;          // waves (streams) per workgroup
   uint32_t only_fallback;  // decode only streams whose status is kSegFallback
+  const uint64_t* units;   // non-null: skip streams split into more than one unit (segmented decode)
 };
 
 // ---- transfer tables (built at compile time) ----
@@ -1151,6 +1152,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint32_t b = blockIdx.x * p.waves + wv;
   if (b >= p.nblocks) return;  // no barrier below this point
   if (p.only_fallback && p.status[b] != rpp_internal::kSegFallback) return;
+  if (p.units && p.units[b] > 1) return;
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
   unsigned long long tprev_;
@@ -1991,7 +1993,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     u0 = (uint32_t)p.sv.unit_base[b];
     nunits = (uint32_t)p.sv.unit_base[b + 1] - u0;
     ju = u - u0;
-    if (p.sv.pass != 0 && (nunits == 1 || p.sv.ustate[4 * u + kUsRerun] == kSegNone)) return;
+    if (nunits == 1) return;  // (decoded by the fused kernel)
+    if (p.sv.pass != 0 && p.sv.ustate[4 * u + kUsRerun] == kSegNone) return;
   } else {
     if (b >= p.nblocks) return;  // no barrier below this point
   }
@@ -2524,7 +2527,8 @@ namespace rpp_internal {
 
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
-                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback) {
+                        const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback,
+                        const uint64_t* d_units) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
   if (nblocks == 0) return RPP_OK;
@@ -2548,7 +2552,7 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
   if (attr_err != hipSuccess) return RPP_HIP_ERROR;
   DecParams p{d_in, d_in_offsets, d_in_bytes, d_out, d_out_offsets, d_n_samples, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count, W, only_fallback ? 1u : 0u};
+              cfg->unused_lsb_count, W, only_fallback ? 1u : 0u, d_units};
   const auto k = kernels[2 * (cfg->component_stream_count - 1) + (cfg->unused_lsb_count ? 1 : 0)];
   hipLaunchKernelGGL(k, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;

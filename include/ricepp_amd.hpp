@@ -30,7 +30,7 @@
 // (src/writer/filesystem_writer.cpp:255-287) and decompress blocks
 // concurrently (src/reader/internal/block_cache.cpp:628-706).  Concurrent
 // encode / decode calls with the same configuration on the same device are
-// coalesced into one rpp_encode_batch / rpp_decode_batch launch (a combining
+// coalesced into one rpp_encode_batch_ws / rpp_decode_batch_ws launch (a combining
 // queue: the first waiting caller launches everything queued, the other
 // callers copy their own data in and out of pinned staging in parallel).
 // Device contexts (stream, device and pinned staging) come from a per-device

@@ -1,5 +1,9 @@
 """Phase timers of the extraction kernel (RICEPP_DEC2_DBG=4): cycles per tile spent in setup, staging,
-decode, scan + look-back, stores, summed over the bench workload's decode launches."""
+decode, scan + look-back, stores, summed over three decode launches.
+
+usage: python tools/dec2_phases.py [bench|long]
+  bench  the bench workload (4096 x 64 KiB) through the two-stage decode
+  long   64 streams of 16 MiB (the segmented decode)"""
 import ctypes as C
 import os
 import sys
@@ -15,7 +19,12 @@ from bench import make_poisson_blocks  # noqa: E402
 from dwarfs_amd import _native as N  # noqa: E402
 from dwarfs_amd import codec, parallel  # noqa: E402
 
-nblocks, n = 4096, 32768
+layout = sys.argv[1] if len(sys.argv) > 1 else "bench"
+if layout == "bench":
+    os.environ["RICEPP_DECODE"] = "two-stage"
+    nblocks, n = 4096, 32768
+else:
+    nblocks, n = 64, 8 << 20
 dev = torch.device("cuda:0")
 x = make_poisson_blocks(nblocks, n, 1000.0, 42, dev)
 pipe = parallel.ShardPipeline(codec.CodecConfig(128, 1, "big", 0), x, np.arange(nblocks, dtype=np.int64) * n,

@@ -9,6 +9,8 @@ the headline bench line is bench.py).  Each case prints one JSON line.
            samples (8 GiB), cut into 1 MiB DwarFS blocks (mkdwarfs -S 20),
            pre-encoded (by the GPU encoder, byte-identical to CPU ricepp per
            the parity tests)
+  frames   configs[2] as whole frames: the same 256 frames, one 32 MiB
+           stream each (the segmented decode splits them into units)
   mix      configs[3]: the per-GPU share of a 32 GiB 1/4/16 MiB block mix
            (4 GiB: equal bytes per size class), encode + decode
   sweep    configs[4]: bs {16, 32, 128} x component bits {10, 12, 14, 16}
@@ -131,6 +133,23 @@ def case_fits():
            roofline_frac=round((raw + comp) / td / 1e9 / 8000.0, 4))
 
 
+def case_frames():
+    """configs[2] with one stream per frame: 256 whole 4096x4096 frames (32 MiB each), decode only
+    (the segmented decode splits every frame into units)."""
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    frames, fs = 256, 4096 * 4096
+    n = frames * fs
+    x = poisson_scaled(n, 1000.0, 0, 42)
+    p = pipe_for(cfg, x, [fs] * frames)
+    comp = int(p.sizes.sum())
+    raw = n * 2
+    td = timed(p.decode, iters=3)
+    report("frames", frames=frames, block="one 32 MiB stream per frame", raw_GiB=raw / GIB,
+           ratio=round(comp / raw, 4), decode_GiBps=round(raw / td / GIB, 2), decode_ms=round(td * 1e3, 2),
+           hbm_GBps_algorithmic=round((raw + comp) / td / 1e9, 1),
+           roofline_frac=round((raw + comp) / td / 1e9 / 8000.0, 4))
+
+
 def case_mix():
     cfg = codec.CodecConfig(128, 1, "big", 0)
     per_class = 1344 * 2**20 // 2  # samples per size class (4032 MiB per GPU in total)
@@ -198,7 +217,8 @@ def case_e2e():
            transfer_bytes_note="encode D2H copies the worst-case-strided image (raw size + framing)")
 
 
-CASES = {"gen": case_gen, "fits": case_fits, "mix": case_mix, "sweep": case_sweep, "e2e": case_e2e}
+CASES = {"gen": case_gen, "fits": case_fits, "frames": case_frames, "mix": case_mix, "sweep": case_sweep,
+         "e2e": case_e2e}
 
 if __name__ == "__main__":
     for name in sys.argv[1:] or list(CASES):
