@@ -370,7 +370,7 @@ __device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t sel, uint32_t
 }
 
 template <uint32_t CS, uint32_t BS, bool SH>
-__global__ __launch_bounds__(kTile) void rpp_extract_kernel(ExtractParams p) {
+__global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t stage[kStageWords + kStagePad];
   __shared__ uint32_t scan_buf[kTile];
   __shared__ uint32_t sh_tile, sh_carry[2], sh_min;

@@ -23,7 +23,9 @@ namespace rpp_internal {
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegOvr = 16;             // headers recorded past a unit's region
 constexpr uint32_t kSegNone = 0xFFFFFFFFu;   // no position
-constexpr uint32_t kSpecSteps = 12;          // sub-blocks a guessed first header must chain through
+constexpr uint32_t kSpecSteps = 12;          // sub-blocks a candidate first header must chain through
+constexpr uint32_t kSpecVerify = 24;         // ... and the unit's own parse then checks (< 64)
+constexpr uint32_t kGuessRetries = 8;        // next candidates tried after a rejected guess
 constexpr int32_t kSegFallback = 0x7F5E0001;  // internal status: decode this stream with the fused kernel
 
 // per-unit state words (SegView::ustate[4 u + i])

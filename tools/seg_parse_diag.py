@@ -36,11 +36,11 @@ def run(name, blocks):
     ev[1].record()
     torch.cuda.synchronize()
     N.lib().rpp_parse_diag_read(buf, 1)
-    g, ch, sb, un, nch, nst, nsl, _ = map(int, buf)
+    g, ch, sb, un, nch, nst, nsl, reg = map(int, buf)
     print(f"{name}: {ev[0].elapsed_time(ev[1]):.3f} ms, units {un}, sub-blocks {sb}, "
           f"guess {g / max(un, 1) / 100:.1f} us/unit, chain {ch / max(un, 1) / 100:.1f} us/unit = "
           f"{ch / max(sb, 1) * 10:.0f} ns/sub-block; per guess {nch / max(un, 1):.2f} chunks {nst / max(un, 1):.1f} steps "
-          f"{nsl / max(un, 1):.1f} slot-steps, exact {torch.equal(out[:sum(ns)], x)}, "
+          f"{nsl / max(un, 1):.1f} slot-steps, re-guesses {reg}, exact {torch.equal(out[:sum(ns)], x)}, "
           f"{codec.segmented_decode_stats()}", flush=True)
 
 
