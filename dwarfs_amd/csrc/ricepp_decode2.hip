@@ -1057,11 +1057,13 @@ uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t ma
     if (max_stream_samples < (1u << 18)) return 0;
     if (max_stream_samples * 1024 < total_samples) return 0;
   }
-  // about 8192 units for the batch (8 bits per sample: Poisson-like data
-  // compresses to 7-8), 2^20..2^23 bits; streams that fit one unit stay on
-  // the fused kernel
-  uint32_t L = 20;
-  while (L < 23 && ((total_samples * 8) >> L) > 8192) ++L;
+  // about 4096 units for the batch (8 bits per sample: Poisson-like data
+  // compresses to 7-8), 2^18..2^23 bits (a unit's guess costs about as much
+  // as parsing 2^20 bits, so small batches take small units for parallelism
+  // and big ones large units); streams that fit one unit stay on the fused
+  // kernel
+  uint32_t L = 18;
+  while (L < 23 && ((total_samples * 8) >> L) > 4096) ++L;
   if (const char* l = getenv("RICEPP_SEG_LOG2")) L = (uint32_t)std::min(26, std::max(10, atoi(l)));
   return L;
 }

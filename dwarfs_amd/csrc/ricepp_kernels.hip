@@ -2056,7 +2056,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     return g == kSegNone ? kSegNone : S + g;
   };
   uint32_t P = 8u * mis + 16u * CS;  // codec.h:81-86: the initial values
-  bool guessed = false;
+  bool guessed = false;     // (verify the chain from P)
+  uint32_t P_first = 0;     // the first guess, taken unverified if no later candidate verifies
   uint32_t* const us = p.sv.ustate + 4 * u;
   if (multi) {
     uint32_t flags = 0;
@@ -2064,7 +2065,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       P = us[kUsRerun];  // a header of the exact chain (stitch)
       flags = kUfRerunDone;
     } else if (ju != 0) {
-      P = do_guess(0);
+      P = P_first = do_guess(0);
       guessed = true;
       if (P == kSegNone) flags = kUfNoGuess;
     }
@@ -2434,14 +2435,11 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       ring_keep(P);
     }
     retire();
-    if (vfail) {  // the guess was wrong: the next candidate that chains
+    if (vfail) {  // the guess failed its check: the next candidate that chains
       P = attempt < kGuessRetries ? do_guess(P0 - S + 1) : kSegNone;
-      if (P == kSegNone) {
-        if (lane == 0) {
-          us[kUsStart] = kSegNone;
-          us[kUsFlags] |= kUfNoGuess;
-        }
-        return;
+      if (P == kSegNone) {  // none: the first guess after all (its chain may just vary more)
+        P = P_first;
+        guessed = false;
       }
       continue;
     }

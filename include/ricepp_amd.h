@@ -162,7 +162,7 @@ uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_sample
  * d_n_samples and max_stream_samples >= the largest.  Fully asynchronous on
  * `stream` (graph-capturable).  A batch whose longest stream holds more than
  * 1/1024 of its samples (and >= 2^18) is decoded segmented (bs 16/32/64/128):
- * long streams are cut into units of 2^20..2^23 bits parsed by one wave each
+ * long streams are cut into units of 2^18..2^23 bits parsed by one wave each
  * from a guessed first header, stitched exactly, then every sub-block of
  * every stream is decoded by its own lane; other batches one wave per stream.
  */
