@@ -64,14 +64,14 @@ struct Workspace {
   uint64_t* ucnt;       // [B + 1] units per stream
   uint64_t* unit_base;  // [B + 1]
   uint32_t* unit_map;   // [U_max]
-  uint64_t* bm_cnt;     // [U_max + 1] bitmap words per unit
-  uint64_t* bm_base;    // [U_max + 1]
-  uint32_t* bitmap;     // [bm_words]
+  uint64_t* pl_cnt;     // [U_max + 1] list capacity per unit
+  uint64_t* pl_base;    // [U_max + 1]
+  uint32_t* plist;      // [list entries]
   uint32_t* ovr;        // [U_max * kSegOvr]
   uint32_t* ustate;     // [U_max * 4]
   uint32_t* ulo;        // [U_max]
   uint32_t* uov;        // [U_max]
-  uint32_t* uhit;       // [U_max]
+  uint32_t* uhit;       // [2 U_max]: overshoot index, list index
   uint32_t* sst;        // [B]
   uint32_t* sflags;     // [B]
   uint64_t* cnt2;       // [U_max + 1] exact positions per unit
@@ -125,19 +125,19 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint64_t max_str
     // header bits of all streams: at most their worst-case sizes (seg_last_bit)
     const uint64_t bits = 8 * rpp_worst_case_bytes(cfg, total_samples) + 128 * B;
     const uint64_t U = B + (bits >> L) + 1;
-    const uint64_t words = (bits >> 5) + 8 * U;
+    const uint64_t entries = bits / std::max<uint32_t>(cfg->block_size, 32) + 68 * U;
     w.units_max = U;
     w.ucnt = reinterpret_cast<uint64_t*>(take((B + 1) * 8));
     w.unit_base = reinterpret_cast<uint64_t*>(take((B + 1) * 8));
     w.unit_map = reinterpret_cast<uint32_t*>(take(U * 4));
-    w.bm_cnt = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
-    w.bm_base = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
-    w.bitmap = reinterpret_cast<uint32_t*>(take(words * 4));
+    w.pl_cnt = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
+    w.pl_base = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
+    w.plist = reinterpret_cast<uint32_t*>(take(entries * 4));
     w.ovr = reinterpret_cast<uint32_t*>(take(U * rpp_internal::kSegOvr * 4));
-    w.ustate = reinterpret_cast<uint32_t*>(take(U * 16));
+    w.ustate = reinterpret_cast<uint32_t*>(take(U * rpp_internal::kUsWords * 4));
     w.ulo = reinterpret_cast<uint32_t*>(take(U * 4));
     w.uov = reinterpret_cast<uint32_t*>(take(U * 4));
-    w.uhit = reinterpret_cast<uint32_t*>(take(U * 4));
+    w.uhit = reinterpret_cast<uint32_t*>(take(U * 8));
     w.sst = reinterpret_cast<uint32_t*>(take(B * 4));
     w.sflags = reinterpret_cast<uint32_t*>(take(B * 4));
     w.cnt2 = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
@@ -348,6 +348,7 @@ __device__ uint32_t decode_general(const Reader& rd, uint32_t pos, uint32_t n, u
       }
       q += 32;
       pos += 32;
+      if (pos > 8u * rd.nbytes + 64u) break;  // (never for a parsed start: a bug may not hang the GPU)
     }
     const uint32_t d = (q << fs) | (rd.peek32(pos) & fmask);
     pos += fs;
@@ -543,12 +544,20 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
           const bool valid = tid <= jt - tfirst;
           uint64_t s = 0;
           if (valid) {
-            do {
-              // (relaxed: the state word carries its payload, no other data is
-              // published with it)
+            // (relaxed: the state word carries its payload, no other data is
+            // published with it; the load is coherent at agent scope (sc1).
+            // Bounded: a tile that never publishes is a bug, reported in
+            // g_dec2_diag[6], not a hung GPU.)
+            for (uint32_t spin = 0;; ++spin) {
               s = __hip_atomic_load(&p.tile_state[jt - tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (!(s >> 62)) __builtin_amdgcn_s_sleep(1);
-            } while (!(s >> 62));
+              if (s >> 62) break;
+              if (spin == (1u << 22)) {
+                atomicAdd(&g_dec2_diag[6], 1ull);
+                s = kFlagIncl;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+            }
           }
           const uint64_t incl = __ballot(valid && (s >> 62) == 2);
           const uint64_t vm = __ballot(valid);
@@ -701,9 +710,12 @@ __global__ void rpp_seg_units_kernel(SegArgs a, uint64_t* ucnt) {
   ucnt[i] = c;
 }
 
-// unit -> stream, and the bitmap words of each unit of a split stream
-// (its region [j 2^L, min((j+1) 2^L, last bit + 1)), a multiple of 4 words)
-__global__ void rpp_seg_map_kernel(SegArgs a, uint32_t* unit_map, uint64_t* bm_cnt) {
+// unit -> stream, and the list capacity of each unit of a split stream: one
+// header per max(bs, 32) bits of its region [j 2^L, min((j+1) 2^L, last bit
+// + 1)), i.e. the sub-blocks of data that codes to >= 1 bit per sample (>= 2
+// for bs 16; below that the stream goes to the fused kernel), a multiple of 4
+// entries
+__global__ void rpp_seg_map_kernel(SegArgs a, uint32_t* unit_map, uint64_t* pl_cnt) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.nblocks) return;
   const uint64_t u0 = a.sv.unit_base[i], nu = a.sv.unit_base[i + 1] - u0;
@@ -713,12 +725,12 @@ __global__ void rpp_seg_map_kernel(SegArgs a, uint32_t* unit_map, uint64_t* bm_c
     Eend = rpp_internal::seg_last_bit((uint32_t)(a.in_off[i] & 3u), a.in_bytes[i], a.n_samples[i], a.bs, a.cs);
   for (uint64_t k = 0; k < nu; ++k) {
     unit_map[u0 + k] = i;
-    uint64_t words = 0;
+    uint64_t cap = 0;
     if (nu > 1) {
       const uint64_t S = k << L, E = k + 1 == nu ? (uint64_t)Eend + 1 : S + (1ull << L);
-      words = align_up((E - S + 31) / 32, 4);
+      cap = align_up((E - S) / max(a.bs, 32u) + 64, 4);
     }
-    bm_cnt[u0 + k] = words;
+    pl_cnt[u0 + k] = cap;
   }
 }
 
@@ -738,13 +750,25 @@ __device__ __forceinline__ UnitGeo unit_geo(const SegArgs& a, uint32_t u) {
   return g;
 }
 
-__device__ __forceinline__ bool bm_test(const SegArgs& a, uint32_t u, uint32_t S, uint32_t pos) {
-  const uint32_t* bm = a.sv.bitmap + a.sv.bm_base[u];
-  return (bm[(pos - S) >> 5] >> (pos & 31u)) & 1u;
+__device__ __forceinline__ uint32_t us_word(const SegArgs& a, uint32_t u, uint32_t w) {
+  return a.sv.ustate[rpp_internal::kUsWords * u + w];
+}
+
+// index of `pos` in unit u's position list (ascending), or kSegNone
+__device__ __forceinline__ uint32_t list_find(const SegArgs& a, uint32_t u, uint32_t pos) {
+  const uint32_t* l = a.sv.plist + a.sv.pl_base[u];
+  uint32_t lo = 0, hi = us_word(a, u, rpp_internal::kUsNpos);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (l[mid] < pos) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < us_word(a, u, rpp_internal::kUsNpos) && l[lo] == pos ? lo : kSegNone;
 }
 
 // One thread per unit of a split stream (not yet resolved): the first of the
-// previous unit's overshoot headers that is also a header of this unit.
+// previous unit's overshoot headers that is also a header of this unit's
+// chain (i, and its index in the unit's list).
 __global__ void rpp_seg_hit_kernel(SegArgs a) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= a.sv.units_max || u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
@@ -752,18 +776,15 @@ __global__ void rpp_seg_hit_kernel(SegArgs a) {
   const uint32_t u0 = (uint32_t)a.sv.unit_base[b], nu = (uint32_t)a.sv.unit_base[b + 1] - u0;
   const uint32_t j = u - u0;
   if (nu <= 1 || j == 0 || j < a.sv.sst[b]) return;
-  const uint32_t L = a.sv.seg_log2, prev = u - 1;
-  const uint32_t S = j << L;
-  const uint32_t E = j + 1 == nu ? rpp_internal::seg_last_bit((uint32_t)(a.in_off[b] & 3u), a.in_bytes[b],
-                                                              a.n_samples[b], a.bs, a.cs) + 1
-                                 : S + (1u << L);
-  const uint32_t np = a.sv.ustate[4 * prev + rpp_internal::kUsNovr];
-  uint32_t hit = kSegNone;
+  const uint32_t prev = u - 1;
+  const uint32_t np = us_word(a, prev, rpp_internal::kUsNovr);
+  uint32_t hit = kSegNone, at = kSegNone;
   for (uint32_t i = 0; i < np && hit == kSegNone; ++i) {
-    const uint32_t o = a.sv.ovr[kSegOvr * prev + i];
-    if (o >= S && o < E && bm_test(a, u, S, o)) hit = i;
+    at = list_find(a, u, a.sv.ovr[kSegOvr * prev + i]);
+    if (at != kSegNone) hit = i;
   }
   a.uhit[u] = hit;
+  a.uhit[a.sv.units_max + u] = at;
 }
 
 // One wave per split stream, 64 units at a time from the first unresolved
@@ -772,7 +793,8 @@ __global__ void rpp_seg_hit_kernel(SegArgs a) {
 // there on the unit's positions are exact.  The first unit without a meeting
 // decides the rest: if the previous chain stopped early the stream ended
 // there; else the unit is parsed again from the last overshoot header (a
-// rerun pass) and the stitch resumes there next time.
+// rerun pass) and the stitch resumes there next time.  ulo = the list index
+// where the unit's exact positions start.
 __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
   using namespace rpp_internal;
   const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -780,8 +802,16 @@ __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
   const uint32_t u0 = (uint32_t)a.sv.unit_base[b], nu = (uint32_t)a.sv.unit_base[b + 1] - u0;
   uint32_t j0 = a.sv.sst[b];
   if (nu <= 1 || j0 >= nu) return;
+  if (a.sv.sflags[b] & kSfListFull) {  // the fused kernel decodes this stream
+    for (uint32_t k = lane; k < nu; k += 64) {
+      a.sv.ulo[u0 + k] = kSegNone;
+      a.sv.uov[u0 + k] = 0;
+    }
+    if (lane == 0) a.sv.sst[b] = nu;
+    return;
+  }
   if (j0 == 0) {
-    if (lane == 0) a.sv.ulo[u0] = a.sv.ustate[4 * u0 + kUsStart];
+    if (lane == 0) a.sv.ulo[u0] = 0;
     j0 = 1;
   }
   enum { kOk, kEnd, kFail };
@@ -791,13 +821,13 @@ __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
     const uint32_t u = u0 + j, prev = u - 1;
     uint32_t cls = kOk, lo = 0, uovp = 0;
     if (in) {
-      const uint32_t np = a.sv.ustate[4 * prev + kUsNovr];
+      const uint32_t np = us_word(a, prev, kUsNovr);
       const uint32_t h = a.uhit[u];
-      if (a.sv.ustate[4 * u + kUsFlags] & kUfRerunDone) {  // parsed from the previous unit's last overshoot header
-        lo = a.sv.ustate[4 * u + kUsStart];
+      if (us_word(a, u, kUsFlags) & kUfRerunDone) {  // parsed from the previous unit's last overshoot header
+        lo = 0;
         uovp = kSegOvr - 1;
       } else if (h != kSegNone) {
-        lo = a.sv.ovr[kSegOvr * prev + h];
+        lo = a.uhit[a.sv.units_max + u];
         uovp = h;
       } else {
         cls = np < kSegOvr ? kEnd : kFail;
@@ -815,10 +845,10 @@ __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
     const uint32_t ce = __shfl((int)cls, (int)e);
     if (ce == kFail) {
       if (lane == e) {
-        a.sv.ustate[4 * u + kUsRerun] = a.sv.ovr[kSegOvr * prev + kSegOvr - 1];
+        a.sv.ustate[kUsWords * u + kUsRerun] = a.sv.ovr[kSegOvr * prev + kSegOvr - 1];
         a.sv.sst[b] = j;
         atomicAdd(&g_seg_diag[a.sv.pass == 2 ? 2 : 1], 1ull);
-        if (a.sv.ustate[4 * u + kUsFlags] & kUfNoGuess) atomicAdd(&g_seg_diag[4], 1ull);
+        if (us_word(a, u, kUsFlags) & kUfNoGuess) atomicAdd(&g_seg_diag[4], 1ull);
       }
       return;
     }
@@ -836,119 +866,44 @@ __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
   }
 }
 
-// exact positions of a unit in its bitmap: the words [wlo, whi), the first
-// masked below bit `lo`
-struct UnitSpan {
-  const uint32_t* bm;
-  uint32_t wlo, whi, lomask;
-};
-__device__ __forceinline__ UnitSpan unit_span(const SegArgs& a, uint32_t u, const UnitGeo& g, uint32_t lo) {
-  UnitSpan s{a.sv.bitmap + a.sv.bm_base[u], 0, 0, 0};
-  if (lo != kSegNone && lo < g.E) {
-    s.wlo = (lo - g.S) >> 5;
-    s.whi = (g.E - g.S + 31) >> 5;
-    s.lomask = ~0u << ((lo - g.S) & 31u);
-  }
-  return s;
-}
-
-__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* red) {
-  const uint32_t tid = threadIdx.x;
-#pragma unroll
-  for (int o = 32; o; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  uint32_t t = 0;
-  for (uint32_t i = 0; i < blockDim.x / 64; ++i) t += red[i];
-  return t;
-}
-
 constexpr uint32_t kSegThreads = 256;
 
 // exact positions per unit of a split stream (0 for other units)
-__global__ __launch_bounds__(kSegThreads) void rpp_seg_count_kernel(SegArgs a) {
-  __shared__ uint32_t red[kSegThreads / 64];
-  const uint32_t u = blockIdx.x;
-  if (u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
+__global__ void rpp_seg_count_kernel(SegArgs a) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= a.sv.units_max || u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
   const UnitGeo g = unit_geo(a, u);
-  if (g.nu <= 1) {
-    if (threadIdx.x == 0) a.cnt[u] = 0;
-    return;
-  }
   const uint32_t lo = a.sv.ulo[u];
-  const UnitSpan sp = unit_span(a, u, g, lo);
-  uint32_t c = 0;
-  for (uint32_t w = sp.wlo + threadIdx.x; w < sp.whi; w += kSegThreads) {
-    uint32_t x = sp.bm[w];
-    if (w == sp.wlo) x &= sp.lomask;
-    c += __builtin_popcount(x);
+  uint64_t c = 0;
+  if (g.nu > 1 && lo != kSegNone) {
+    const uint32_t n = us_word(a, u, rpp_internal::kUsNpos);
+    c = (n > lo ? n - lo : 0u) + a.sv.uov[u];
   }
-  c = block_sum_u32(c, red);
-  if (threadIdx.x == 0) a.cnt[u] = c + (lo != kSegNone ? a.sv.uov[u] : 0u);
+  a.cnt[u] = c;
 }
 
-// positions of each unit into the stream's sb_pos: the bitmap's set bits in
-// order (rounds of 4 consecutive words per thread, a block scan of their
-// counts per round), then its own overshoot entries; entries past the
-// stream's nsb + 1 are dropped
+// each unit's exact positions into the stream's sb_pos: its list from ulo,
+// then its own overshoot entries; entries past the stream's nsb + 1 dropped
 __global__ __launch_bounds__(kSegThreads) void rpp_seg_write_kernel(SegArgs a) {
-  __shared__ uint32_t wsum[kSegThreads / 64];
-  const uint32_t u = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t u = blockIdx.x, tid = threadIdx.x;
   if (u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
   const UnitGeo g = unit_geo(a, u);
   if (g.nu <= 1) return;
   const uint32_t lo = a.sv.ulo[u];
   if (lo == kSegNone) return;
-  const UnitSpan sp = unit_span(a, u, g, lo);
   const uint64_t N = a.n_samples[g.b];
   const uint32_t chunk_len = a.bs * a.cs;
   const uint64_t cap = (N + chunk_len - 1) / chunk_len * a.cs + 1;
   uint32_t* dst = a.sb_pos + a.sb_base[g.b];
   const uint64_t idx0 = a.off[u] - a.off[g.u0];
-  const uint32_t nw = sp.whi - sp.wlo;
-  uint64_t run = idx0;
-  for (uint32_t r0 = 0; r0 < nw && run < cap; r0 += 4 * kSegThreads) {
-    uint32_t x[4], c = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-      const uint32_t w = r0 + 4 * tid + q;
-      x[q] = w < nw ? sp.bm[sp.wlo + w] : 0u;
-      if (w == 0) x[q] &= sp.lomask;
-      c += __builtin_popcount(x[q]);
-    }
-    uint32_t incl = c;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-      if (lane >= (uint32_t)d) incl += y;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-    for (uint32_t i = 0; i < kSegThreads / 64; ++i) {
-      before += i < wv ? wsum[i] : 0u;
-      total += wsum[i];
-    }
-    uint64_t idx = run + before + incl - c;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-      const uint32_t w = r0 + 4 * tid + q;
-      uint32_t v = x[q];
-      while (v && idx < cap) {
-        dst[idx++] = g.S + 32u * (sp.wlo + w) + (uint32_t)__builtin_ctz(v);
-        v &= v - 1;
-      }
-    }
-    run += total;
-    __syncthreads();  // (wsum is reused)
-  }
-  const uint64_t bits_total = run - idx0;  // (all of them unless the cap cut the rounds short)
+  const uint32_t n = us_word(a, u, rpp_internal::kUsNpos);
+  const uint32_t nl = n > lo ? n - lo : 0u;
+  const uint32_t* l = a.sv.plist + a.sv.pl_base[u] + lo;
+  for (uint32_t i = tid; i < nl; i += kSegThreads)
+    if (idx0 + i < cap) dst[idx0 + i] = l[i];
   const uint32_t nov = a.sv.uov[u];
-  if (run < cap)
-    for (uint32_t i = tid; i < nov; i += kSegThreads) {
-      const uint64_t k = idx0 + bits_total + i;
-      if (k < cap) dst[k] = a.sv.ovr[kSegOvr * u + i];
-    }
+  for (uint32_t i = tid; i < nov; i += kSegThreads)
+    if (idx0 + nl + i < cap) dst[idx0 + nl + i] = a.sv.ovr[kSegOvr * u + i];
 }
 
 // One sub-block of n samples from bit `pos` (decode.h:42-83, positions only);
@@ -996,8 +951,10 @@ __global__ void rpp_seg_tail_kernel(SegArgs a) {
   const uint32_t rag = N % chunk_len;
   const uint64_t need = rag ? nsb - cs + 1 : nsb + 1;
   int32_t st = RPP_OK;
-  if (T < need) {
-    st = (a.sv.sflags[b] & 1u) ? kSegFallback : RPP_TRUNCATED_INPUT;
+  if (a.sv.sflags[b] & kSfListFull) {
+    st = kSegFallback;
+  } else if (T < need) {
+    st = (a.sv.sflags[b] & kSfPastRegion) ? kSegFallback : RPP_TRUNCATED_INPUT;
     if (st == kSegFallback) atomicAdd(&g_seg_diag[3], 1ull);
   } else if (rag) {
     const uint64_t ioff = a.in_off[b];
@@ -1119,7 +1076,7 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
   const uint32_t g256 = (nblocks + 256) / 256;
   SegArgs a{};
   if (L) {
-    a.sv = rpp_internal::SegView{w.unit_map, w.unit_base, w.bm_base, w.bitmap, w.ovr, w.ustate, w.ulo, w.uov,
+    a.sv = rpp_internal::SegView{w.unit_map, w.unit_base, w.pl_base, w.plist, w.ovr, w.ustate, w.ulo, w.uov,
                                  w.sst, w.sflags, L, 0, (uint32_t)w.units_max};
     a.in = d_in;
     a.in_off = d_in_offsets;
@@ -1158,13 +1115,13 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
     st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
                                            d_n_samples, d_status, s, false, w.ucnt);
     if (st != RPP_OK) return st;
-    if (hipMemsetAsync(w.bm_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
+    if (hipMemsetAsync(w.pl_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.cnt2, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.sst, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
-    hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.bm_cnt);
-    if ((st = rpp_exclusive_scan_u64(w.bm_cnt, U + 1, w.bm_base, s)) != RPP_OK) return st;
-    if (hipMemsetAsync(w.ustate, 0xFF, U * 16, s) != hipSuccess) return RPP_HIP_ERROR;
+    hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.pl_cnt);
+    if ((st = rpp_exclusive_scan_u64(w.pl_cnt, U + 1, w.pl_base, s)) != RPP_OK) return st;
+    if (hipMemsetAsync(w.ustate, 0xFF, U * rpp_internal::kUsWords * 4, s) != hipSuccess) return RPP_HIP_ERROR;
     const uint32_t gu = (uint32_t)((U + 255) / 256);
     // pass 0: every unit; three rerun passes; a serial pass for what is left
     for (uint32_t pass : {0u, 1u, 1u, 1u, 2u}) {
@@ -1177,7 +1134,7 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
                                           w.sb_pos, d_status, a.sv, s);
       if (st != RPP_OK) return st;
     }
-    hipLaunchKernelGGL(rpp_seg_count_kernel, dim3((uint32_t)U), dim3(kSegThreads), 0, s, a);
+    hipLaunchKernelGGL(rpp_seg_count_kernel, dim3(gu), dim3(256), 0, s, a);
     if ((st = rpp_exclusive_scan_u64(w.cnt2, U + 1, w.off2, s)) != RPP_OK) return st;
     hipLaunchKernelGGL(rpp_seg_write_kernel, dim3((uint32_t)U), dim3(kSegThreads), 0, s, a);
     hipLaunchKernelGGL(rpp_seg_tail_kernel, dim3(g256), dim3(256), 0, s, a);

@@ -13,13 +13,14 @@ namespace rpp_internal {
 // Segmented decode of long streams (ricepp_decode2.hip, DESIGN.md "Segmented
 // decode").  A stream longer than 2^L bits is cut into units of 2^L bits;
 // every unit is parsed by its own wave from a guessed first header (unit 0
-// from the true start), recording the header positions it visits in a bitmap
-// of its region and the first kSegOvr headers past the region in a list.  A
-// guessed chain that meets the previous unit's exact chain is exact from the
-// meeting point on (the parse is deterministic), so the stitch pass keeps each
-// unit's positions from there; a unit whose chain never meets is parsed again
-// from a known header (rerun passes, then one serial pass): the result is the
-// serial parse's, whatever the guesses were.
+// from the true start), recording the header positions it visits inside its
+// region in a list (in chain order, so ascending) and the first kSegOvr
+// headers past the region in an overshoot list.  A guessed chain that meets
+// the previous unit's exact chain is exact from the meeting point on (the
+// parse is deterministic), so the stitch pass keeps each unit's positions from
+// there; a unit whose chain never meets is parsed again from a known header
+// (rerun passes, then one serial pass): the result is the serial parse's,
+// whatever the guesses were.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegOvr = 16;             // headers recorded past a unit's region
 constexpr uint32_t kSegNone = 0xFFFFFFFFu;   // no position
@@ -28,21 +29,25 @@ constexpr uint32_t kSpecVerify = 24;         // ... and the unit's own parse the
 constexpr uint32_t kGuessRetries = 8;        // next candidates tried after a rejected guess
 constexpr int32_t kSegFallback = 0x7F5E0001;  // internal status: decode this stream with the fused kernel
 
-// per-unit state words (SegView::ustate[4 u + i])
-enum : uint32_t { kUsNovr = 0, kUsStart = 1, kUsRerun = 2, kUsFlags = 3 };
+// per-unit state words (SegView::ustate[kUsWords u + i]): overshoot entries,
+// the chain's first header, a pending rerun's start, flags, positions listed
+constexpr uint32_t kUsWords = 8;
+enum : uint32_t { kUsNovr = 0, kUsStart = 1, kUsRerun = 2, kUsFlags = 3, kUsNpos = 4 };
 enum : uint32_t { kUfRerunDone = 1, kUfNoGuess = 2, kUfTrunc = 4 };
+// per-stream flags (SegView::sflags)
+enum : uint32_t { kSfPastRegion = 1, kSfListFull = 2 };
 
 struct SegView {
   const uint32_t* unit_map;   // [U] stream of unit u
   const uint64_t* unit_base;  // [B + 1] first unit of stream b (entry B: the number of units)
-  const uint64_t* bm_base;    // [U_max + 1] first bitmap word of unit u
-  uint32_t* bitmap;           // header positions, one bit per stream bit of the unit's region
+  const uint64_t* pl_base;    // [U_max + 1] first list entry of unit u (capacity: the next minus this)
+  uint32_t* plist;            // header positions of each unit's region, in chain order
   uint32_t* ovr;              // [U_max * kSegOvr] first headers past the region
-  uint32_t* ustate;           // [U_max * 4]
-  uint32_t* ulo;              // [U_max] the unit's exact positions start here (stitch)
+  uint32_t* ustate;           // [U_max * kUsWords]
+  uint32_t* ulo;              // [U_max] the unit's exact positions start at this list index (stitch)
   uint32_t* uov;              // [U_max] overshoot entries of the unit that are its own (stitch)
   uint32_t* sst;              // [B] first unresolved unit of stream b
-  uint32_t* sflags;           // [B] bit 0: the exact chain ran past the stream's region
+  uint32_t* sflags;           // [B] kSfPastRegion, kSfListFull
   uint32_t seg_log2;          // L
   uint32_t pass;              // 0 all units; 1 pending reruns; 2 pending reruns, serial to the end
   uint32_t units_max;         // grid bound (U_max)

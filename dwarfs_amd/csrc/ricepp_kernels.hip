@@ -1959,7 +1959,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
 // SEG = false: one wave per stream (launch_parse).  SEG = true: one wave per
 // unit of rpp_internal::SegView; a stream of one unit is parsed exactly as
 // with SEG = false, a unit of a split stream (ricepp_internal.h) records into
-// the bitmaps / overshoot list instead of sb_pos.
+// its position list / overshoot list instead of sb_pos.
 template <uint32_t CS, bool SEG>
 __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParseParams p) {
   using namespace rpp_internal;
@@ -1969,7 +1969,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     // leave before loading the tables
     if (p.sv.pass != 0) {
       const uint32_t w = blockIdx.x * p.waves + threadIdx.x / kWave;
-      if (w >= (uint32_t)p.sv.unit_base[p.nblocks] || p.sv.ustate[4 * w + kUsRerun] == kSegNone) return;
+      if (w >= (uint32_t)p.sv.unit_base[p.nblocks] || p.sv.ustate[kUsWords * w + kUsRerun] == kSegNone) return;
     }
   }
   {
@@ -1997,7 +1997,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     nunits = (uint32_t)p.sv.unit_base[b + 1] - u0;
     ju = u - u0;
     if (nunits == 1) return;  // (decoded by the fused kernel)
-    if (p.sv.pass != 0 && p.sv.ustate[4 * u + kUsRerun] == kSegNone) return;
+    if (p.sv.pass != 0 && p.sv.ustate[kUsWords * u + kUsRerun] == kSegNone) return;
   } else {
     if (b >= p.nblocks) return;  // no barrier below this point
   }
@@ -2058,7 +2058,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
   uint32_t P = 8u * mis + 16u * CS;  // codec.h:81-86: the initial values
   bool guessed = false;     // (verify the chain from P)
   uint32_t P_first = 0;     // the first guess, taken unverified if no later candidate verifies
-  uint32_t* const us = p.sv.ustate + 4 * u;
+  uint32_t* const us = p.sv.ustate + kUsWords * u;
   if (multi) {
     uint32_t flags = 0;
     if (p.sv.pass != 0) {
@@ -2069,23 +2069,20 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       guessed = true;
       if (P == kSegNone) flags = kUfNoGuess;
     }
-    // the unit's bitmap words (serial: also those of every later unit)
-    const uint64_t bw0 = p.sv.bm_base[u];
-    const uint64_t bw1 = p.sv.bm_base[serial ? u0 + nunits : u + 1];
-    for (uint64_t i = bw0 / 4 + lane; i < bw1 / 4; i += kWave)
-      reinterpret_cast<uint4*>(p.sv.bitmap)[i] = make_uint4(0, 0, 0, 0);
-    vm_drain();
     if (lane == 0) {
       us[kUsNovr] = 0;
       us[kUsStart] = P;
       us[kUsRerun] = kSegNone;
       us[kUsFlags] = flags;
+      us[kUsNpos] = 0;
     }
+    if (serial)  // (the serial pass lists the positions of every later unit)
+      for (uint32_t k = ju + 1 + lane; k < nunits; k += kWave) p.sv.ustate[kUsWords * (u0 + k) + kUsNpos] = 0;
     if (serial && lane == 0) {  // the stitch bookkeeping of the rest of the stream
       p.sv.uov[u - 1] = kSegOvr - 1;
-      p.sv.ulo[u] = P;
+      p.sv.ulo[u] = 0;  // (list indices: every position this pass lists is exact)
       for (uint32_t k = ju + 1; k < nunits; ++k) {
-        p.sv.ulo[u0 + k] = k << L;
+        p.sv.ulo[u0 + k] = 0;
         p.sv.uov[u0 + k - 1] = 0;
       }
       p.sv.uov[u0 + nunits - 1] = 0;
@@ -2152,33 +2149,50 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       if (!pend && fill_w <= (q >> 5) + 766) request();
     };
 
-    // ---- sub-block start positions, buffered 64 at a time in one VGPR ----
+    // ---- sub-block start positions, buffered 64 at a time in one VGPR,
+    //      then to sb_pos (one-unit streams) or to the list of the unit
+    //      whose region holds them (the serial pass crosses units) ----
     uint32_t pbuf = 0, pcnt = 0, pstart = 0;
     uint32_t novr = 0;
     bool stop = false;
+    uint32_t lk = ju;  // (SEG) the unit whose list is being written
+    uint64_t lbase = multi ? p.sv.pl_base[u] : 0;
+    uint32_t lcap = multi ? (uint32_t)(p.sv.pl_base[u + 1] - lbase) : 0;
     auto flush = [&]() {
-      if (multi) {  // into the bitmap of the unit holding the position
-        if (lane < pcnt) {
-          const uint32_t k = pbuf >> L;
-          const uint64_t w = p.sv.bm_base[u0 + k] + ((pbuf - (k << L)) >> 5);
-          atomicOr(p.sv.bitmap + w, 1u << (pbuf & 31u));
+      if (multi) {
+        if (pstart + pcnt > lcap) {  // below 1 bit per sample: the fused kernel takes the stream
+          stop = true;
+          if (lane == 0) atomicOr(p.sv.sflags + b, kSfListFull);
+        } else if (lane < pcnt) {
+          p.sv.plist[lbase + pstart + lane] = pbuf;
         }
       } else {
         if (lane < pcnt) pos_out[pstart + lane] = pbuf;
-        pstart += pcnt;
       }
+      pstart += pcnt;
       pcnt = 0;
+    };
+    auto close_list = [&]() {
+      if (lane == 0) p.sv.ustate[kUsWords * (u0 + lk) + kUsNpos] = min(pstart, lcap);
     };
     auto record = [&](uint32_t pos) {
       if (multi && pos >= E) {  // past the region: the overshoot list, or the end
         if (last || serial) {
           stop = true;
-          if (lane == 0) atomicOr(p.sv.sflags + b, 1u);
+          if (lane == 0) atomicOr(p.sv.sflags + b, kSfPastRegion);
         } else {
           if (lane == 0 && novr < kSegOvr) p.sv.ovr[kSegOvr * u + novr] = pos;
           if (++novr >= kSegOvr) stop = true;
         }
         return;
+      }
+      if (serial && (pos >> L) != lk) {  // into the next unit's region
+        flush();
+        close_list();
+        lk = pos >> L;
+        lbase = p.sv.pl_base[u0 + lk];
+        lcap = (uint32_t)(p.sv.pl_base[u0 + lk + 1] - lbase);
+        pstart = 0;
       }
       pbuf = lane == pcnt ? pos : pbuf;
       if (++pcnt == kWave) flush();
@@ -2445,6 +2459,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     }
     if (multi) {
       flush();
+      close_list();
       vm_drain();
       if (lane == 0) {
         atomicAdd(&g_parse_diag[1], (unsigned long long)(memtime() - t_chain));

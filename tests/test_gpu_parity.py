@@ -493,6 +493,9 @@ def test_segmented_decode_config_matrix(bs, cs, seg_log2):
             _decode_oracle_streams(cfg, blocks, ragged=True)
     stats = codec.segmented_decode_stats(reset=True)
     assert stats["met"] > 0, stats  # the units were split and stitched
+    diag = (__import__("ctypes").c_ulonglong * 8)()
+    __import__("dwarfs_amd._native", fromlist=["lib"]).lib().rpp_diag_read(diag, 1)
+    assert diag[6] == 0, "an extraction tile waited for a predecessor that never published"
     if seg_log2 == 10:
         assert stats["reruns"] + stats["serial"] > 0, stats
 
