@@ -33,6 +33,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "ricepp_amd.h"
@@ -74,6 +76,7 @@ struct Workspace {
   uint32_t* uhit;       // [2 U_max]: overshoot index, list index
   uint32_t* sst;        // [B]
   uint32_t* sflags;     // [B]
+  uint32_t* queue;      // [1]
   uint64_t* cnt2;       // [U_max + 1] exact positions per unit
   uint64_t* off2;       // [U_max + 1]
   uint64_t bytes;
@@ -140,6 +143,7 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint64_t max_str
     w.uhit = reinterpret_cast<uint32_t*>(take(U * 8));
     w.sst = reinterpret_cast<uint32_t*>(take(B * 4));
     w.sflags = reinterpret_cast<uint32_t*>(take(B * 4));
+    w.queue = reinterpret_cast<uint32_t*>(take(256));
     w.cnt2 = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
     w.off2 = reinterpret_cast<uint64_t*>(take((U + 1) * 8));
   }
@@ -984,6 +988,25 @@ ExtractKernel extract_kernel_for(uint32_t bs) {
   }
 }
 
+// The segmented decode forks the fused launch of a batch's one-unit streams
+// onto a second stream of the device (created once, never destroyed), so that
+// it overlaps the units' parse; events order it after the unit counts and
+// before the batch's end on the caller's stream (graph-capturable).
+constexpr uint32_t kDecSideWaves = 16;  // (full workgroups: the fused launch holds as few CUs as it can)
+hipStream_t side_stream() {
+  static std::mutex mu;
+  static std::map<int, hipStream_t>* streams = new std::map<int, hipStream_t>;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams->find(dev);
+  if (it != streams->end()) return it->second;
+  hipStream_t s2 = nullptr;
+  if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  streams->emplace(dev, s2);
+  return s2;
+}
+
 bool extract_bs(uint32_t bs) { return bs == 16 || bs == 32 || bs == 64 || bs == 128; }
 
 // The two-stage decode of every stream is selected by RICEPP_DECODE=two-stage;
@@ -1074,10 +1097,12 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
   if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
   const uint32_t chunk_len = cfg->block_size * cfg->component_stream_count;
   const uint32_t g256 = (nblocks + 256) / 256;
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   SegArgs a{};
   if (L) {
     a.sv = rpp_internal::SegView{w.unit_map, w.unit_base, w.pl_base, w.plist, w.ovr, w.ustate, w.ulo, w.uov,
-                                 w.sst, w.sflags, L, 0, (uint32_t)w.units_max};
+                                 w.sst, w.sflags, w.queue, L, 0, (uint32_t)w.units_max};
     a.in = d_in;
     a.in_off = d_in_offsets;
     a.in_bytes = d_in_bytes;
@@ -1111,14 +1136,22 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
     if (st != RPP_OK) return st;
   } else {
     const uint64_t U = w.units_max;
-    // the streams that fit one unit: one wave each, parse and values fused
+    // the streams that fit one unit: one wave each, parse and values fused,
+    // on the side stream while the units are parsed
+    s2 = side_stream();
+    if (!s2 || hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(ev_fork, s) != hipSuccess || hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess)
+      return RPP_HIP_ERROR;
     st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                           d_n_samples, d_status, s, false, w.ucnt);
+                                           d_n_samples, d_status, s2, false, w.ucnt, kDecSideWaves);
     if (st != RPP_OK) return st;
+    if (hipEventRecord(ev_join, s2) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.pl_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.cnt2, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.sst, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
     if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
+    if (hipMemsetAsync(w.queue, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
     hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.pl_cnt);
     if ((st = rpp_exclusive_scan_u64(w.pl_cnt, U + 1, w.pl_base, s)) != RPP_OK) return st;
     if (hipMemsetAsync(w.ustate, 0xFF, U * rpp_internal::kUsWords * 4, s) != hipSuccess) return RPP_HIP_ERROR;
@@ -1153,7 +1186,12 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
   const uint32_t grid = (uint32_t)std::min<uint64_t>(w.max_tiles, kMaxExtractGrid);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kTile), 0, s, p);
   if (hipGetLastError() != hipSuccess) return RPP_HIP_ERROR;
-  if (L) {  // streams whose exact chain left the region the units cover (malformed input)
+  if (L) {
+    // join the side stream, then the streams whose exact chain left the
+    // region the units cover or whose lists overflowed (the fused kernel)
+    if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return RPP_HIP_ERROR;
+    (void)hipEventDestroy(ev_fork);  // (released once complete)
+    (void)hipEventDestroy(ev_join);
     st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
                                            d_n_samples, d_status, s, true);
     if (st != RPP_OK) return st;

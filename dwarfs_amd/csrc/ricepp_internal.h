@@ -48,6 +48,7 @@ struct SegView {
   uint32_t* uov;              // [U_max] overshoot entries of the unit that are its own (stitch)
   uint32_t* sst;              // [B] first unresolved unit of stream b
   uint32_t* sflags;           // [B] kSfPastRegion, kSfListFull
+  uint32_t* queue;            // [1] pass 0: the next unit to take
   uint32_t seg_log2;          // L
   uint32_t pass;              // 0 all units; 1 pending reruns; 2 pending reruns, serial to the end
   uint32_t units_max;         // grid bound (U_max)
@@ -68,10 +69,11 @@ __host__ __device__ inline uint32_t seg_last_bit(uint32_t mis, uint64_t in_bytes
 // rpp_decode_kernel: one wave per stream, parse and values fused (any bs).
 // only_fallback: decode only the streams whose status is kSegFallback;
 // d_units (the segmented decode's units per stream): skip split streams.
+// waves: streams per workgroup (0: by batch size).
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                         const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback = false,
-                        const uint64_t* d_units = nullptr);
+                        const uint64_t* d_units = nullptr, uint32_t waves = 0);
 
 // rpp_parse_kernel: sub-block start positions of every stream into sb_pos
 // (stream b's entries from sb_base[b]: nsb_b header positions, then the end).

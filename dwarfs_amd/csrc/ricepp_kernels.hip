@@ -1810,8 +1810,9 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // Segmented decode, the first header of a unit (ricepp_internal.h): the
 // first candidate bit c in [c_first, 4 + 16 bs) of the staged words `st`
 // whose chain of kSpecSteps sub-blocks (each parsed exactly as
-// decode.h:42-83 would from there) keeps its header values within a range of
-// 4 (highest - lowest <= 3), with zero headers only in an all-zero chain.
+// decode.h:42-83 would from there) keeps its header values within a range
+// (highest - lowest <= `range`: 3, or 5 in a second search when the first
+// finds nothing), with zero headers only in an all-zero chain.
 // ricepp output does: the Rice parameter follows the local noise level
 // (Poisson data stays on one or two values, 6-bit noise with outliers on fs
 // 11..13).  Random bits do not, except through the zero high bits of small
@@ -1827,7 +1828,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // every sub-block the survivors are compacted into `list` (512 words of LDS).
 // A wrong guess costs time, never a wrong result.
 __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_rel, uint32_t bs,
-                                              uint32_t lane, uint32_t c_first) {
+                                              uint32_t lane, uint32_t c_first, uint32_t range) {
   using rpp_internal::kSegNone;
   using rpp_internal::kSpecSteps;
   constexpr uint32_t kSlots = 4;
@@ -1866,7 +1867,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
           // (zero sub-blocks only in an all-zero run: chains of small
           // headers through the zero high bits of small remainders are the
           // common false survivors)
-          alive[i] = alive[i] && hi - lo <= 3 && (lo != 0 || hi == 0) && nc + 4 <= end_rel;
+          alive[i] = alive[i] && hi - lo <= range && (lo != 0 || hi == 0) && nc + 4 <= end_rel;
           rice[i] = alive[i] && v - 1u < 14u;
           fsv[i] = v - 1;
           cur[i] = alive[i] ? nc : 0u;
@@ -1985,497 +1986,521 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + ring_w;
   const uint32_t bs = p.bs;
   const uint32_t lane24 = kSegBits * lane;
-  const uint32_t wid = blockIdx.x * p.waves + wv;
-  // ---- the stream (and, SEG, the unit) of this wave ----
-  uint32_t b = wid, u = 0, u0 = 0, ju = 0, nunits = 1;
-  if constexpr (SEG) {
-    if (wid >= p.sv.units_max) return;
-    if (wid >= (uint32_t)p.sv.unit_base[p.nblocks]) return;
-    u = wid;
-    b = __builtin_amdgcn_readfirstlane(p.sv.unit_map[u]);
-    u0 = (uint32_t)p.sv.unit_base[b];
-    nunits = (uint32_t)p.sv.unit_base[b + 1] - u0;
-    ju = u - u0;
-    if (nunits == 1) return;  // (decoded by the fused kernel)
-    if (p.sv.pass != 0 && p.sv.ustate[kUsWords * u + kUsRerun] == kSegNone) return;
-  } else {
-    if (b >= p.nblocks) return;  // no barrier below this point
-  }
-  const bool multi = SEG && nunits > 1;
-
-  // ---- per-stream setup (wave-uniform) ----
-  int32_t status = RPP_OK;
-  uint32_t N = 0, nbytes = 0, mis = 0;
-  const uint8_t* in = p.in;
-  {
-    const uint64_t n64 = p.n_samples[b];
-    const uint64_t ioff = p.in_off[b];
-    const uint64_t nb64 = p.in_bytes[b];
-    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
-      status = RPP_INVALID_ARGUMENT;
+  // One work item: a stream (SEG = false) or a unit.  Pass 0 of the
+  // segmented decode takes units from a queue (one 16-wave workgroup per CU,
+  // each wave unit after unit), so that every CU parses whatever the stream
+  // mix and the side-stream fused launch leave it; the other launches map one
+  // item per wave.
+  auto work = [&](const uint32_t wid) {
+    // ---- the stream (and, SEG, the unit) of this wave ----
+    uint32_t b = wid, u = 0, u0 = 0, ju = 0, nunits = 1;
+    if constexpr (SEG) {
+      if (wid >= p.sv.units_max) return;
+      if (wid >= (uint32_t)p.sv.unit_base[p.nblocks]) return;
+      u = wid;
+      b = __builtin_amdgcn_readfirstlane(p.sv.unit_map[u]);
+      u0 = (uint32_t)p.sv.unit_base[b];
+      nunits = (uint32_t)p.sv.unit_base[b + 1] - u0;
+      ju = u - u0;
+      if (nunits == 1) return;  // (decoded by the fused kernel)
+      if (p.sv.pass != 0 && p.sv.ustate[kUsWords * u + kUsRerun] == kSegNone) return;
     } else {
-      N = (uint32_t)n64;
-      mis = (uint32_t)(ioff & 3u);
-      nbytes = (uint32_t)nb64 + mis;  // bytes from the aligned base
-      in = p.in + (ioff - mis);
+      if (b >= p.nblocks) return;  // no barrier below this point
     }
-  }
-  uint32_t* const pos_out = multi ? nullptr : p.sb_pos + p.sb_base[b];
-  const bool aligned16 = ((uintptr_t)in & 15u) == 0;
-  // last readable bit + 1: the reader pulls whole 8-byte packets of the
-  // stream (bitstream_reader.h:149-183), zero past its last byte
-  const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
-  const uint32_t chunk_len = CS * bs;
-  const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
+    const bool multi = SEG && nunits > 1;
 
-  // ---- SEG: the unit's region [S, E) of header positions ----
-  const uint32_t L = p.sv.seg_log2;
-  const bool serial = multi && p.sv.pass == 2;
-  uint32_t S = 0, E = 0, Eend = 0;
-  bool last = false;
-  if (multi) {
-    Eend = seg_last_bit(mis, nbytes - mis, N, bs, CS);
-    S = ju << L;
-    last = ju + 1 == nunits;
-    E = last ? Eend + 1 : S + (1u << L);
-    if (serial) E = Eend + 1;
-  }
-
-  // ---- SEG: the first header of the unit ----
-  // A guess: the first candidate bit in [S + c_first, S + max sub-block) whose
-  // chain of kSpecSteps sub-blocks looks like ricepp output (seg_guess).
-  auto do_guess = [&](uint32_t c_first) -> uint32_t {
-    constexpr uint32_t kStW = kRingWords + kRingPad;
-    const uint32_t w0 = S >> 5;
-    for (uint32_t i = lane; i < kStW; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
-    lds_fence();
-    const uint64_t tg = memtime();
-    const uint32_t g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, c_first);
-    if (lane == 0) atomicAdd(&g_parse_diag[0], (unsigned long long)(memtime() - tg));
-    lds_fence();  // (the ring is refilled next)
-    return g == kSegNone ? kSegNone : S + g;
-  };
-  uint32_t P = 8u * mis + 16u * CS;  // codec.h:81-86: the initial values
-  bool guessed = false;     // (verify the chain from P)
-  uint32_t P_first = 0;     // the first guess, taken unverified if no later candidate verifies
-  uint32_t* const us = p.sv.ustate + kUsWords * u;
-  if (multi) {
-    uint32_t flags = 0;
-    if (p.sv.pass != 0) {
-      P = us[kUsRerun];  // a header of the exact chain (stitch)
-      flags = kUfRerunDone;
-    } else if (ju != 0) {
-      P = P_first = do_guess(0);
-      guessed = true;
-      if (P == kSegNone) flags = kUfNoGuess;
-    }
-    if (lane == 0) {
-      us[kUsNovr] = 0;
-      us[kUsStart] = P;
-      us[kUsRerun] = kSegNone;
-      us[kUsFlags] = flags;
-      us[kUsNpos] = 0;
-    }
-    if (serial)  // (the serial pass lists the positions of every later unit)
-      for (uint32_t k = ju + 1 + lane; k < nunits; k += kWave) p.sv.ustate[kUsWords * (u0 + k) + kUsNpos] = 0;
-    if (serial && lane == 0) {  // the stitch bookkeeping of the rest of the stream
-      p.sv.uov[u - 1] = kSegOvr - 1;
-      p.sv.ulo[u] = 0;  // (list indices: every position this pass lists is exact)
-      for (uint32_t k = ju + 1; k < nunits; ++k) {
-        p.sv.ulo[u0 + k] = 0;
-        p.sv.uov[u0 + k - 1] = 0;
-      }
-      p.sv.uov[u0 + nunits - 1] = 0;
-      p.sv.sst[b] = nunits;
-    }
-    if (P == kSegNone) return;
-  }
-
-  for (uint32_t attempt = 0;; ++attempt) {
-    // ---- LDS ring of the stream's words (as rpp_decode_kernel) ----
-    uint32_t fill_w = multi ? (P >> 5) & ~(kChunkWords - 1) : 0u;
-    bool pend = false;
-    auto retire = [&]() {
-      if (pend) {
-        vm_drain();
-        fill_w += kChunkWords;
-        pend = false;
-      }
-    };
-    auto refill_sync = [&]() {
-      const uint32_t w = fill_w + 4 * lane;
-      uint4 v;
-      if (aligned16 && 4 * w + 16 <= nbytes) {
-        v = *reinterpret_cast<const uint4*>(in + 4 * w);
+    // ---- per-stream setup (wave-uniform) ----
+    int32_t status = RPP_OK;
+    uint32_t N = 0, nbytes = 0, mis = 0;
+    const uint8_t* in = p.in;
+    {
+      const uint64_t n64 = p.n_samples[b];
+      const uint64_t ioff = p.in_off[b];
+      const uint64_t nb64 = p.in_bytes[b];
+      if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
+        status = RPP_INVALID_ARGUMENT;
       } else {
-        v = make_uint4(stream_word(in, nbytes, w), stream_word(in, nbytes, w + 1), stream_word(in, nbytes, w + 2),
-                       stream_word(in, nbytes, w + 3));
+        N = (uint32_t)n64;
+        mis = (uint32_t)(ioff & 3u);
+        nbytes = (uint32_t)nb64 + mis;  // bytes from the aligned base
+        in = p.in + (ioff - mis);
       }
-      *reinterpret_cast<uint4*>(&ring[w & kRingMask]) = v;
-      if ((w & kRingMask) < kRingPad) *reinterpret_cast<uint4*>(&ring[kRingWords + (w & kRingMask)]) = v;
-      fill_w += kChunkWords;
-    };
-    auto request = [&]() {
-      if (4u * (fill_w + kChunkWords) > nbytes) return;
-      const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[fill_w & kRingMask]);
-      const uint8_t* src = in + 4u * fill_w;
-      if (aligned16) {
-        glds16(src + 16u * lane, slot);
-      } else {
-  #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) glds4(src + 256u * q + 4u * lane, slot + 256u * q);
-      }
-      if ((fill_w & kRingMask) == 0)
-        glds4(src + 4u * lane, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[kRingWords]));
-      pend = true;
-    };
-    refill_sync();
-    refill_sync();
-    lds_fence();
-    auto ensure = [&](uint32_t w) {
-      if (fill_w < w + kAhead) {
-        retire();
-        while (fill_w < w + kAhead) refill_sync();
-        lds_fence();
-      }
-    };
-    auto wptr = [&](uint32_t w) -> const uint32_t* { return ring + (w & kRingMask); };
-    auto load_x = [&](uint32_t sb, uint32_t& xl) {
-      const uint32_t* q = wptr(sb >> 5);
-      xl = __builtin_amdgcn_alignbit(q[1], q[0], sb & 31u);
-    };
-    auto ring_keep = [&](uint32_t q) {
-      if (pend && fill_w < (q >> 5) + kAhead + 128) retire();
-      if (!pend && fill_w <= (q >> 5) + 766) request();
-    };
+    }
+    uint32_t* const pos_out = multi ? nullptr : p.sb_pos + p.sb_base[b];
+    const bool aligned16 = ((uintptr_t)in & 15u) == 0;
+    // last readable bit + 1: the reader pulls whole 8-byte packets of the
+    // stream (bitstream_reader.h:149-183), zero past its last byte
+    const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
+    const uint32_t chunk_len = CS * bs;
+    const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
 
-    // ---- sub-block start positions, buffered 64 at a time in one VGPR,
-    //      then to sb_pos (one-unit streams) or to the list of the unit
-    //      whose region holds them (the serial pass crosses units) ----
-    uint32_t pbuf = 0, pcnt = 0, pstart = 0;
-    uint32_t novr = 0;
-    bool stop = false;
-    uint32_t lk = ju;  // (SEG) the unit whose list is being written
-    uint64_t lbase = multi ? p.sv.pl_base[u] : 0;
-    uint32_t lcap = multi ? (uint32_t)(p.sv.pl_base[u + 1] - lbase) : 0;
-    auto flush = [&]() {
-      if (multi) {
-        if (pstart + pcnt > lcap) {  // below 1 bit per sample: the fused kernel takes the stream
-          stop = true;
-          if (lane == 0) atomicOr(p.sv.sflags + b, kSfListFull);
-        } else if (lane < pcnt) {
-          p.sv.plist[lbase + pstart + lane] = pbuf;
+    // ---- SEG: the unit's region [S, E) of header positions ----
+    const uint32_t L = p.sv.seg_log2;
+    const bool serial = multi && p.sv.pass == 2;
+    uint32_t S = 0, E = 0, Eend = 0;
+    bool last = false;
+    if (multi) {
+      Eend = seg_last_bit(mis, nbytes - mis, N, bs, CS);
+      S = ju << L;
+      last = ju + 1 == nunits;
+      E = last ? Eend + 1 : S + (1u << L);
+      if (serial) E = Eend + 1;
+    }
+
+    // ---- SEG: the first header of the unit ----
+    // A guess: the first candidate bit in [S + c_first, S + max sub-block) whose
+    // chain of kSpecSteps sub-blocks looks like ricepp output (seg_guess).
+    auto do_guess = [&](uint32_t c_first) -> uint32_t {
+      constexpr uint32_t kStW = kRingWords + kRingPad;
+      const uint32_t w0 = S >> 5;
+      for (uint32_t i = lane; i < kStW; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
+      lds_fence();
+      const uint64_t tg = memtime();
+      uint32_t g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, c_first, 3);
+    // none: the true chain's headers may span a wider range for a few
+    // sub-blocks; a second search with range 5 (its candidates are checked
+    // by the parse as any other)
+    if (g == kSegNone && c_first == 0)
+      g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, 0, 5);
+      if (lane == 0) atomicAdd(&g_parse_diag[0], (unsigned long long)(memtime() - tg));
+      lds_fence();  // (the ring is refilled next)
+      return g == kSegNone ? kSegNone : S + g;
+    };
+    uint32_t P = 8u * mis + 16u * CS;  // codec.h:81-86: the initial values
+    bool guessed = false;     // (verify the chain from P)
+    uint32_t P_first = 0;     // the first guess, taken unverified if no later candidate verifies
+    uint32_t* const us = p.sv.ustate + kUsWords * u;
+    if (multi) {
+      uint32_t flags = 0;
+      if (p.sv.pass != 0) {
+        P = us[kUsRerun];  // a header of the exact chain (stitch)
+        flags = kUfRerunDone;
+      } else if (ju != 0) {
+        P = P_first = do_guess(0);
+        guessed = true;
+        if (P == kSegNone) flags = kUfNoGuess;
+      }
+      if (lane == 0) {
+        us[kUsNovr] = 0;
+        us[kUsStart] = P;
+        us[kUsRerun] = kSegNone;
+        us[kUsFlags] = flags;
+        us[kUsNpos] = 0;
+      }
+      if (serial)  // (the serial pass lists the positions of every later unit)
+        for (uint32_t k = ju + 1 + lane; k < nunits; k += kWave) p.sv.ustate[kUsWords * (u0 + k) + kUsNpos] = 0;
+      if (serial && lane == 0) {  // the stitch bookkeeping of the rest of the stream
+        p.sv.uov[u - 1] = kSegOvr - 1;
+        p.sv.ulo[u] = 0;  // (list indices: every position this pass lists is exact)
+        for (uint32_t k = ju + 1; k < nunits; ++k) {
+          p.sv.ulo[u0 + k] = 0;
+          p.sv.uov[u0 + k - 1] = 0;
         }
-      } else {
-        if (lane < pcnt) pos_out[pstart + lane] = pbuf;
+        p.sv.uov[u0 + nunits - 1] = 0;
+        p.sv.sst[b] = nunits;
       }
-      pstart += pcnt;
-      pcnt = 0;
-    };
-    auto close_list = [&]() {
-      if (lane == 0) p.sv.ustate[kUsWords * (u0 + lk) + kUsNpos] = min(pstart, lcap);
-    };
-    auto record = [&](uint32_t pos) {
-      if (multi && pos >= E) {  // past the region: the overshoot list, or the end
-        if (last || serial) {
-          stop = true;
-          if (lane == 0) atomicOr(p.sv.sflags + b, kSfPastRegion);
-        } else {
-          if (lane == 0 && novr < kSegOvr) p.sv.ovr[kSegOvr * u + novr] = pos;
-          if (++novr >= kSegOvr) stop = true;
-        }
-        return;
-      }
-      if (serial && (pos >> L) != lk) {  // into the next unit's region
-        flush();
-        close_list();
-        lk = pos >> L;
-        lbase = p.sv.pl_base[u0 + lk];
-        lcap = (uint32_t)(p.sv.pl_base[u0 + lk + 1] - lbase);
-        pstart = 0;
-      }
-      pbuf = lane == pcnt ? pos : pbuf;
-      if (++pcnt == kWave) flush();
-    };
+      if (P == kSegNone) return;
+    }
 
-    // SEG, a guessed start: the first kSpecVerify headers of the chain must
-    // keep to the guess's rule (seg_guess), else the guess was wrong and the
-    // next candidate is tried.  Until then no position has left pbuf
-    // (kSpecVerify < 64), so a rejected chain leaves nothing behind.
-    uint32_t vcnt = guessed ? 0u : kSpecVerify, vlo = 15, vhi = 0;
-    bool vfail = false;
-    auto note = [&](uint32_t v) {
-      if (vcnt < kSpecVerify) {
-        ++vcnt;
-        vlo = min(vlo, v);
-        vhi = max(vhi, v);
-        if (vhi - vlo > 3 || (vlo == 0 && vhi != 0)) vfail = stop = true;
-      }
-    };
-
-    if (!multi && status == RPP_OK && P > lim) status = RPP_TRUNCATED_INPUT;
-    // a unit of a split stream parses bs-sample sub-blocks until its region
-    // ends (the ragged last chunk is re-parsed by rpp_seg_tail_kernel)
-    const uint32_t nsb = multi ? 0xFFFFFFFFu : nchunks * CS;
-    const bool fast_bs = bs == 2 * kWave || bs == 16 || bs == 32 || bs == 64;
-    const uint32_t nsb_fast = multi ? 0xFFFFFFFFu : fast_bs ? (N / chunk_len) * CS : 0u;
-    ScanRegs sreg;
-
-    uint32_t s = 0;
-    const uint64_t t_chain = multi ? memtime() : 0;
-    const uint32_t P0 = P;
-    while (s < nsb && status == RPP_OK && !stop) {
-      // ---- fast loop: Rice sub-blocks of bs codes with fs in [LO, HI] lying
-      //      in one window, ring resident; the parse of sub-block s+1 is issued
-      //      as soon as the end of s is known ----
-      auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI>() {
-        const uint32_t n = bs;
-        auto seg_bits = [&](uint32_t q) {
-          const uint32_t o = lane24 + (q & 31u);
-          uint32_t oi = o >> 5;
-          asm("" : "+v"(oi));
-          const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
-          return __builtin_amdgcn_alignbit(w[1], w[0], o);
-        };
-        auto fs_of = [](uint32_t h) {
-          uint32_t r;
-          asm("s_and_b32 %0, %1, 15\n\ts_max_u32 %0, %0, %2\n\ts_min_u32 %0, %0, %3\n\ts_sub_u32 %0, %0, 1"
-              : "=&s"(r)
-              : "s"(h), "n"(LO + 1), "n"(HI + 1)
-              : "scc");
-          return r;
-        };
-        auto header_ok = [](uint32_t h) { return (h & 15u) - (LO + 1) <= HI - LO; };
-        // end (next header) of the sub-block at bit q, if it lies in the window
-        auto parse = [&](uint32_t q, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
-          const uint32_t k = fs + 1;
-          const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});
-          Map8 M = comp8(Map8{e2.x, e2.y}, M01);
-          M = scan8_shr1(M, sreg.r1);
-          M = scan8_shr2(M, sreg.r2);
-          M = scan8_shr4(M, sreg.r4);
-          M = scan8_shr8(M, sreg.r8);
-          M = scan8_bc15(M, sreg.b15);
-          M = scan8_bc31(M, sreg.b31);
-          const Map8 X = shift8_wave(M, sreg.w1);
-          const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
-          const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-          const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
-          const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
-          uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
-          const uint32_t cnt = __builtin_popcount(tm);
-          const uint32_t incl = wave_incl_sum(cnt);
-          const uint64_t finm = __ballot(incl >= n);
-          const uint32_t excl = incl - cnt;
-          uint32_t t[MT];
-  #pragma unroll
-          for (uint32_t j = 0; j < MT; ++j) {
-            t[j] = ffbl(tm);
-            tm &= tm - 1;
-          }
-          const uint32_t r = n - 1 - excl;
-          uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
-          if constexpr (MT > 4) {
-            const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
-            tpk = r < 4 ? tpk : tpk1;
-          }
-          const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
-          const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
-          Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
-          return finm != 0;
-        };
-        auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2) {
-          const uint4* tb = tab + 256u * fs;
-          e0 = tb[xl & 0xFFu];
-          e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
-          e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
-        };
-        uint32_t pn_limit, trig_w;
-        auto ring_bounds = [&]() {
-          pn_limit = min(lim - 4u, 32u * (fill_w - kAhead) + 31u);
-          trig_w = pend ? fill_w - (kAhead + 127u) : (fill_w > 766u ? fill_w - 766u : 0u);
-        };
-        ring_bounds();
-        uint32_t Pn;
-        const uint32_t xl = seg_bits(P);
-        const uint32_t h = __builtin_amdgcn_readfirstlane(xl);
-        uint32_t fs = fs_of(h);
-        uint4 e0, e1, e2;
-        lookups(xl, fs, e0, e1, e2);
-        bool ok = parse(P, fs, e0, e1, e2, Pn) && header_ok(h);
-        uint32_t hc = h;  // header of the sub-block at P
-        while (ok) {
-          // sub-block s at P ends at Pn; parse s+1 at Pn
-          const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit && !stop;
-          const uint32_t xlB = seg_bits(Pn);
-          const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
-          const uint32_t fsB = fs_of(hB);
-          lookups(xlB, fsB, e0, e1, e2);
-          uint32_t PnB;
-          ok = parse(Pn, fsB, e0, e1, e2, PnB) && header_ok(hB) && nxt;
-          record(P);
-          if (multi) note(hc & 15u);
-          hc = hB;
-          ++s;
-          P = Pn;
-          if (!ok) {
-            if (P > lim) status = RPP_TRUNCATED_INPUT;
-            break;
-          }
-          Pn = PnB;
-          fs = fsB;
-          if ((Pn >> 5) >= trig_w) {
-            ring_keep(Pn);
-            ring_bounds();
-          }
+    for (uint32_t attempt = 0;; ++attempt) {
+      // ---- LDS ring of the stream's words (as rpp_decode_kernel) ----
+      uint32_t fill_w = multi ? (P >> 5) & ~(kChunkWords - 1) : 0u;
+      bool pend = false;
+      auto retire = [&]() {
+        if (pend) {
+          vm_drain();
+          fill_w += kChunkWords;
+          pend = false;
         }
       };
-      while (s < nsb_fast && status == RPP_OK && !stop && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
-        const uint32_t* w = ring + ((P >> 5) & kRingMask);
-        const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
-        const uint32_t s0 = s;
-        if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
-        else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
-        if (s == s0) break;  // the general path takes this sub-block
-      }
-      if (s >= nsb || status != RPP_OK || stop) break;
-      // ---- general path: one sub-block of any kind ----
-      const uint32_t cbase = (s / CS) * chunk_len;
-      const uint32_t n = multi ? bs : min(N - cbase, chunk_len) / CS;
-      ensure(P >> 5);
-      if (multi) {  // (the end of the stream's last sub-block is a position too)
-        record(P);
-        if (stop) break;
-      }
-      if (P + 4 > lim) {  // decode.h:60: the 4-bit header
-        status = RPP_TRUNCATED_INPUT;
-        break;
-      }
-      if (!multi) record(P);
-      uint32_t xl;
-      load_x(P + kSegBits * lane, xl);
-      const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
-      if (multi) {
-        note(fsp1);
-        if (vfail) break;
-      }
-      if (fsp1 == 0) {  // decode.h:79-80
-        P += 4;
-      } else if (fsp1 == 15) {  // decode.h:72-77: n raw 16-bit values
-        if ((uint64_t)P + 4 + 16ull * n > lim) {
+      auto refill_sync = [&]() {
+        const uint32_t w = fill_w + 4 * lane;
+        uint4 v;
+        if (aligned16 && 4 * w + 16 <= nbytes) {
+          v = *reinterpret_cast<const uint4*>(in + 4 * w);
+        } else {
+          v = make_uint4(stream_word(in, nbytes, w), stream_word(in, nbytes, w + 1), stream_word(in, nbytes, w + 2),
+                         stream_word(in, nbytes, w + 3));
+        }
+        *reinterpret_cast<uint4*>(&ring[w & kRingMask]) = v;
+        if ((w & kRingMask) < kRingPad) *reinterpret_cast<uint4*>(&ring[kRingWords + (w & kRingMask)]) = v;
+        fill_w += kChunkWords;
+      };
+      auto request = [&]() {
+        if (4u * (fill_w + kChunkWords) > nbytes) return;
+        const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[fill_w & kRingMask]);
+        const uint8_t* src = in + 4u * fill_w;
+        if (aligned16) {
+          glds16(src + 16u * lane, slot);
+        } else {
+    #pragma unroll
+          for (uint32_t q = 0; q < 4; ++q) glds4(src + 256u * q + 4u * lane, slot + 256u * q);
+        }
+        if ((fill_w & kRingMask) == 0)
+          glds4(src + 4u * lane, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&ring[kRingWords]));
+        pend = true;
+      };
+      refill_sync();
+      refill_sync();
+      lds_fence();
+      auto ensure = [&](uint32_t w) {
+        if (fill_w < w + kAhead) {
+          retire();
+          while (fill_w < w + kAhead) refill_sync();
+          lds_fence();
+        }
+      };
+      auto wptr = [&](uint32_t w) -> const uint32_t* { return ring + (w & kRingMask); };
+      auto load_x = [&](uint32_t sb, uint32_t& xl) {
+        const uint32_t* q = wptr(sb >> 5);
+        xl = __builtin_amdgcn_alignbit(q[1], q[0], sb & 31u);
+      };
+      auto ring_keep = [&](uint32_t q) {
+        if (pend && fill_w < (q >> 5) + kAhead + 128) retire();
+        if (!pend && fill_w <= (q >> 5) + 766) request();
+      };
+
+      // ---- sub-block start positions, buffered 64 at a time in one VGPR,
+      //      then to sb_pos (one-unit streams) or to the list of the unit
+      //      whose region holds them (the serial pass crosses units) ----
+      uint32_t pbuf = 0, pcnt = 0, pstart = 0;
+      uint32_t novr = 0;
+      bool stop = false;
+      uint32_t lk = ju;  // (SEG) the unit whose list is being written
+      uint64_t lbase = multi ? p.sv.pl_base[u] : 0;
+      uint32_t lcap = multi ? (uint32_t)(p.sv.pl_base[u + 1] - lbase) : 0;
+      auto flush = [&]() {
+        if (multi) {
+          if (pstart + pcnt > lcap) {  // below 1 bit per sample: the fused kernel takes the stream
+            stop = true;
+            if (lane == 0) atomicOr(p.sv.sflags + b, kSfListFull);
+          } else if (lane < pcnt) {
+            p.sv.plist[lbase + pstart + lane] = pbuf;
+          }
+        } else {
+          if (lane < pcnt) pos_out[pstart + lane] = pbuf;
+        }
+        pstart += pcnt;
+        pcnt = 0;
+      };
+      auto close_list = [&]() {
+        if (lane == 0) p.sv.ustate[kUsWords * (u0 + lk) + kUsNpos] = min(pstart, lcap);
+      };
+      auto record = [&](uint32_t pos) {
+        if (multi && pos >= E) {  // past the region: the overshoot list, or the end
+          if (last || serial) {
+            stop = true;
+            if (lane == 0) atomicOr(p.sv.sflags + b, kSfPastRegion);
+          } else {
+            if (lane == 0 && novr < kSegOvr) p.sv.ovr[kSegOvr * u + novr] = pos;
+            if (++novr >= kSegOvr) stop = true;
+          }
+          return;
+        }
+        if (serial && (pos >> L) != lk) {  // into the next unit's region
+          flush();
+          close_list();
+          lk = pos >> L;
+          lbase = p.sv.pl_base[u0 + lk];
+          lcap = (uint32_t)(p.sv.pl_base[u0 + lk + 1] - lbase);
+          pstart = 0;
+        }
+        pbuf = lane == pcnt ? pos : pbuf;
+        if (++pcnt == kWave) flush();
+      };
+
+      // SEG, a guessed start: the first kSpecVerify headers of the chain must
+      // keep to the guess's rule (seg_guess), else the guess was wrong and the
+      // next candidate is tried.  Until then no position has left pbuf
+      // (kSpecVerify < 64), so a rejected chain leaves nothing behind.
+      uint32_t vcnt = guessed ? 0u : kSpecVerify, vlo = 15, vhi = 0;
+      bool vfail = false;
+      auto note = [&](uint32_t v) {
+        if (vcnt < kSpecVerify) {
+          ++vcnt;
+          vlo = min(vlo, v);
+          vhi = max(vhi, v);
+          if (vhi - vlo > 3 || (vlo == 0 && vhi != 0)) vfail = stop = true;
+        }
+      };
+
+      if (!multi && status == RPP_OK && P > lim) status = RPP_TRUNCATED_INPUT;
+      // a unit of a split stream parses bs-sample sub-blocks until its region
+      // ends (the ragged last chunk is re-parsed by rpp_seg_tail_kernel)
+      const uint32_t nsb = multi ? 0xFFFFFFFFu : nchunks * CS;
+      const bool fast_bs = bs == 2 * kWave || bs == 16 || bs == 32 || bs == 64;
+      const uint32_t nsb_fast = multi ? 0xFFFFFFFFu : fast_bs ? (N / chunk_len) * CS : 0u;
+      ScanRegs sreg;
+
+      uint32_t s = 0;
+      const uint64_t t_chain = multi ? memtime() : 0;
+      const uint32_t P0 = P;
+      while (s < nsb && status == RPP_OK && !stop) {
+        // ---- fast loop: Rice sub-blocks of bs codes with fs in [LO, HI] lying
+        //      in one window, ring resident; the parse of sub-block s+1 is issued
+        //      as soon as the end of s is known ----
+        auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI>() {
+          const uint32_t n = bs;
+          auto seg_bits = [&](uint32_t q) {
+            const uint32_t o = lane24 + (q & 31u);
+            uint32_t oi = o >> 5;
+            asm("" : "+v"(oi));
+            const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
+            return __builtin_amdgcn_alignbit(w[1], w[0], o);
+          };
+          auto fs_of = [](uint32_t h) {
+            uint32_t r;
+            asm("s_and_b32 %0, %1, 15\n\ts_max_u32 %0, %0, %2\n\ts_min_u32 %0, %0, %3\n\ts_sub_u32 %0, %0, 1"
+                : "=&s"(r)
+                : "s"(h), "n"(LO + 1), "n"(HI + 1)
+                : "scc");
+            return r;
+          };
+          auto header_ok = [](uint32_t h) { return (h & 15u) - (LO + 1) <= HI - LO; };
+          // end (next header) of the sub-block at bit q, if it lies in the window
+          auto parse = [&](uint32_t q, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
+            const uint32_t k = fs + 1;
+            const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});
+            Map8 M = comp8(Map8{e2.x, e2.y}, M01);
+            M = scan8_shr1(M, sreg.r1);
+            M = scan8_shr2(M, sreg.r2);
+            M = scan8_shr4(M, sreg.r4);
+            M = scan8_shr8(M, sreg.r8);
+            M = scan8_bc15(M, sreg.b15);
+            M = scan8_bc31(M, sreg.b31);
+            const Map8 X = shift8_wave(M, sreg.w1);
+            const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
+            const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+            const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
+            const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
+            uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
+            const uint32_t cnt = __builtin_popcount(tm);
+            const uint32_t incl = wave_incl_sum(cnt);
+            const uint64_t finm = __ballot(incl >= n);
+            const uint32_t excl = incl - cnt;
+            uint32_t t[MT];
+    #pragma unroll
+            for (uint32_t j = 0; j < MT; ++j) {
+              t[j] = ffbl(tm);
+              tm &= tm - 1;
+            }
+            const uint32_t r = n - 1 - excl;
+            uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
+            if constexpr (MT > 4) {
+              const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
+              tpk = r < 4 ? tpk : tpk1;
+            }
+            const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
+            const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
+            Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
+            return finm != 0;
+          };
+          auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2) {
+            const uint4* tb = tab + 256u * fs;
+            e0 = tb[xl & 0xFFu];
+            e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
+            e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+          };
+          uint32_t pn_limit, trig_w;
+          auto ring_bounds = [&]() {
+            pn_limit = min(lim - 4u, 32u * (fill_w - kAhead) + 31u);
+            trig_w = pend ? fill_w - (kAhead + 127u) : (fill_w > 766u ? fill_w - 766u : 0u);
+          };
+          ring_bounds();
+          uint32_t Pn;
+          const uint32_t xl = seg_bits(P);
+          const uint32_t h = __builtin_amdgcn_readfirstlane(xl);
+          uint32_t fs = fs_of(h);
+          uint4 e0, e1, e2;
+          lookups(xl, fs, e0, e1, e2);
+          bool ok = parse(P, fs, e0, e1, e2, Pn) && header_ok(h);
+          uint32_t hc = h;  // header of the sub-block at P
+          while (ok) {
+            // sub-block s at P ends at Pn; parse s+1 at Pn
+            const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit && !stop;
+            const uint32_t xlB = seg_bits(Pn);
+            const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
+            const uint32_t fsB = fs_of(hB);
+            lookups(xlB, fsB, e0, e1, e2);
+            uint32_t PnB;
+            ok = parse(Pn, fsB, e0, e1, e2, PnB) && header_ok(hB) && nxt;
+            record(P);
+            if (multi) note(hc & 15u);
+            hc = hB;
+            ++s;
+            P = Pn;
+            if (!ok) {
+              if (P > lim) status = RPP_TRUNCATED_INPUT;
+              break;
+            }
+            Pn = PnB;
+            fs = fsB;
+            if ((Pn >> 5) >= trig_w) {
+              ring_keep(Pn);
+              ring_bounds();
+            }
+          }
+        };
+        while (s < nsb_fast && status == RPP_OK && !stop && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
+          const uint32_t* w = ring + ((P >> 5) & kRingMask);
+          const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
+          const uint32_t s0 = s;
+          if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
+          else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
+          if (s == s0) break;  // the general path takes this sub-block
+        }
+        if (s >= nsb || status != RPP_OK || stop) break;
+        // ---- general path: one sub-block of any kind ----
+        const uint32_t cbase = (s / CS) * chunk_len;
+        const uint32_t n = multi ? bs : min(N - cbase, chunk_len) / CS;
+        ensure(P >> 5);
+        if (multi) {  // (the end of the stream's last sub-block is a position too)
+          record(P);
+          if (stop) break;
+        }
+        if (P + 4 > lim) {  // decode.h:60: the 4-bit header
           status = RPP_TRUNCATED_INPUT;
           break;
         }
-        P += 4 + 16 * n;
-      } else {  // decode.h:62-71: n Rice codes; find the end of code n-1
-        const uint32_t fs = fsp1 - 1;
-        const uint4* tb = tab + 256u * fs;
-        uint32_t q0 = P, s0 = 4, done = 0;
-        for (;;) {
-          const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
-                      e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
-          uint32_t tm, xexit;
-          if (fs < 8) {
-            Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
-            M = scan_step8<kDppRowShr1>(M);
-            M = scan_step8<kDppRowShr2>(M);
-            M = scan_step8<kDppRowShr4>(M);
-            M = scan_step8<kDppRowShr8>(M);
-            M = scan_step8<kDppRowBcast15, 0xA>(M);
-            M = scan_step8<kDppRowBcast31, 0xC>(M);
-            const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
-            uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
-            const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-            sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
-            const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
-            sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
-            const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
-            xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
-            tm = t0 | (t1 << 8) | (t2 << 16);
-          } else {
-            const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
-            Map16 M = comp16(b2, comp16(b1, b0));
-            M = scan_step16<kDppRowShr1>(M);
-            M = scan_step16<kDppRowShr2>(M);
-            M = scan_step16<kDppRowShr4>(M);
-            M = scan_step16<kDppRowShr8>(M);
-            M = scan_step16<kDppRowBcast15, 0xA>(M);
-            M = scan_step16<kDppRowBcast31, 0xC>(M);
-            const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
-                           dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
-            uint32_t st = sel16(X, s0) & 0xFFu;
-            uint32_t t[3];
-            const uint4 ee[3] = {e0, e1, e2};
-  #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              const uint32_t sel = st | kSelByte0;
-              const bool skip = st >= 8;
-              t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
-              st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
-            }
-            tm = t[0] | (t[1] << 8) | (t[2] << 16);
-            xexit = st;
-          }
-          const uint32_t cnt = __builtin_popcount(tm);
-          const uint32_t incl = wave_incl_sum(cnt);
-          const uint32_t need = n - done;
-          const uint64_t fin = __ballot(incl >= need);
-          if (fin) {
-            // terminator need-1-excl of the first lane reaching need
-            const uint32_t lz = (uint32_t)__builtin_ctzll(fin);
-            uint32_t tmv = readlane(tm, (int)lz);
-            const uint32_t r = need - 1 - (readlane(incl, (int)lz) - readlane(cnt, (int)lz));
-            for (uint32_t j = 0; j < r; ++j) tmv &= tmv - 1;
-            P = q0 + kSegBits * lz + (uint32_t)__builtin_ctz(tmv) + fsp1;
-            break;
-          }
-          done += wave_last(incl);
-          s0 = wave_last(xexit);
-          q0 += kWinBits;
-          if (q0 >= lim) {  // the open unary search would read past the input
+        if (!multi) record(P);
+        uint32_t xl;
+        load_x(P + kSegBits * lane, xl);
+        const uint32_t fsp1 = __builtin_amdgcn_readfirstlane(xl) & 15u;
+        if (multi) {
+          note(fsp1);
+          if (vfail) break;
+        }
+        if (fsp1 == 0) {  // decode.h:79-80
+          P += 4;
+        } else if (fsp1 == 15) {  // decode.h:72-77: n raw 16-bit values
+          if ((uint64_t)P + 4 + 16ull * n > lim) {
             status = RPP_TRUNCATED_INPUT;
             break;
           }
-          ensure(q0 >> 5);
-          load_x(q0 + kSegBits * lane, xl);
+          P += 4 + 16 * n;
+        } else {  // decode.h:62-71: n Rice codes; find the end of code n-1
+          const uint32_t fs = fsp1 - 1;
+          const uint4* tb = tab + 256u * fs;
+          uint32_t q0 = P, s0 = 4, done = 0;
+          for (;;) {
+            const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)],
+                        e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+            uint32_t tm, xexit;
+            if (fs < 8) {
+              Map8 M = comp8(Map8{e2.x, e2.y}, comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y}));
+              M = scan_step8<kDppRowShr1>(M);
+              M = scan_step8<kDppRowShr2>(M);
+              M = scan_step8<kDppRowShr4>(M);
+              M = scan_step8<kDppRowShr8>(M);
+              M = scan_step8<kDppRowBcast15, 0xA>(M);
+              M = scan_step8<kDppRowBcast31, 0xC>(M);
+              const Map8 X{dpp_keep<kDppWaveShr1>(kId0, M.lo), dpp_keep<kDppWaveShr1>(kId1, M.hi)};
+              uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, s0 | kSelByte0) | kSelByte0;
+              const uint32_t t0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+              sel = __builtin_amdgcn_perm(e0.y, e0.x, sel) | kSelByte0;
+              const uint32_t t1 = __builtin_amdgcn_perm(e1.w, e1.z, sel);
+              sel = __builtin_amdgcn_perm(e1.y, e1.x, sel) | kSelByte0;
+              const uint32_t t2 = __builtin_amdgcn_perm(e2.w, e2.z, sel);
+              xexit = __builtin_amdgcn_perm(e2.y, e2.x, sel);
+              tm = t0 | (t1 << 8) | (t2 << 16);
+            } else {
+              const Map16 b0{{e0.x, e0.y, kId0, kId1}}, b1{{e1.x, e1.y, kId0, kId1}}, b2{{e2.x, e2.y, kId0, kId1}};
+              Map16 M = comp16(b2, comp16(b1, b0));
+              M = scan_step16<kDppRowShr1>(M);
+              M = scan_step16<kDppRowShr2>(M);
+              M = scan_step16<kDppRowShr4>(M);
+              M = scan_step16<kDppRowShr8>(M);
+              M = scan_step16<kDppRowBcast15, 0xA>(M);
+              M = scan_step16<kDppRowBcast31, 0xC>(M);
+              const Map16 X{{dpp_keep<kDppWaveShr1>(kId0, M.w[0]), dpp_keep<kDppWaveShr1>(kId1, M.w[1]),
+                             dpp_keep<kDppWaveShr1>(kId2, M.w[2]), dpp_keep<kDppWaveShr1>(kId3, M.w[3])}};
+              uint32_t st = sel16(X, s0) & 0xFFu;
+              uint32_t t[3];
+              const uint4 ee[3] = {e0, e1, e2};
+    #pragma unroll
+              for (int j = 0; j < 3; ++j) {
+                const uint32_t sel = st | kSelByte0;
+                const bool skip = st >= 8;
+                t[j] = skip ? 0u : __builtin_amdgcn_perm(ee[j].w, ee[j].z, sel);
+                st = skip ? st - 8 : __builtin_amdgcn_perm(ee[j].y, ee[j].x, sel);
+              }
+              tm = t[0] | (t[1] << 8) | (t[2] << 16);
+              xexit = st;
+            }
+            const uint32_t cnt = __builtin_popcount(tm);
+            const uint32_t incl = wave_incl_sum(cnt);
+            const uint32_t need = n - done;
+            const uint64_t fin = __ballot(incl >= need);
+            if (fin) {
+              // terminator need-1-excl of the first lane reaching need
+              const uint32_t lz = (uint32_t)__builtin_ctzll(fin);
+              uint32_t tmv = readlane(tm, (int)lz);
+              const uint32_t r = need - 1 - (readlane(incl, (int)lz) - readlane(cnt, (int)lz));
+              for (uint32_t j = 0; j < r; ++j) tmv &= tmv - 1;
+              P = q0 + kSegBits * lz + (uint32_t)__builtin_ctz(tmv) + fsp1;
+              break;
+            }
+            done += wave_last(incl);
+            s0 = wave_last(xexit);
+            q0 += kWinBits;
+            if (q0 >= lim) {  // the open unary search would read past the input
+              status = RPP_TRUNCATED_INPUT;
+              break;
+            }
+            ensure(q0 >> 5);
+            load_x(q0 + kSegBits * lane, xl);
+          }
+          if (status != RPP_OK) break;
+          if (P > lim) {
+            status = RPP_TRUNCATED_INPUT;
+            break;
+          }
         }
-        if (status != RPP_OK) break;
-        if (P > lim) {
-          status = RPP_TRUNCATED_INPUT;
-          break;
+        ++s;
+        ring_keep(P);
+      }
+      retire();
+      if (vfail) {  // the guess failed its check: the next candidate that chains
+        P = attempt < kGuessRetries ? do_guess(P0 - S + 1) : kSegNone;
+        if (P == kSegNone) {  // none: the first guess after all (its chain may just vary more)
+          P = P_first;
+          guessed = false;
         }
+        continue;
       }
-      ++s;
-      ring_keep(P);
-    }
-    retire();
-    if (vfail) {  // the guess failed its check: the next candidate that chains
-      P = attempt < kGuessRetries ? do_guess(P0 - S + 1) : kSegNone;
-      if (P == kSegNone) {  // none: the first guess after all (its chain may just vary more)
-        P = P_first;
-        guessed = false;
+      if (multi) {
+        flush();
+        close_list();
+        vm_drain();
+        if (lane == 0) {
+          atomicAdd(&g_parse_diag[1], (unsigned long long)(memtime() - t_chain));
+          atomicAdd(&g_parse_diag[2], (unsigned long long)s);
+          atomicAdd(&g_parse_diag[3], 1ull);
+          if (attempt) atomicAdd(&g_parse_diag[7], (unsigned long long)attempt);
+          us[kUsStart] = P0;
+          us[kUsNovr] = min(novr, kSegOvr);
+          if (status != RPP_OK) us[kUsFlags] |= kUfTrunc;
+        }
+        return;
       }
-      continue;
-    }
-    if (multi) {
+      if (status == RPP_OK) record(P);  // the end of the last sub-block
       flush();
-      close_list();
-      vm_drain();
-      if (lane == 0) {
-        atomicAdd(&g_parse_diag[1], (unsigned long long)(memtime() - t_chain));
-        atomicAdd(&g_parse_diag[2], (unsigned long long)s);
-        atomicAdd(&g_parse_diag[3], 1ull);
-        if (attempt) atomicAdd(&g_parse_diag[7], (unsigned long long)attempt);
-        us[kUsStart] = P0;
-        us[kUsNovr] = min(novr, kSegOvr);
-        if (status != RPP_OK) us[kUsFlags] |= kUfTrunc;
-      }
+      if (lane == 0) p.status[b] = status;
       return;
     }
-    if (status == RPP_OK) record(P);  // the end of the last sub-block
-    flush();
-    if (lane == 0) p.status[b] = status;
-    return;
+  };
+  const bool queue = SEG && p.sv.pass == 0;
+  const uint32_t items = queue ? (uint32_t)p.sv.unit_base[p.nblocks] : 0u;
+  for (;;) {
+    uint32_t wid = blockIdx.x * p.waves + wv;
+    if (queue) {
+      uint32_t w = 0;
+      if (lane == 0) w = atomicAdd(p.sv.queue, 1u);
+      wid = __builtin_amdgcn_readfirstlane(w);
+      if (wid >= items) break;
+    }
+    work(wid);
+    if (!queue) break;
   }
 }
 
@@ -2589,7 +2614,7 @@ namespace rpp_internal {
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                         const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback,
-                        const uint64_t* d_units) {
+                        const uint64_t* d_units, uint32_t waves) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
   if (nblocks == 0) return RPP_OK;
@@ -2598,6 +2623,7 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
   // one stream per wave; up to kDecMaxWaves waves share one copy of the
   // transfer tables, fewer when the batch cannot fill the 256 CUs anyway
   uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
+  if (waves) W = std::min<uint32_t>(kDecMaxWaves, waves);
   if (const char* e = getenv("RICEPP_DEC_WAVES")) W = std::min<uint32_t>(kDecMaxWaves, std::max(1, atoi(e)));  // diagnostics
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
   static void (*const kernels[4])(DecParams) = {rpp_decode_kernel<1, false>, rpp_decode_kernel<1, true>,
@@ -2647,9 +2673,17 @@ int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
                      const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,
                      hipStream_t stream) {
   if (nblocks == 0 || sv.units_max == 0) return RPP_OK;
-  // rerun passes have a few units to do: fewer waves per workgroup spread them
-  const uint32_t W = sv.pass == 0 ? std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (sv.units_max + 255) / 256))
-                                  : 1u;
+  // pass 0: a work queue, one full workgroup per CU; rerun passes have a few
+  // units to do: one wave per workgroup, one unit each
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      cus = n;
+    if (cus <= 0) cus = 256;
+  }
+  const uint32_t W = sv.pass == 0 ? kDecMaxWaves : 1u;
+  const uint32_t grid = sv.pass == 0 ? std::min<uint32_t>((uint32_t)cus, (sv.units_max + W - 1) / W) : sv.units_max;
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
   static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1, true>, rpp_parse_kernel<2, true>};
   static std::once_flag attr_once;
@@ -2663,8 +2697,7 @@ int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   if (attr_err != hipSuccess) return RPP_HIP_ERROR;
   ParseParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_sb_base, d_sb_pos, d_status, nblocks,
                 cfg->block_size, W, sv};
-  hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3((sv.units_max + W - 1) / W), dim3(kWave * W),
-                     lds, stream, p);
+  hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3(grid), dim3(kWave * W), lds, stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
