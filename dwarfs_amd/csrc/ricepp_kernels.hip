@@ -2673,8 +2673,8 @@ int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
                      const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,
                      hipStream_t stream) {
   if (nblocks == 0 || sv.units_max == 0) return RPP_OK;
-  // pass 0: a work queue, one full workgroup per CU; rerun passes have a few
-  // units to do: one wave per workgroup, one unit each
+  // pass 0: a work queue, one workgroup per CU; rerun passes have a few units
+  // to do: one wave per workgroup, one unit each
   static int cus = 0;
   if (!cus) {
     int dev = 0, n = 0;
@@ -2682,7 +2682,10 @@ int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
       cus = n;
     if (cus <= 0) cus = 256;
   }
-  const uint32_t W = sv.pass == 0 ? kDecMaxWaves : 1u;
+  // (pass 0: as many waves per workgroup as the unit bound needs to give every
+  // CU some, at most 16, so that a batch of few units still spreads over all CUs)
+  const uint32_t W = sv.pass == 0 ? std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (sv.units_max + cus - 1) / cus))
+                                  : 1u;
   const uint32_t grid = sv.pass == 0 ? std::min<uint32_t>((uint32_t)cus, (sv.units_max + W - 1) / W) : sv.units_max;
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
   static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1, true>, rpp_parse_kernel<2, true>};
