@@ -290,6 +290,14 @@ __device__ __forceinline__ uint64_t pack_state(uint32_t c0, uint32_t c1, uint64_
   return flag | (uint64_t)(c0 & 0x1FFFFu) | ((uint64_t)(c1 & 0x1FFFFu) << 17);
 }
 
+// Asynchronous global -> LDS copy (global_load_lds_dword): lane l's 4 bytes
+// land at LDS byte address m0 + 4 l; retired by s_waitcnt vmcnt(0).
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t m0) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(m0) : "memory");
+}
+
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
@@ -429,35 +437,24 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
     uint16_t* const out = p.out + p.out_off[b];
 
     stamp(0);
-    // ---- stage the tile's words: 16-byte loads, several in flight per
-    //      lane; the group holding the stream's end word by word (zero past
+    // ---- stage the tile's words: asynchronous global -> LDS copies (no
+    //      registers held: every wave issues its 256-byte chunks back to
+    //      back), the chunk holding the stream's end word by word (zero past
     //      the last byte) ----
     const uint32_t w0 = pos_tab[k0] >> 5;
     const uint32_t wend = (pos_tab[k0 + kcount] >> 5) + 2;
     const uint32_t nst = min(wend - w0, kStageWords);
     {
-      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-      const uint32_t nq = (nst + 3) / 4;  // 16-byte groups
-      constexpr uint32_t kInFlight = 4;
-      for (uint32_t q0 = 0; q0 < nq; q0 += kInFlight * kTile) {
-        u4 v[kInFlight];
-#pragma unroll
-        for (uint32_t j = 0; j < kInFlight; ++j) {
-          const uint32_t q = q0 + j * kTile + tid;
-          const uint32_t wq = w0 + 4 * q;
-          if (q < nq && 4 * wq + 16 <= nbytes) {
-            v[j] = *reinterpret_cast<const u4*>(base + 4 * wq);  // (4-byte aligned)
-          } else {
-            v[j] = u4{stream_word(base, nbytes, wq), stream_word(base, nbytes, wq + 1), stream_word(base, nbytes, wq + 2),
-                      stream_word(base, nbytes, wq + 3)};
-          }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kInFlight; ++j) {
-          const uint32_t q = q0 + j * kTile + tid;
-          if (q < nq) *reinterpret_cast<u4*>(&stage[4 * q]) = v[j];
+      const uint32_t l = tid & 63u, wv = tid >> 6;
+      for (uint32_t c = wv; 64 * c < nst; c += kTile / 64) {
+        const uint32_t wq = w0 + 64 * c;
+        if (4 * (wq + 64) <= nbytes) {
+          glds4(base + 4 * (wq + l), __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&stage[64 * c]));
+        } else {
+          stage[64 * c + l] = stream_word(base, nbytes, wq + l);
         }
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     stamp(1);
@@ -598,7 +595,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
     if (active && !fast) decode_general<true>(rd, start, n, carry, out + cbase + comp, CS, be, ulsb);
     // fast lanes: their BS samples, in output order (lane k's BS samples are
     // output samples [k BS, (k+1) BS) of the tile for either CS)
-    uint32_t o32[BS / 2];
+    uint32_t o32[CS == 1 ? 1 : BS / 2];  // (cs 1: the words are r itself)
     if (fast) {
       const uint32_t c2 = carry * 0x10001u;
 #pragma unroll
@@ -607,10 +604,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
         r[i] = px_write2<SH>(__builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, r[i]) + __builtin_bit_cast(us2, c2)),
                              selbe, ulsb);
       }
-      if constexpr (CS == 1) {
-#pragma unroll
-        for (uint32_t i = 0; i < BS / 2; ++i) o32[i] = r[i];
-      } else {
+      if constexpr (CS == 2) {
         // lane 2c holds component 0 of chunk c, lane 2c+1 component 1; the
         // chunk interleaves them.  The even lane takes chunk dwords [0, BS/2),
         // the odd lane [BS/2, BS); dword j = (c0[j], c1[j]).
@@ -626,11 +620,15 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
         }
       }
     }
+    auto word = [&](uint32_t i) -> uint32_t {
+      if constexpr (CS == 1) return r[i];
+      else return o32[i];
+    };
     if (p.dbg & 2) {
       if (fast)
         for (uint32_t i = 0; i < BS / 2; ++i) {
-          out[(size_t)k * BS + 2 * i] = (uint16_t)o32[i];
-          out[(size_t)k * BS + 2 * i + 1] = (uint16_t)(o32[i] >> 16);
+          out[(size_t)k * BS + 2 * i] = (uint16_t)word(i);
+          out[(size_t)k * BS + 2 * i + 1] = (uint16_t)(word(i) >> 16);
         }
     } else if constexpr (BS >= 64) {
       // Through LDS, so that every store instruction writes whole 128-byte
@@ -649,7 +647,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
 #pragma unroll
           for (uint32_t j = 0; j < 8; ++j)
             *reinterpret_cast<uint4*>(tr + l * kRow + 4 * j) =
-                make_uint4(o32[32 * h + 4 * j], o32[32 * h + 4 * j + 1], o32[32 * h + 4 * j + 2], o32[32 * h + 4 * j + 3]);
+                make_uint4(word(32 * h + 4 * j), word(32 * h + 4 * j + 1), word(32 * h + 4 * j + 2), word(32 * h + 4 * j + 3));
         }
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -664,7 +662,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
     } else if (fast) {
       uint4* o = reinterpret_cast<uint4*>(out + (size_t)k * BS);
 #pragma unroll
-      for (uint32_t i = 0; i < BS / 8; ++i) o[i] = make_uint4(o32[4 * i], o32[4 * i + 1], o32[4 * i + 2], o32[4 * i + 3]);
+      for (uint32_t i = 0; i < BS / 8; ++i) o[i] = make_uint4(word(4 * i), word(4 * i + 1), word(4 * i + 2), word(4 * i + 3));
     }
     __syncthreads();  // (stage and scan_buf are reused by the next tile)
     stamp(4);
