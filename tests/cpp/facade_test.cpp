@@ -101,6 +101,10 @@ int main(int argc, char** argv) {
   roundtrip(cfg(128, 1, false, 0), 65536, 50, 5);
   roundtrip(cfg(512, 2, false, 3), 10000, 50, 6);
   roundtrip(cfg(8, 1, true, 0), 3001, 50, 11);  // the factory accepts any size <= 512
+  // DwarFS block sizes (mkdwarfs -S 22 / -S 24): one call = one long stream, encoded and
+  // decoded by several waves (the segmented paths behind the facade's _ws launches)
+  roundtrip(cfg(128, 1, true, 0), (size_t)8 << 20, 50, 12);
+  roundtrip(cfg(128, 2, false, 2), (size_t)2 << 20, 50, 13);
 
   // codec_test.cpp:154-196: worst-case KATs; incompressible == worst case
   {

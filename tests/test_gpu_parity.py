@@ -524,3 +524,13 @@ def test_segmented_decode_is_chosen_for_long_streams():
     assert stats["met"] > 0 and stats["fallback"] == 0, stats
     with _decode_mode("fused"):
         _decode_oracle_streams(cfg, blocks[1:3])
+
+
+def test_segmented_decode_of_a_64mib_stream():
+    """The longest stream of the suite: 32 Mi samples (64 MiB) in one stream, cs 2, little endian, ulsb 1 --
+    segmented encode and decode against the oracle byte for byte."""
+    rng = np.random.default_rng(6464)
+    x = datagen.poisson_data(rng, 32 << 20, lam=700.0, ulsb=1, big_endian=False)
+    codec.segmented_decode_stats(reset=True)
+    run_batch(codec.CodecConfig(128, 2, "little", 1), [x])
+    assert codec.segmented_decode_stats(reset=True)["met"] > 0
