@@ -1022,6 +1022,10 @@ RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc")
 // shift, initialised to the identity map (opaque to the compiler)
 struct ScanRegs {
   Map8 r1, r2, r4, r8, b15, b31, w1;
+  // entry-state rounds (jacobi8, fs >= 8 loop): lane 0 holds the window's
+  // entry state (skip the 4-bit header) in replicated form and is never
+  // written
+  uint32_t ja, jb;
   __device__ ScanRegs() {
     Map8* all[7] = {&r1, &r2, &r4, &r8, &b15, &b31, &w1};
     for (Map8* x : all) {
@@ -1029,8 +1033,61 @@ struct ScanRegs {
       x->hi = kId1;
       asm volatile("" : "+v"(x->lo), "+v"(x->hi));
     }
+    ja = jb = 0x04040404u;
+    asm volatile("" : "+v"(ja), "+v"(jb));
   }
 };
+// the value of lane l-1 into `keep` (lane 0 keeps its value)
+__device__ __forceinline__ uint32_t jshift(uint32_t x, uint32_t& keep) {
+  asm("s_nop 1\n\tv_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(keep) : "v"(x));
+  return keep;
+}
+// Entry states of the lanes' segments by fixed-point rounds instead of the
+// map scan.  With E_0 = 4 (skip the header), E_l = M_(l-1)(E_(l-1)) defines
+// the exact entry states; a round sets E_l <- M_(l-1)(E_l-1) for all lanes at
+// once (one v_perm + one DPP move), starting from "state 0 before every
+// lane".  Parses from different states of a Rice stream merge within a few
+// codes, so after R rounds E is exact for every lane whose R preceding
+// segments merge all entry states.  Returns E after R + 1 rounds in selector
+// form (the state replicated in all four bytes) and in `unsettled` the lanes where
+// the last round still changed E.  If no lane up to l changed, E is exact up
+// to lane l (induction from lane 0), so the caller needs the map scan only
+// when an unsettled lane lies before the sub-block's end (rare).
+#ifndef RPP_JACOBI
+#define RPP_JACOBI 0  // measured: rounds 4 / 6 / 8 = 286 / 267 / 265 us vs 262 us with the scan (bench decode)
+#endif
+template <int R>
+__device__ __forceinline__ uint32_t jacobi8(Map8 M, ScanRegs& sr, uint64_t& unsettled) {
+  uint32_t ea = jshift(__builtin_amdgcn_perm(M.hi, M.lo, 0u), sr.ja), eb = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (r & 1) ea = jshift(__builtin_amdgcn_perm(M.hi, M.lo, eb), sr.ja);
+    else eb = jshift(__builtin_amdgcn_perm(M.hi, M.lo, ea), sr.jb);
+  }
+  unsettled = __ballot(ea != eb);
+  return (R & 1) ? eb : ea;
+}
+
+// fs >= 8: states 0..13 (13 remainder bits still to skip at most).  A state
+// is kept replicated in all four bytes of a dword (a v_perm selector that
+// yields the looked-up byte in all four bytes).  One byte of the segment:
+// states 0..7 go through the byte's 8-entry map (table entry .x/.y); a state
+// s >= 8 skips the byte (s - 8).  v_perm gives 0x00 for selectors 8..12 (the
+// map bytes are < 0x80) and 0xFF for 13, so s' = max_i16(perm, s - 8) per
+// half-word: below 8 the subtraction is negative in both halves.
+constexpr int kJacobi16 = 4;  // fixed rounds before the settle check (fs >= 8)
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+  return as_u32(__builtin_bit_cast(us2, __builtin_elementwise_max(__builtin_bit_cast(ss2, a), __builtin_bit_cast(ss2, b))));
+}
+__device__ __forceinline__ uint32_t byte_step(uint32_t S, uint4 e) {
+  return pk_max_i16(__builtin_amdgcn_perm(e.y, e.x, S), S - 0x08080808u);
+}
+// the byte's terminator bits when entered in state S (none when skipped)
+__device__ __forceinline__ uint32_t byte_term(uint32_t S, uint4 e) {
+  uint32_t skip;  // all ones for s >= 8 (bit 3; s <= 13)
+  asm("v_bfe_i32 %0, %1, 3, 1" : "=v"(skip) : "v"(S));
+  return __builtin_amdgcn_perm(e.w, e.z, S) & ~skip;
+}
 #undef RPP_SCAN8_STEP
 // exclusive form: the map of lanes 0..l-1 (identity on lane 0)
 __device__ __forceinline__ Map8 shift8_wave(Map8 m, Map8& keep) {
@@ -1148,7 +1205,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
   const uint32_t selpack = be ? 0x04050001u : 0x05040100u;  // v_perm(hi, lo): pack two samples (+ swap)
-  const uint32_t lane24 = kSegBits * lane, lane24m4 = lane24 - 4u;
+  const uint32_t lane24 = kSegBits * lane;
   const uint32_t b = blockIdx.x * p.waves + wv;
   if (b >= p.nblocks) return;  // no barrier below this point
   if (p.only_fallback && p.status[b] != rpp_internal::kSegFallback) return;
@@ -1302,23 +1359,38 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
     //      lookups, scans) in the same basic block, so the LDS latencies and
     //      DPP chains of the two overlap.  Anything else leaves the loop and
     //      takes the general path below for that sub-block. ----
-    // MT: terminators a 24-bit segment can hold (codes of >= fs + 1 bits),
-    // [LO, HI]: the fs range of this instance
+    // MT: terminators a lane segment can hold (codes of >= fs + 1 bits),
+    // [LO, HI]: the fs range of this instance (fs 8..13: 32-bit segments)
     // TWO: bs 128, two codes per lane; else bs <= 64, one code per lane
     auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI, bool TWO>() {
+      // fs >= 8: 32-bit lane segments (2048-bit windows), entry states by
+      // jacobi rounds over 14 states; else 24-bit segments and 8-state maps
+      constexpr bool W32 = LO >= 8;
+      constexpr uint32_t SB = W32 ? 32u : kSegBits;
       const uint32_t n = TWO ? 2 * kWave : bs;
       const uint4* const list4 = reinterpret_cast<const uint4*>(list);
       uint2* const list2 = reinterpret_cast<uint2*>(list);
-      // this lane's 32 bits from bit q + 24 lane (its 24-bit segment and 8
-      // more: a terminator in the segment has its <= 7 remainder bits in them)
-      // (window start word and bit offset are scalar; the lane's words lie
-      // within 50 words of the window start, inside the ring's mirror)
-      auto seg_bits = [&](uint32_t q) {
-        const uint32_t o = lane24 + (q & 31u);
-        uint32_t oi = o >> 5;
-        asm("" : "+v"(oi));  // (else the compiler masks o >> 3: one more op)
-        const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
-        return __builtin_amdgcn_alignbit(w[1], w[0], o);  // (shift o mod 32)
+      // this lane's 32 bits from bit q + SB lane (24-bit segments: the
+      // segment and 8 more, where a terminator in it has its <= 7 remainder
+      // bits; 32-bit segments: the next 32 bits in xh)
+      // (window start word and bit offset are scalar; 24-bit segments: the
+      // lane's words lie within 50 words of the window start, inside the
+      // ring's mirror; 32-bit segments: the first word index is wrapped per
+      // lane, the next two are in the mirror)
+      auto seg_bits = [&](uint32_t q, uint32_t& xh) {
+        if constexpr (W32) {
+          const uint32_t* w = ring + (((q >> 5) + lane) & kRingMask);
+          const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+          xh = __builtin_amdgcn_alignbit(w2, w1, q & 31u);
+          return __builtin_amdgcn_alignbit(w1, w0, q & 31u);
+        } else {
+          const uint32_t o = lane24 + (q & 31u);
+          uint32_t oi = o >> 5;
+          asm("" : "+v"(oi));  // (else the compiler masks o >> 3: one more op)
+          const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
+          xh = 0u;
+          return __builtin_amdgcn_alignbit(w[1], w[0], o);  // (shift o mod 32)
+        }
       };
       // the header's fs clamped to [LO, HI] (scalar), so the lookups stay in
       // range for any header; the loop only keeps sub-blocks whose fs is in
@@ -1340,34 +1412,110 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // The count scan also carries a rider: the previous sub-block's delta
       // sums in the high halves (mod 2^16; counts <= 512 stay in the low
       // halves), so that sub-block's value prefix costs no scan of its own.
-      auto parse = [&](uint32_t q, uint32_t xl, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe,
-                       uint32_t rider, uint32_t& rider_incl) -> bool {
+      auto parse = [&](uint32_t q, uint32_t xl, uint32_t xh, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint4 e3,
+                       uint32_t& Pe, uint32_t rider, uint32_t& rider_incl) -> bool {
         const uint32_t k = fs + 1;
-        const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});  // (also gives byte 2's entry state)
-        Map8 M = comp8(Map8{e2.x, e2.y}, M01);
-        M = scan8_shr1(M, sreg.r1);
-        M = scan8_shr2(M, sreg.r2);
-        M = scan8_shr4(M, sreg.r4);
-        M = scan8_shr8(M, sreg.r8);
-        M = scan8_bc15(M, sreg.b15);
-        M = scan8_bc31(M, sreg.b31);
-        const Map8 X = shift8_wave(M, sreg.w1);
-        RPP_TSTAMP(3);
-        // state 4 at the window start: skip the header.  The selectors
-        // carry the state in byte 0 and 0xFF (a v_perm selector for 0xFF)
-        // in bytes 1-3, so each byte's next state comes out of its v_perm
-        // as the next selector, with no masking.
-        const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
-        const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-        const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
-        const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
-        // terminator mask: byte 0 of a0, a1, a2 -> bytes 0, 1, 2
-        uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
-        const uint32_t cnt = __builtin_popcount(tm);
-        const uint32_t incl2 = wave_incl_sum(cnt | (rider << 16));
-        const uint32_t incl = incl2 & 0xFFFFu;
-        rider_incl = incl2 >> 16;
-        const uint64_t finm = __ballot(incl >= n);
+        uint32_t tm, cnt, incl;
+        uint64_t finm;
+        // lanes up to the first one that ends the sub-block (all when none
+        // does)
+        auto upto_end = [](uint64_t fm) {
+          return (2ull << (uint32_t)__builtin_ctzll(fm | (1ull << 63))) - 1ull;
+        };
+        if constexpr (!W32) {
+          const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});  // (also gives byte 2's entry state)
+          const Map8 M = comp8(Map8{e2.x, e2.y}, M01);
+          // state 4 at the window start: skip the header.  A selector
+          // carries the state in byte 0 (the other bytes are 0xFF or copies
+          // of byte 0), so each byte's next state comes out of its v_perm as
+          // the next selector, with no masking.
+          auto scan_sel = [&]() {
+            Map8 S = scan8_shr1(M, sreg.r1);
+            S = scan8_shr2(S, sreg.r2);
+            S = scan8_shr4(S, sreg.r4);
+            S = scan8_shr8(S, sreg.r8);
+            S = scan8_bc15(S, sreg.b15);
+            S = scan8_bc31(S, sreg.b31);
+            const Map8 X = shift8_wave(S, sreg.w1);
+            return __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
+          };
+          // terminator mask of the segment entered in state sel: byte 0 of
+          // a0, a1, a2 -> bytes 0, 1, 2
+          auto term_mask = [&](uint32_t sel) {
+            const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+            const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
+            const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
+            return __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
+          };
+#if RPP_JACOBI > 0
+          uint64_t unsettled;
+          tm = term_mask(jacobi8<RPP_JACOBI>(M, sreg, unsettled));
+#else
+          tm = term_mask(scan_sel());
+#endif
+          cnt = __builtin_popcount(tm);
+          const uint32_t incl2 = wave_incl_sum(cnt | (rider << 16));
+          incl = incl2 & 0xFFFFu;
+          // (the rider in the high halves is exact whatever the counts: they
+          // sum to at most 512 and never carry into it)
+          rider_incl = incl2 >> 16;
+          finm = __ballot(incl >= n);
+#if RPP_JACOBI > 0
+          if (unsettled & upto_end(finm)) {
+            RPP_STAT(9, 1);
+            tm = term_mask(scan_sel());
+            cnt = __builtin_popcount(tm);
+            incl = wave_incl_sum(cnt);
+            finm = __ballot(incl >= n);
+          }
+#endif
+        } else {
+          // fs 8..13: states 0..13, 32-bit segments, no map scan: the entry
+          // states by jacobi rounds of byte steps (states in replicated
+          // form, byte_step), the per-byte states of the final round give
+          // the terminators.
+          uint32_t S1, S2, S3;
+          auto eval = [&](uint32_t S0) {
+            S1 = byte_step(S0, e0);
+            S2 = byte_step(S1, e1);
+            S3 = byte_step(S2, e2);
+            return byte_step(S3, e3);
+          };
+          auto term_mask = [&](uint32_t S0) {
+            const uint32_t a0 = byte_term(S0, e0), a1 = byte_term(S1, e1), a2 = byte_term(S2, e2),
+                           a3 = byte_term(S3, e3);
+            return __builtin_amdgcn_perm(a3, a2, 0x04000C0Cu) | __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u);
+          };
+          uint32_t ea = jshift(eval(0u), sreg.ja), eb = 0;
+#pragma unroll
+          for (int r = 0; r < kJacobi16; ++r) {
+            if (r & 1) ea = jshift(eval(eb), sreg.ja);
+            else eb = jshift(eval(ea), sreg.jb);
+          }
+          // the last eval ran on the older of ea / eb; where the round
+          // changed nothing its byte states are exact
+          uint32_t Sold = (kJacobi16 & 1) ? ea : eb;
+          uint32_t Snew = (kJacobi16 & 1) ? eb : ea;
+          uint64_t unsettled = __ballot(Sold != Snew);
+          tm = term_mask(Sold);
+          cnt = __builtin_popcount(tm);
+          const uint32_t incl2 = wave_incl_sum(cnt | (rider << 16));
+          incl = incl2 & 0xFFFFu;
+          rider_incl = incl2 >> 16;
+          finm = __ballot(incl >= n);
+          // more rounds until every lane up to the sub-block's end is
+          // settled (lane l is exact after l rounds: at most 64)
+          for (uint32_t guard = 0; (unsettled & upto_end(finm)) && guard < 2 * kWave; ++guard) {
+            RPP_STAT(9, 1);
+            Sold = Snew;
+            Snew = jshift(eval(Sold), sreg.ja);
+            unsettled = __ballot(Sold != Snew);
+            tm = term_mask(Sold);
+            cnt = __builtin_popcount(tm);
+            incl = wave_incl_sum(cnt);
+            finm = __ballot(incl >= n);
+          }
+        }
         const uint32_t excl = incl - cnt;
         RPP_TSTAMP(7);
         // terminator positions t0 < t1 < ... in the segment (garbage past
@@ -1393,7 +1541,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // (bit 63 set: a defined lane when no lane ends the sub-block; Pe is
         // then unused)
         const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
-        Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
+        Pe = q + SB * lz + readlane(tend, (int)lz) + k;
         RPP_TSTAMP(8);
         // pair excl + j for j = MT-1 .. 0, one instruction each (kept apart:
         // a merged ds_write2 would put two j in one instruction): a slot past
@@ -1401,12 +1549,15 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // later instruction (its j is smaller); lanes without terminators or
         // past the sub-block write the unused pairs from 256
         const uint32_t base = cnt != 0 && excl < n ? excl : 256u;
-        uint32_t abase = (uint32_t)((int)lane24m4 + __mul24((int)base, -(int)k));
+        uint32_t abase = (uint32_t)((int)(SB * lane - 4u) + __mul24((int)base, -(int)k));
         asm volatile("" : "+v"(abase));  // computed once, not per pair
         const uint32_t xr = xl >> 1;     // the remainder of a terminator at t is bits t+1 .. t+fs
 #pragma unroll
         for (int j = MT - 1; j >= 0; --j) {
-          list2[base + j] = make_uint2(abase + t[j] - j * k, __builtin_amdgcn_ubfe(xr, t[j], fs));
+          // (32-bit segments: the remainder may reach into the next word)
+          const uint32_t rem = W32 ? __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(xh, xl, t[j]), 1, fs)
+                                   : __builtin_amdgcn_ubfe(xr, t[j], fs);
+          list2[base + j] = make_uint2(abase + t[j] - j * k, rem);
           lds_fence();
         }
         RPP_TSTAMP(13);
@@ -1473,11 +1624,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         if (comp) last1 = lnew;
         else last0 = lnew;
       };
-      auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2) {
+      auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2, uint4& e3) {
         const uint4* tb = tab + 256u * fs;
         e0 = tb[xl & 0xFFu];
         e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
         e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+        if constexpr (W32) e3 = tb[xl >> 24];
+        else e3 = make_uint4(0u, 0u, 0u, 0u);
       };
 
       // Ring bounds, recomputed only when the ring changes: the next window
@@ -1492,13 +1645,14 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       ring_bounds();
       // prologue: parse sub-block s
       uint32_t Pn;
-      uint32_t xl = seg_bits(P);
+      uint32_t xh;
+      uint32_t xl = seg_bits(P, xh);
       const uint32_t h = __builtin_amdgcn_readfirstlane(xl);
       uint32_t fs = fs_of(h);
-      uint4 e0, e1, e2;
-      lookups(xl, fs, e0, e1, e2);
+      uint4 e0, e1, e2, e3;
+      lookups(xl, fs, e0, e1, e2, e3);
       uint32_t unused_rider;
-      bool ok = parse(P, xl, fs, e0, e1, e2, Pn, 0u, unused_rider) && header_ok(h);
+      bool ok = parse(P, xl, xh, fs, e0, e1, e2, e3, Pn, 0u, unused_rider) && header_ok(h);
       while (ok) {
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
@@ -1509,12 +1663,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           const uint2 t2 = list2[lane];
           tt = make_uint4(t2.x, t2.y, 0u, 0u);
         }
-        const uint32_t xlB = seg_bits(Pn);
+        uint32_t xhB;
+        const uint32_t xlB = seg_bits(Pn, xhB);
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
         RPP_TSTAMP(1);
         RPP_STAT(0, 1);
         const uint32_t fsB = fs_of(hB);
-        lookups(xlB, fsB, e0, e1, e2);
+        lookups(xlB, fsB, e0, e1, e2, e3);
         uint32_t d1A, sumA, incA;
         deltas(tt, fs, d1A, sumA);
         if (RPP_ABLATE & 1024) asm volatile(".rept 20\n\tv_nop\n\t.endr" ::: "memory");
@@ -1539,7 +1694,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         }
         RPP_TSTAMP(2);
         uint32_t PnB;
-        ok = parse(Pn, xlB, fsB, e0, e1, e2, PnB, sumA, incA) && header_ok(hB) && nxt;
+        ok = parse(Pn, xlB, xhB, fsB, e0, e1, e2, e3, PnB, sumA, incA) && header_ok(hB) && nxt;
         store(d1A, incA, s);
         ++s;
         P = Pn;
@@ -1566,9 +1721,11 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       if (bs == 2 * kWave) {
         if (h - 6u <= 2u) fast.template operator()<4, 5, 7, true>();
         else if (h - 3u <= 2u) fast.template operator()<8, 2, 4, true>();
+        else if (h - 9u <= 5u) fast.template operator()<4, 8, 13, true>();
       } else {
         if (h - 6u <= 2u) fast.template operator()<4, 5, 7, false>();
         else if (h - 3u <= 2u) fast.template operator()<8, 2, 4, false>();
+        else if (h - 9u <= 5u) fast.template operator()<4, 8, 13, false>();
       }
       last0 &= 0xFFFFu;
       last1 &= 0xFFFFu;

@@ -95,6 +95,30 @@ def test_rice_parameter_classes(bs, cs, ulsb):
     run_batch(codec.CodecConfig(bs, cs, "big", ulsb), blocks)
 
 
+@pytest.mark.parametrize("bs", [16, 32, 64, 128])
+@pytest.mark.parametrize("cs", [1, 2])
+@pytest.mark.parametrize("ulsb", [0, 3])
+def test_high_rice_parameters(bs, cs, ulsb):
+    """fs 8-13 (the decoder's 32-bit-segment loop with jacobi entry states):
+    uniform noise of 9..14 bits (each class alone, and switching class per
+    sub-block), the configs[0] generator (noise + full-range outliers: raw
+    sub-blocks between Rice ones), and noisy sub-blocks whose codes overflow
+    a 2048-bit window (general path between loop runs)."""
+    rng = np.random.default_rng(5 + 100 * bs + 10 * cs + ulsb)
+    top = 16 - ulsb
+
+    def noise(count, bits):
+        base = int(rng.integers(0, 1 << top))
+        v = (base + rng.integers(0, 1 << min(bits, top), count)) & ((1 << top) - 1)
+        return datagen.store(v.astype(np.uint64) << ulsb, ulsb, True)
+
+    n = bs * cs * 40
+    blocks = [noise(n, b) for b in range(9, 16)]
+    blocks.append(np.concatenate([noise(bs * cs, int(rng.integers(8, 16))) for _ in range(150)]))
+    blocks.append(datagen.benchmark_data(rng, n + 7 * cs, ulsb, True))
+    run_batch(codec.CodecConfig(bs, cs, "big", ulsb), blocks)
+
+
 @pytest.mark.parametrize("ulsb", list(range(0, 16)))
 def test_unused_lsb_sweep(ulsb):
     rng = np.random.default_rng(ulsb)
