@@ -1122,6 +1122,58 @@ __device__ __forceinline__ Map16 scan_step16(const Map16& m) {
   return comp16(m, d);
 }
 
+// Front end of the fs 8..13 parse (32-bit lane segments): states 0..13 and no
+// map scan -- the entry states by jacobi rounds of byte steps (states in
+// replicated form, byte_step); the per-byte states of the final round give
+// the terminator mask tm of the lane's segment; then the counts (inclusive
+// prefix incl, the lanes reaching n codes in finm) and the rider's prefix as
+// in the fused fast loop.
+__device__ __forceinline__ void w32_count(uint4 e0, uint4 e1, uint4 e2, uint4 e3, uint32_t n, uint32_t rider,
+                                          ScanRegs& sreg, uint32_t& tm, uint32_t& cnt, uint32_t& incl,
+                                          uint64_t& finm, uint32_t& rider_incl) {
+  // lanes up to the first one that ends the sub-block (all when none does)
+  auto upto_end = [](uint64_t fm) { return (2ull << (uint32_t)__builtin_ctzll(fm | (1ull << 63))) - 1ull; };
+  uint32_t S1, S2, S3;
+  auto eval = [&](uint32_t S0) {
+    S1 = byte_step(S0, e0);
+    S2 = byte_step(S1, e1);
+    S3 = byte_step(S2, e2);
+    return byte_step(S3, e3);
+  };
+  auto term_mask = [&](uint32_t S0) {
+    const uint32_t a0 = byte_term(S0, e0), a1 = byte_term(S1, e1), a2 = byte_term(S2, e2), a3 = byte_term(S3, e3);
+    return __builtin_amdgcn_perm(a3, a2, 0x04000C0Cu) | __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u);
+  };
+  uint32_t ea = jshift(eval(0u), sreg.ja), eb = 0;
+#pragma unroll
+  for (int r = 0; r < kJacobi16; ++r) {
+    if (r & 1) ea = jshift(eval(eb), sreg.ja);
+    else eb = jshift(eval(ea), sreg.jb);
+  }
+  // the last eval ran on the older of ea / eb; where the round changed
+  // nothing its byte states are exact
+  uint32_t Sold = (kJacobi16 & 1) ? ea : eb;
+  uint32_t Snew = (kJacobi16 & 1) ? eb : ea;
+  uint64_t unsettled = __ballot(Sold != Snew);
+  tm = term_mask(Sold);
+  cnt = __builtin_popcount(tm);
+  const uint32_t incl2 = wave_incl_sum(cnt | (rider << 16));
+  incl = incl2 & 0xFFFFu;
+  rider_incl = incl2 >> 16;
+  finm = __ballot(incl >= n);
+  // more rounds until every lane up to the sub-block's end is settled (lane
+  // l is exact after l rounds: at most 64)
+  for (uint32_t guard = 0; (unsettled & upto_end(finm)) && guard < 2 * kWave; ++guard) {
+    Sold = Snew;
+    Snew = jshift(eval(Sold), sreg.ja);
+    unsettled = __ballot(Sold != Snew);
+    tm = term_mask(Sold);
+    cnt = __builtin_popcount(tm);
+    incl = wave_incl_sum(cnt);
+    finm = __ballot(incl >= n);
+  }
+}
+
 // Orders this wave's LDS accesses without waiting on its global stores
 // (LDS operations of one wave complete in order; a full __syncthreads()
 // would also drain vmcnt, i.e. wait for the previous chunk's output stores).
@@ -1470,51 +1522,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           }
 #endif
         } else {
-          // fs 8..13: states 0..13, 32-bit segments, no map scan: the entry
-          // states by jacobi rounds of byte steps (states in replicated
-          // form, byte_step), the per-byte states of the final round give
-          // the terminators.
-          uint32_t S1, S2, S3;
-          auto eval = [&](uint32_t S0) {
-            S1 = byte_step(S0, e0);
-            S2 = byte_step(S1, e1);
-            S3 = byte_step(S2, e2);
-            return byte_step(S3, e3);
-          };
-          auto term_mask = [&](uint32_t S0) {
-            const uint32_t a0 = byte_term(S0, e0), a1 = byte_term(S1, e1), a2 = byte_term(S2, e2),
-                           a3 = byte_term(S3, e3);
-            return __builtin_amdgcn_perm(a3, a2, 0x04000C0Cu) | __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u);
-          };
-          uint32_t ea = jshift(eval(0u), sreg.ja), eb = 0;
-#pragma unroll
-          for (int r = 0; r < kJacobi16; ++r) {
-            if (r & 1) ea = jshift(eval(eb), sreg.ja);
-            else eb = jshift(eval(ea), sreg.jb);
-          }
-          // the last eval ran on the older of ea / eb; where the round
-          // changed nothing its byte states are exact
-          uint32_t Sold = (kJacobi16 & 1) ? ea : eb;
-          uint32_t Snew = (kJacobi16 & 1) ? eb : ea;
-          uint64_t unsettled = __ballot(Sold != Snew);
-          tm = term_mask(Sold);
-          cnt = __builtin_popcount(tm);
-          const uint32_t incl2 = wave_incl_sum(cnt | (rider << 16));
-          incl = incl2 & 0xFFFFu;
-          rider_incl = incl2 >> 16;
-          finm = __ballot(incl >= n);
-          // more rounds until every lane up to the sub-block's end is
-          // settled (lane l is exact after l rounds: at most 64)
-          for (uint32_t guard = 0; (unsettled & upto_end(finm)) && guard < 2 * kWave; ++guard) {
-            RPP_STAT(9, 1);
-            Sold = Snew;
-            Snew = jshift(eval(Sold), sreg.ja);
-            unsettled = __ballot(Sold != Snew);
-            tm = term_mask(Sold);
-            cnt = __builtin_popcount(tm);
-            incl = wave_incl_sum(cnt);
-            finm = __ballot(incl >= n);
-          }
+          w32_count(e0, e1, e2, e3, n, rider, sreg, tm, cnt, incl, finm, rider_incl);
         }
         const uint32_t excl = incl - cnt;
         RPP_TSTAMP(7);
@@ -2397,13 +2405,21 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
         //      in one window, ring resident; the parse of sub-block s+1 is issued
         //      as soon as the end of s is known ----
         auto fast = [&]<uint32_t MT, uint32_t LO, uint32_t HI>() {
+          // fs 8..13: 32-bit lane segments and jacobi entry states (w32_count)
+          constexpr bool W32 = LO >= 8;
+          constexpr uint32_t SB = W32 ? 32u : kSegBits;
           const uint32_t n = bs;
           auto seg_bits = [&](uint32_t q) {
-            const uint32_t o = lane24 + (q & 31u);
-            uint32_t oi = o >> 5;
-            asm("" : "+v"(oi));
-            const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
-            return __builtin_amdgcn_alignbit(w[1], w[0], o);
+            if constexpr (W32) {
+              const uint32_t* w = ring + (((q >> 5) + lane) & kRingMask);
+              return __builtin_amdgcn_alignbit(w[1], w[0], q & 31u);
+            } else {
+              const uint32_t o = lane24 + (q & 31u);
+              uint32_t oi = o >> 5;
+              asm("" : "+v"(oi));
+              const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
+              return __builtin_amdgcn_alignbit(w[1], w[0], o);
+            }
           };
           auto fs_of = [](uint32_t h) {
             uint32_t r;
@@ -2415,25 +2431,32 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
           };
           auto header_ok = [](uint32_t h) { return (h & 15u) - (LO + 1) <= HI - LO; };
           // end (next header) of the sub-block at bit q, if it lies in the window
-          auto parse = [&](uint32_t q, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint32_t& Pe) -> bool {
+          auto parse = [&](uint32_t q, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint4 e3, uint32_t& Pe) -> bool {
             const uint32_t k = fs + 1;
-            const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});
-            Map8 M = comp8(Map8{e2.x, e2.y}, M01);
-            M = scan8_shr1(M, sreg.r1);
-            M = scan8_shr2(M, sreg.r2);
-            M = scan8_shr4(M, sreg.r4);
-            M = scan8_shr8(M, sreg.r8);
-            M = scan8_bc15(M, sreg.b15);
-            M = scan8_bc31(M, sreg.b31);
-            const Map8 X = shift8_wave(M, sreg.w1);
-            const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
-            const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
-            const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
-            const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
-            uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
-            const uint32_t cnt = __builtin_popcount(tm);
-            const uint32_t incl = wave_incl_sum(cnt);
-            const uint64_t finm = __ballot(incl >= n);
+            uint32_t tm, cnt, incl;
+            uint64_t finm;
+            if constexpr (W32) {
+              uint32_t unused_rider;
+              w32_count(e0, e1, e2, e3, n, 0u, sreg, tm, cnt, incl, finm, unused_rider);
+            } else {
+              const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});
+              Map8 M = comp8(Map8{e2.x, e2.y}, M01);
+              M = scan8_shr1(M, sreg.r1);
+              M = scan8_shr2(M, sreg.r2);
+              M = scan8_shr4(M, sreg.r4);
+              M = scan8_shr8(M, sreg.r8);
+              M = scan8_bc15(M, sreg.b15);
+              M = scan8_bc31(M, sreg.b31);
+              const Map8 X = shift8_wave(M, sreg.w1);
+              const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);
+              const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+              const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
+              const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
+              tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
+              cnt = __builtin_popcount(tm);
+              incl = wave_incl_sum(cnt);
+              finm = __ballot(incl >= n);
+            }
             const uint32_t excl = incl - cnt;
             uint32_t t[MT];
     #pragma unroll
@@ -2449,14 +2472,16 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
             }
             const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
             const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
-            Pe = q + kSegBits * lz + readlane(tend, (int)lz) + k;
+            Pe = q + SB * lz + readlane(tend, (int)lz) + k;
             return finm != 0;
           };
-          auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2) {
+          auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2, uint4& e3) {
             const uint4* tb = tab + 256u * fs;
             e0 = tb[xl & 0xFFu];
             e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
             e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+            if constexpr (W32) e3 = tb[xl >> 24];
+            else e3 = make_uint4(0u, 0u, 0u, 0u);
           };
           uint32_t pn_limit, trig_w;
           auto ring_bounds = [&]() {
@@ -2468,9 +2493,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
           const uint32_t xl = seg_bits(P);
           const uint32_t h = __builtin_amdgcn_readfirstlane(xl);
           uint32_t fs = fs_of(h);
-          uint4 e0, e1, e2;
-          lookups(xl, fs, e0, e1, e2);
-          bool ok = parse(P, fs, e0, e1, e2, Pn) && header_ok(h);
+          uint4 e0, e1, e2, e3;
+          lookups(xl, fs, e0, e1, e2, e3);
+          bool ok = parse(P, fs, e0, e1, e2, e3, Pn) && header_ok(h);
           uint32_t hc = h;  // header of the sub-block at P
           while (ok) {
             // sub-block s at P ends at Pn; parse s+1 at Pn
@@ -2478,9 +2503,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
             const uint32_t xlB = seg_bits(Pn);
             const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
             const uint32_t fsB = fs_of(hB);
-            lookups(xlB, fsB, e0, e1, e2);
+            lookups(xlB, fsB, e0, e1, e2, e3);
             uint32_t PnB;
-            ok = parse(Pn, fsB, e0, e1, e2, PnB) && header_ok(hB) && nxt;
+            ok = parse(Pn, fsB, e0, e1, e2, e3, PnB) && header_ok(hB) && nxt;
             record(P);
             if (multi) note(hc & 15u);
             hc = hB;
@@ -2504,6 +2529,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
           const uint32_t s0 = s;
           if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
           else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
+          else if (h - 9u <= 5u) fast.template operator()<4, 8, 13>();
           if (s == s0) break;  // the general path takes this sub-block
         }
         if (s >= nsb || status != RPP_OK || stop) break;

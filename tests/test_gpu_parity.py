@@ -116,7 +116,13 @@ def test_high_rice_parameters(bs, cs, ulsb):
     blocks = [noise(n, b) for b in range(9, 16)]
     blocks.append(np.concatenate([noise(bs * cs, int(rng.integers(8, 16))) for _ in range(150)]))
     blocks.append(datagen.benchmark_data(rng, n + 7 * cs, ulsb, True))
-    run_batch(codec.CodecConfig(bs, cs, "big", ulsb), blocks)
+    cfg = codec.CodecConfig(bs, cs, "big", ulsb)
+    run_batch(cfg, blocks)
+    # the same streams split into 4 Kib / 32 Kib units (the segmented
+    # decode's parse runs the same loop per unit)
+    for log2 in (12, 15):
+        with _decode_mode("segmented", log2):
+            run_batch(cfg, blocks)
 
 
 @pytest.mark.parametrize("ulsb", list(range(0, 16)))
