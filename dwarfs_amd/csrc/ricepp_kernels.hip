@@ -1465,7 +1465,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // sums in the high halves (mod 2^16; counts <= 512 stay in the low
       // halves), so that sub-block's value prefix costs no scan of its own.
       auto parse = [&](uint32_t q, uint32_t xl, uint32_t xh, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint4 e3,
-                       uint32_t& Pe, uint32_t rider, uint32_t& rider_incl) -> bool {
+                       uint32_t& Pe, uint32_t rider, uint32_t& rider_incl, auto&& mid) -> bool {
         const uint32_t k = fs + 1;
         uint32_t tm, cnt, incl;
         uint64_t finm;
@@ -1511,6 +1511,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           // (the rider in the high halves is exact whatever the counts: they
           // sum to at most 512 and never carry into it)
           rider_incl = incl2 >> 16;
+          // (the previous sub-block's stores, issued before the settle
+          // branch so that they overlap this parse)
+          mid(rider_incl);
           finm = __ballot(incl >= n);
 #if RPP_JACOBI > 0
           if (unsettled & upto_end(finm)) {
@@ -1523,6 +1526,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
 #endif
         } else {
           w32_count(e0, e1, e2, e3, n, rider, sreg, tm, cnt, incl, finm, rider_incl);
+          mid(rider_incl);
         }
         const uint32_t excl = incl - cnt;
         RPP_TSTAMP(7);
@@ -1660,7 +1664,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       uint4 e0, e1, e2, e3;
       lookups(xl, fs, e0, e1, e2, e3);
       uint32_t unused_rider;
-      bool ok = parse(P, xl, xh, fs, e0, e1, e2, e3, Pn, 0u, unused_rider) && header_ok(h);
+      bool ok = parse(P, xl, xh, fs, e0, e1, e2, e3, Pn, 0u, unused_rider, [](uint32_t) {}) && header_ok(h);
       while (ok) {
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
@@ -1702,8 +1706,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         }
         RPP_TSTAMP(2);
         uint32_t PnB;
-        ok = parse(Pn, xlB, xhB, fsB, e0, e1, e2, e3, PnB, sumA, incA) && header_ok(hB) && nxt;
-        store(d1A, incA, s);
+        ok = parse(Pn, xlB, xhB, fsB, e0, e1, e2, e3, PnB, sumA, incA,
+                   [&](uint32_t inc) { store(d1A, inc, s); }) &&
+             header_ok(hB) && nxt;
         ++s;
         P = Pn;
         if (!ok) {
