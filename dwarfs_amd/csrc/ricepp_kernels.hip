@@ -947,7 +947,7 @@ constexpr uint32_t kAhead = 288;                 // words kept resident ahead of
 constexpr uint32_t kDecMaxWaves = 16;            // waves per workgroup (one table copy each)
 constexpr uint32_t kRingPad = 64;               // ring words 0..63 mirrored after the ring end
 constexpr uint32_t kListDump = 512;            // list slot written by masked-off lanes
-constexpr uint32_t kListWords = kListDump + 16;  // terminator positions of one sub-block (bs <= 512), dump pairs
+constexpr uint32_t kListWords = kListDump + 24;  // terminator positions of one sub-block (bs <= 512), dump pairs (MT <= 12)
 constexpr uint32_t kWaveLdsWords = kRingWords + kRingPad + kListWords;
 constexpr uint32_t kTabBytes = kMapEntries * 16;
 
@@ -1549,6 +1549,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
           tpk = r < 4 ? tpk : tpk1;
         }
+        if constexpr (MT > 8) {
+          const uint32_t tpk2 = t[8] | (t[9] << 8) | ((t[10] | (t[11] << 8)) << 16);
+          tpk = r < 8 ? tpk : tpk2;
+        }
         const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
         // (bit 63 set: a defined lane when no lane ends the sub-block; Pe is
         // then unused)
@@ -1731,14 +1735,18 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       const uint32_t* w = ring + ((P >> 5) & kRingMask);
       const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
       const uint32_t s0 = s;
+      // (fs 1: the fs 1-4 instance, 12 terminators per segment; a stream
+      // that mixes fs 1 and 2..4 sub-blocks stays in it)
       if (bs == 2 * kWave) {
         if (h - 6u <= 2u) fast.template operator()<4, 5, 7, true>();
         else if (h - 3u <= 2u) fast.template operator()<8, 2, 4, true>();
         else if (h - 9u <= 5u) fast.template operator()<4, 8, 13, true>();
+        else if (h == 2u) fast.template operator()<12, 1, 4, true>();
       } else {
         if (h - 6u <= 2u) fast.template operator()<4, 5, 7, false>();
         else if (h - 3u <= 2u) fast.template operator()<8, 2, 4, false>();
         else if (h - 9u <= 5u) fast.template operator()<4, 8, 13, false>();
+        else if (h == 2u) fast.template operator()<12, 1, 4, false>();
       }
       last0 &= 0xFFFFu;
       last1 &= 0xFFFFu;
@@ -2475,6 +2483,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
               const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
               tpk = r < 4 ? tpk : tpk1;
             }
+            if constexpr (MT > 8) {
+              const uint32_t tpk2 = t[8] | (t[9] << 8) | ((t[10] | (t[11] << 8)) << 16);
+              tpk = r < 8 ? tpk : tpk2;
+            }
             const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
             const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
             Pe = q + SB * lz + readlane(tend, (int)lz) + k;
@@ -2535,6 +2547,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
           if (h - 6u <= 2u) fast.template operator()<4, 5, 7>();
           else if (h - 3u <= 2u) fast.template operator()<8, 2, 4>();
           else if (h - 9u <= 5u) fast.template operator()<4, 8, 13>();
+          else if (h == 2u) fast.template operator()<12, 1, 4>();
           if (s == s0) break;  // the general path takes this sub-block
         }
         if (s >= nsb || status != RPP_OK || stop) break;

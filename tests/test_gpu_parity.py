@@ -125,6 +125,27 @@ def test_high_rice_parameters(bs, cs, ulsb):
             run_batch(cfg, blocks)
 
 
+@pytest.mark.parametrize("bs", [16, 32, 64, 128])
+@pytest.mark.parametrize("cs", [1, 2])
+def test_low_bit_depth_fs1_fs2_mix(bs, cs):
+    """configs[4]'s 10/12-bit rows: Poisson(4) samples put ~30 % of the sub-blocks at fs 1 and
+    the rest at fs 2 (the fs 1-4 loop, 12 terminators per segment, with switches to and from
+    the fs 2-4 loop), plus fs 0 runs (the general path) between them; fused and segmented."""
+    rng = np.random.default_rng(31 + bs + cs)
+    cases = []
+    for ulsb in (6, 4):
+        v = np.clip(rng.poisson(4.0, bs * cs * 300), 0, 0xFFFF >> ulsb).astype(np.uint64) << ulsb
+        cases.append((ulsb, [datagen.store(v, ulsb, True)]))
+    runs = [datagen.poisson_data(rng, bs * cs, lam=float(rng.choice([0.2, 1.0, 4.0, 12.0, 40.0])))
+            for _ in range(200)]
+    cases.append((0, [np.concatenate(runs)]))
+    for ulsb, blocks in cases:
+        cfg = codec.CodecConfig(bs, cs, "big", ulsb)
+        run_batch(cfg, blocks)
+        with _decode_mode("segmented", 12):
+            run_batch(cfg, blocks)
+
+
 @pytest.mark.parametrize("ulsb", list(range(0, 16)))
 def test_unused_lsb_sweep(ulsb):
     rng = np.random.default_rng(ulsb)
