@@ -1985,6 +1985,33 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
+// The end (next header) of the sub-block with its header at bit r of the
+// staged words st (relative positions), parsed by the whole wave: one 2048-bit
+// window of 32-bit lane segments with exact entry states (w32_count, byte maps
+// for any fs), kSegNone when its codes do not end in that window (a guess
+// candidate is then dropped: a missed guess costs time, never a result).
+__device__ __forceinline__ uint32_t seg_sb_end_wave(const uint32_t* st, const uint4* tab, uint32_t r, uint32_t bs,
+                                                    uint32_t lane, ScanRegs& sreg) {
+  const uint32_t* w = st + (r >> 5) + lane;
+  const uint32_t x = __builtin_amdgcn_alignbit(w[1], w[0], r & 31u);
+  const uint32_t v = __builtin_amdgcn_readfirstlane(x) & 15u;
+  if (v == 0) return r + 4u;
+  if (v == 15) return r + 4u + 16u * bs;
+  const uint32_t fs = v - 1u;
+  const uint4* tb = tab + 256u * fs;
+  const uint4 e0 = tb[x & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(x, 8, 8)], e2 = tb[__builtin_amdgcn_ubfe(x, 16, 8)],
+              e3 = tb[x >> 24];
+  uint32_t tm, cnt, incl, unused;
+  uint64_t finm;
+  w32_count(e0, e1, e2, e3, bs, 0u, sreg, tm, cnt, incl, finm, unused);
+  if (finm == 0) return rpp_internal::kSegNone;
+  const uint32_t lz = (uint32_t)__builtin_ctzll(finm);
+  uint32_t t = readlane(tm, (int)lz);
+  const uint32_t rr = bs - 1u - (readlane(incl, (int)lz) - readlane(cnt, (int)lz));
+  for (uint32_t i = 0; i < rr; ++i) t &= t - 1u;  // (scalar: the rr-th terminator of lane lz)
+  return r + 32u * lz + (uint32_t)__builtin_ctz(t) + v;
+}
+
 // Segmented decode, the first header of a unit (ricepp_internal.h): the
 // first candidate bit c in [c_first, 4 + 16 bs) of the staged words `st`
 // whose chain of kSpecSteps sub-blocks (each parsed exactly as
@@ -2005,8 +2032,9 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // chains per lane and three codes per read, 256 candidates at a time; after
 // every sub-block the survivors are compacted into `list` (512 words of LDS).
 // A wrong guess costs time, never a wrong result.
+constexpr uint32_t kGuessWaveMax = 12;  // survivors below which seg_guess parses wave-parallel
 __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_rel, uint32_t bs,
-                                              uint32_t lane, uint32_t c_first, uint32_t range) {
+                                              uint32_t lane, uint32_t c_first, uint32_t range, const uint4* tab) {
   using rpp_internal::kSegNone;
   using rpp_internal::kSpecSteps;
   constexpr uint32_t kSlots = 4;
@@ -2106,6 +2134,37 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
       }
       lds_fence();
       if (cnt == 0) break;
+      // few survivors: the remaining steps survivor by survivor (candidate
+      // order) with the wave-parallel parse, ~1/20 of a lane-serial step each
+      if (cnt <= kGuessWaveMax && step + 1 < kSpecSteps) {
+        ScanRegs sreg;
+        for (uint32_t idx = 0; idx < cnt; ++idx) {
+          uint32_t cur = __builtin_amdgcn_readfirstlane(list[2 * idx]);
+          const uint32_t o = __builtin_amdgcn_readfirstlane(list[2 * idx + 1]);
+          uint32_t lo = (o >> 16) & 15u, hi = (o >> 20) & 15u;
+          bool ok = true;
+          for (uint32_t st2 = step + 1; st2 < kSpecSteps && ok; ++st2) {
+            const uint32_t* w = st + (cur >> 5);
+            const uint32_t v = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], cur & 31u)) & 15u;
+            lo = min(lo, v);
+            hi = max(hi, v);
+            const uint32_t nc = seg_sb_end_wave(st, tab, cur, bs, lane, sreg);
+            ok = hi - lo <= range && (lo != 0 || hi == 0) && nc != rpp_internal::kSegNone && nc + 4 <= end_rel;
+            cur = nc;
+          }
+          if (ok) {
+            if (lane == 0) {
+              atomicAdd(&g_parse_diag[4], (unsigned long long)n_chunks);
+              atomicAdd(&g_parse_diag[5], (unsigned long long)n_steps);
+              atomicAdd(&g_parse_diag[6], (unsigned long long)n_slotsteps);
+            }
+            return o & 0xFFFFu;
+          }
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kSlots; ++i) alive[i] = false;  // (none survived)
+        break;
+      }
       nslots = (cnt + kWave - 1) / kWave;
 #pragma unroll
       for (uint32_t i = 0; i < kSlots; ++i) {
@@ -2234,12 +2293,12 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       for (uint32_t i = lane; i < kStW; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
       lds_fence();
       const uint64_t tg = memtime();
-      uint32_t g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, c_first, 3);
+      uint32_t g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, c_first, 3, tab);
     // none: the true chain's headers may span a wider range for a few
     // sub-blocks; a second search with range 5 (its candidates are checked
     // by the parse as any other)
     if (g == kSegNone && c_first == 0)
-      g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, 0, 5);
+      g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, 0, 5, tab);
       if (lane == 0) atomicAdd(&g_parse_diag[0], (unsigned long long)(memtime() - tg));
       lds_fence();  // (the ring is refilled next)
       return g == kSegNone ? kSegNone : S + g;
