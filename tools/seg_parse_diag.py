@@ -1,4 +1,4 @@
-"""Where the segmented parse spends its time: s_memtime cycles (100 MHz) in the guess and in the unit
+"""Where the segmented parse spends its time: s_memtime cycles (shader clock) in the guess and in the unit
 chains, sub-blocks parsed, units -- for one 16 MiB Poisson stream and the block mix.
 
 usage: python tools/seg_parse_diag.py"""
@@ -37,9 +37,10 @@ def run(name, blocks):
     torch.cuda.synchronize()
     N.lib().rpp_parse_diag_read(buf, 1)
     g, ch, sb, un, nch, nst, nsl, reg = map(int, buf)
+    # (s_memtime counts shader-clock cycles on gfx950)
     print(f"{name}: {ev[0].elapsed_time(ev[1]):.3f} ms, units {un}, sub-blocks {sb}, "
-          f"guess {g / max(un, 1) / 100:.1f} us/unit, chain {ch / max(un, 1) / 100:.1f} us/unit = "
-          f"{ch / max(sb, 1) * 10:.0f} ns/sub-block; per guess {nch / max(un, 1):.2f} chunks {nst / max(un, 1):.1f} steps "
+          f"guess {g / max(un, 1) / 1e3:.0f} K cycles/unit, chain {ch / max(un, 1) / 1e3:.0f} K cycles/unit = "
+          f"{ch / max(sb, 1):.0f} cycles/sub-block; per guess {nch / max(un, 1):.2f} chunks {nst / max(un, 1):.1f} steps "
           f"{nsl / max(un, 1):.1f} slot-steps, re-guesses {reg}, exact {torch.equal(out[:sum(ns)], x)}, "
           f"{codec.segmented_decode_stats()}", flush=True)
 
