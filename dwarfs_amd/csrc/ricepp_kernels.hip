@@ -187,7 +187,13 @@ struct EncParams {
 // segment starts from the real preceding sample, at bit 0 of its own scratch
 // slot (segment 0: after the initial values, in the stream's output), and
 // rpp_enc_concat_kernel then places each segment at its bit offset.
-constexpr uint32_t kEncSegChunks = 256;
+#ifndef RPP_ENC_SEG_CHUNKS
+#define RPP_ENC_SEG_CHUNKS 256
+#endif
+constexpr uint32_t kEncSegChunks = RPP_ENC_SEG_CHUNKS;
+#ifndef RPP_EPRIO
+#define RPP_EPRIO 1  // wave priority in the pipelined encode (1: plans over emission, 2: the reverse, 0: off)
+#endif
 
 // Compile-time shape of an encode launch: SPL samples per lane (8 or 16), a
 // ricepp sub-block owned by an aligned group of G lanes (G = next pow2 of
@@ -636,13 +642,29 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
     auto step = [&](EncPlan<SPL>& E, EncPlan<SPL>& F, EncRaw<SPL>& rn, EncGeom& gn) {
       RPP_STAT(0, 1);
       RPP_TSTAMP(1);
+#if RPP_EPRIO == 1
+      __builtin_amdgcn_s_setprio(1);
+#endif
       enc_plan_a<SPL, G, CS, SH>(F, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
       gn = enc_geom<SPL, CS>(s_lo + (it + 3) * spw + g, j, nsb, N, bs);
       rn = enc_load_vec<SPL, CS>(in, gn, !dpp_prev);
       RPP_TSTAMP(2);
+#if RPP_EPRIO == 1
+      __builtin_amdgcn_s_setprio(0);
+#elif RPP_EPRIO == 2
+      __builtin_amdgcn_s_setprio(1);
+#endif
       enc_emit<SPL>(E, st, j, empty_lanes);
+#if RPP_EPRIO == 1
+      __builtin_amdgcn_s_setprio(1);
+#elif RPP_EPRIO == 2
+      __builtin_amdgcn_s_setprio(0);
+#endif
       RPP_TSTAMP(3);
       enc_plan_b<SPL, G>(F, st, j);
+#if RPP_EPRIO == 1
+      __builtin_amdgcn_s_setprio(0);
+#endif
       RPP_TSTAMP(4);
       enc_flush(st, false);
       RPP_TSTAMP(5);
@@ -1053,6 +1075,12 @@ __device__ __forceinline__ uint32_t jshift(uint32_t x, uint32_t& keep) {
 // the last round still changed E.  If no lane up to l changed, E is exact up
 // to lane l (induction from lane 0), so the caller needs the map scan only
 // when an unsettled lane lies before the sub-block's end (rare).
+#ifndef RPP_PRIO
+#define RPP_PRIO 1  // wave priority over the fast loop's parse chain (0: off)
+#endif
+#ifndef RPP_PRIO_TOP
+#define RPP_PRIO_TOP 0
+#endif
 #ifndef RPP_JACOBI
 #define RPP_JACOBI 0  // measured: rounds 4 / 6 / 8 = 286 / 267 / 265 us vs 262 us with the scan (bench decode)
 #endif
@@ -1466,6 +1494,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // halves), so that sub-block's value prefix costs no scan of its own.
       auto parse = [&](uint32_t q, uint32_t xl, uint32_t xh, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint4 e3,
                        uint32_t& Pe, uint32_t rider, uint32_t& rider_incl, auto&& mid) -> bool {
+#if RPP_PRIO
+        __builtin_amdgcn_s_setprio(RPP_PRIO);
+#endif
         const uint32_t k = fs + 1;
         uint32_t tm, cnt, incl;
         uint64_t finm;
@@ -1558,6 +1589,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // then unused)
         const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
         Pe = q + SB * lz + readlane(tend, (int)lz) + k;
+#if RPP_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         RPP_TSTAMP(8);
         // pair excl + j for j = MT-1 .. 0, one instruction each (kept apart:
         // a merged ds_write2 would put two j in one instruction): a slot past
@@ -1680,6 +1714,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           tt = make_uint4(t2.x, t2.y, 0u, 0u);
         }
         uint32_t xhB;
+#if RPP_PRIO && RPP_PRIO_TOP
+        __builtin_amdgcn_s_setprio(RPP_PRIO);  // (the chain: ring read, lookups, parse)
+#endif
         const uint32_t xlB = seg_bits(Pn, xhB);
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
         RPP_TSTAMP(1);
