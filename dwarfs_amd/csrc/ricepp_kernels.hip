@@ -1079,7 +1079,10 @@ __device__ __forceinline__ uint32_t jshift(uint32_t x, uint32_t& keep) {
 #define RPP_PRIO 1  // wave priority over the fast loop's parse chain (0: off)
 #endif
 #ifndef RPP_PRIO_TOP
-#define RPP_PRIO_TOP 0
+#define RPP_PRIO_TOP 0  // diagnostics: raise it from the ring read before the parse
+#endif
+#ifndef RPP_PRIO_MID
+#define RPP_PRIO_MID 0  // diagnostics: drop it for the previous sub-block's stores inside the parse
 #endif
 #ifndef RPP_JACOBI
 #define RPP_JACOBI 0  // measured: rounds 4 / 6 / 8 = 286 / 267 / 265 us vs 262 us with the scan (bench decode)
@@ -1544,7 +1547,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           rider_incl = incl2 >> 16;
           // (the previous sub-block's stores, issued before the settle
           // branch so that they overlap this parse)
+#if RPP_PRIO && RPP_PRIO_MID
+          __builtin_amdgcn_s_setprio(0);
+#endif
           mid(rider_incl);
+#if RPP_PRIO && RPP_PRIO_MID
+          __builtin_amdgcn_s_setprio(RPP_PRIO);
+#endif
           finm = __ballot(incl >= n);
 #if RPP_JACOBI > 0
           if (unsettled & upto_end(finm)) {
