@@ -1,13 +1,19 @@
 #!/usr/bin/env python3
-"""ricepp encode+decode benchmark on MI355X (BASELINE.json configs[1]).
+"""ricepp encode+decode benchmark on MI355X.
 
+Workloads (BASELINE.json):
+  blocks (default, configs[1]): 4096 independent 64 KiB uint16 blocks per GPU
+      (weak scaling: every rank holds its own 4096 blocks);
+  mix (configs[3]): one fixed mkdwarfs-style mix of 1 / 4 / 16 MiB blocks,
+      32 GiB in all, sharded by block across the ranks with
+      parallel.partition_blocks (strong scaling: the total is fixed).
 One step = encode every block of the shard on the GPU, all-gather the
-per-block encoded sizes over RCCL (N > 1), decode every block back.  Inputs
-are resident in HBM before the timed region; `value` is uncompressed bytes
-of all ranks per second (GiB/s), the accounting of
-ricepp/ricepp_benchmark.cpp:145-146,155-156 applied to the round trip.
+per-block encoded sizes over RCCL (N > 1) and scan them into image offsets,
+decode every block back.  Inputs are resident in HBM before the timed region;
+`value` is uncompressed bytes of all ranks per second (GiB/s), the accounting
+of ricepp/ricepp_benchmark.cpp:145-146,155-156 applied to the round trip.
 
-Launch:  python bench.py [--gpus N --steps K --warmup W]
+Launch:  python bench.py [--gpus N --steps K --warmup W] [--workload mix]
          (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 """
 
@@ -45,6 +51,39 @@ def make_poisson_blocks(nblocks: int, n: int, lam: float, seed: int, device) -> 
         v = ((v & 0xFF) << 8) | ((v >> 8) & 0xFF)
         out[s:e] = v.to(torch.int16)  # wraps to the same 16 bits
     return out
+
+
+def mix_block_mib(total_gib: int = 32, seed: int = 2024) -> list:
+    """configs[3]'s block list: mkdwarfs cuts each category into blocks of the block size (16 MiB at its
+    default -S 24) with a short last block per category, so the mix is mostly 16 MiB blocks with 4 and
+    1 MiB ones in between: 3/4 of the bytes in 16 MiB blocks, 3/16 in 4 MiB, 1/16 in 1 MiB, shuffled
+    (seeded: every rank derives the same list)."""
+    total_mib = total_gib * 1024
+    n16, n4, n1 = total_mib * 3 // 4 // 16, total_mib * 3 // 16 // 4, total_mib // 16
+    sizes = np.array([16] * n16 + [4] * n4 + [1] * n1, np.int64)
+    np.random.default_rng(seed).shuffle(sizes)
+    return sizes.tolist()
+
+
+def make_mix_shard(block_mib: list, lo: int, hi: int, device) -> tuple:
+    """This rank's blocks [lo, hi) of the mix, generated on the GPU: block i is Poisson(lambda_i) noise
+    (lambda from {300, 1000, 3000} by block), stored big endian, from a generator seeded by the block index
+    alone, so the data do not depend on the rank count."""
+    n = [m << 19 for m in block_mib[lo:hi]]  # samples per block
+    offs = np.zeros(len(n), np.int64)
+    if n:
+        offs[1:] = np.cumsum(n)[:-1]
+    x = torch.empty(max(int(sum(n)), 8), dtype=torch.int16, device=device)
+    g = torch.Generator(device=device)
+    for j, i in enumerate(range(lo, hi)):
+        g.manual_seed(7919 * i + 1)
+        lam = (300.0, 1000.0, 3000.0)[i % 3]
+        for s0 in range(0, n[j], 1 << 24):
+            e0 = min(n[j], s0 + (1 << 24))
+            v = torch.poisson(torch.full((e0 - s0,), lam, device=device), generator=g).clamp_(0, 65535).to(torch.int32)
+            v = ((v & 0xFF) << 8) | ((v >> 8) & 0xFF)
+            x[offs[j] + s0:offs[j] + e0] = v.to(torch.int16)
+    return x, offs, np.asarray(n, np.int64)
 
 
 def device_copy_gbps(dev, nbytes: int = 1 << 30, iters: int = 10) -> float:
@@ -167,6 +206,9 @@ def main() -> None:
     ap.add_argument("--block-bytes", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", choices=("blocks", "mix"), default="blocks",
+                    help="blocks: configs[1] (default, weak scaling); mix: configs[3] (strong scaling)")
+    ap.add_argument("--mix-gib", type=int, default=32, help="total size of the configs[3] mix")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,10 +220,20 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=dev)
 
     cfg = codec.CodecConfig(block_size=128, component_stream_count=1, byteorder="big", unused_lsb_count=0)
-    nblocks, n = args.blocks, args.block_bytes // 2
-    x = make_poisson_blocks(nblocks, n, 1000.0, 42 + rank, dev)
-    in_offsets = np.arange(nblocks, dtype=np.int64) * n
-    pipe = parallel.ShardPipeline(cfg, x, in_offsets, np.full(nblocks, n, np.int64), group=dist.group.WORLD if world > 1 else None)
+    group = dist.group.WORLD if world > 1 else None
+    if args.workload == "mix":
+        mix = mix_block_mib(args.mix_gib)
+        lo, hi = parallel.partition_blocks([m << 20 for m in mix], world)[rank]
+        x, in_offsets, ns = make_mix_shard(mix, lo, hi, dev)
+        nblocks, n = hi - lo, 0
+        pipe = parallel.ShardPipeline(cfg, x, in_offsets, ns, group=group)
+        shard_bytes = int(ns.sum()) * 2
+    else:
+        nblocks, n = args.blocks, args.block_bytes // 2
+        x = make_poisson_blocks(nblocks, n, 1000.0, 42 + rank, dev)
+        in_offsets = np.arange(nblocks, dtype=np.int64) * n
+        pipe = parallel.ShardPipeline(cfg, x, in_offsets, np.full(nblocks, n, np.int64), group=group)
+        shard_bytes = nblocks * n * 2
 
     # correctness gate before timing: round trip must be exact
     pipe.step()
@@ -210,12 +262,62 @@ def main() -> None:
     # per-kernel timing with events on the launch stream (torch's current stream)
     k_enc, k_dec = pipe.kernel_times(iters=max(5, args.steps))
     comp_bytes = int(pipe.enc.sizes.sum().item())
-    raw_bytes = nblocks * n * 2
+    raw_bytes = shard_bytes
     enc_bytes = raw_bytes + comp_bytes + 8 * nblocks
     dec_bytes = comp_bytes + raw_bytes
     dominant = "decode" if k_dec >= k_enc else "encode"
     kt, kb = (k_dec, dec_bytes) if dominant == "decode" else (k_enc, enc_bytes)
     achieved = kb / kt / 1e9
+
+    if args.workload == "mix":
+        t = torch.tensor([raw_bytes, comp_bytes], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t)
+        total_raw, total_comp = float(t[0].item()), float(t[1].item())
+        value = total_raw * args.steps / elapsed / 2**30
+        result = {
+            "metric": "ricepp encode+decode GiB/s, device-resident uint16 blocks, 1/2/4/8 GPUs",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic Poisson(300/1000/3000) sensor samples per block, stored big endian, generated on device",
+            "config": {
+                "workload": f"mkdwarfs-style mix of 1/4/16 MiB uint16 blocks, {args.mix_gib} GiB in all, sharded by "
+                            "block across the ranks (BASELINE.json configs[3]), ricepp bs128 cs1 BE ulsb0, "
+                            "encode+decode round trip",
+                "blocks_total": len(mix),
+                "blocks_rank0": nblocks,
+                "bytes_total": int(total_raw),
+                "compression_ratio": round(total_comp / total_raw, 5),
+                "parallelism": f"shard{world} (byte-balanced contiguous block ranges, RCCL all-gather of encoded sizes)",
+                "rank0_encode_ms": round(k_enc * 1e3, 3),
+                "rank0_decode_ms": round(k_dec * 1e3, 3),
+                "rank0_encode_GiBps": round(raw_bytes / k_enc / 2**30, 2),
+                "rank0_decode_GiBps": round(raw_bytes / k_dec / 2**30, 2),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "rpp_decode_batch_ws (segmented: unit parse + extraction + fused short streams)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "traffic_source": "not profiled for the mix",
+            },
+        }
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     traffic, traffic_src = profiled_traffic(f"rpp_{dominant}_kernel")
 

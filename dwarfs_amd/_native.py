@@ -20,6 +20,14 @@ RPP_TRUNCATED_INPUT = -2
 RPP_INVALID_ARGUMENT = -3
 RPP_OUTPUT_TOO_SMALL = -4
 RPP_HIP_ERROR = -5
+RPP_INTERNAL_ERROR = -6
+
+RPP_DECODE_AUTO = 0
+RPP_DECODE_FUSED = 1
+RPP_DECODE_SEGMENTED = 2
+RPP_TEST_NO_FAST_LANES = 1
+RPP_TEST_LOOKBACK_STALL = 2
+RPP_TEST_PHASE_TIMERS = 4
 
 STATUS_NAMES = {
     RPP_OK: "OK",
@@ -28,6 +36,7 @@ STATUS_NAMES = {
     RPP_INVALID_ARGUMENT: "INVALID_ARGUMENT",
     RPP_OUTPUT_TOO_SMALL: "OUTPUT_TOO_SMALL",
     RPP_HIP_ERROR: "HIP_ERROR",
+    RPP_INTERNAL_ERROR: "INTERNAL_ERROR",
 }
 
 # Every symbol declared in include/ricepp_amd.h.
@@ -41,6 +50,8 @@ EXPORTED_SYMBOLS = (
     "rpp_decode_batch",
     "rpp_decode_workspace_bytes",
     "rpp_decode_batch_ws",
+    "rpp_decode_workspace_bytes_ex",
+    "rpp_decode_batch_ex",
     "rpp_unused_lsb_batch",
     "rpp_exclusive_scan_u64",
     "rpp_pack_batch",
@@ -60,6 +71,17 @@ class RppConfig(C.Structure):
         ("component_stream_count", C.c_uint32),
         ("big_endian", C.c_uint32),
         ("unused_lsb_count", C.c_uint32),
+    ]
+
+
+class RppDecodeOptions(C.Structure):
+    """``rpp_decode_options`` (explicit decode path selection, tests and diagnostics)."""
+
+    _fields_ = [
+        ("path", C.c_uint32),
+        ("seg_log2", C.c_uint32),
+        ("fused_waves", C.c_uint32),
+        ("test_flags", C.c_uint32),
     ]
 
 
@@ -120,6 +142,12 @@ def lib() -> C.CDLL:
         L.rpp_decode_batch_ws.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, C.c_uint64,
                                           C.c_uint64, P, C.c_uint64, P]
         L.rpp_decode_batch_ws.restype = C.c_int
+        L.rpp_decode_workspace_bytes_ex.argtypes = [C.POINTER(RppConfig), C.c_uint64, C.c_uint64, C.c_uint32,
+                                                    C.POINTER(RppDecodeOptions)]
+        L.rpp_decode_workspace_bytes_ex.restype = C.c_uint64
+        L.rpp_decode_batch_ex.argtypes = [C.POINTER(RppConfig), P, P, P, C.c_uint32, P, P, P, P, C.c_uint64,
+                                          C.c_uint64, P, C.c_uint64, C.POINTER(RppDecodeOptions), P]
+        L.rpp_decode_batch_ex.restype = C.c_int
         L.rpp_unused_lsb_batch.argtypes = [P, P, P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P]
         L.rpp_unused_lsb_batch.restype = C.c_int
         L.rpp_exclusive_scan_u64.argtypes = [P, C.c_uint64, P, P]

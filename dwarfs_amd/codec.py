@@ -40,6 +40,7 @@ __all__ = [
     "worst_case_encoded_bytes",
     "encode_batch",
     "decode_batch",
+    "DecodeOptions",
 ]
 
 
@@ -203,6 +204,25 @@ def encode_workspace(config: CodecConfig, total_samples: int, max_stream_samples
     return ws
 
 
+_PATHS = {"auto": N.RPP_DECODE_AUTO, "fused": N.RPP_DECODE_FUSED, "segmented": N.RPP_DECODE_SEGMENTED}
+
+
+@dataclass(frozen=True)
+class DecodeOptions:
+    """``rpp_decode_options``: explicit decode path selection (tests, diagnostics, tuning).  The default is
+    exactly ``rpp_decode_batch_ws``: segmented when the batch has long streams, else one wave per stream."""
+
+    path: str = "auto"        # "auto", "fused" (one wave per stream) or "segmented" (split every long stream)
+    seg_log2: int = 0         # units of 2**seg_log2 bits (10..26); 0: chosen from the batch
+    fused_waves: int = 0      # streams per workgroup of the fused kernel (1..16); 0: auto
+    test_flags: int = 0       # RPP_TEST_* fault injection / diagnostics
+
+    def native(self) -> N.RppDecodeOptions:
+        if self.path not in _PATHS:
+            raise ValueError(f"decode path must be one of {sorted(_PATHS)}, not {self.path!r}")
+        return N.RppDecodeOptions(_PATHS[self.path], int(self.seg_log2), int(self.fused_waves), int(self.test_flags))
+
+
 def decode_batch(
     config: CodecConfig,
     data: torch.Tensor,
@@ -212,6 +232,7 @@ def decode_batch(
     stream: Optional[torch.cuda.Stream] = None,
     out: Optional[torch.Tensor] = None,
     out_offsets: Optional[Sequence[int]] = None,
+    options: Optional[DecodeOptions] = None,
 ):
     """Decodes independent blocks of a device-resident encoded buffer.
 
@@ -238,14 +259,15 @@ def decode_batch(
     status = torch.empty(nb, dtype=torch.int32, device=dev)
     total = int(n_samples.sum()) if nb else 0
     longest = int(n_samples.max()) if nb else 0
-    ws = decode_workspace(config, total, nb, dev, longest)
+    ws = decode_workspace(config, total, nb, dev, longest, options)
     if stream is not None:
         ws.record_stream(stream)
-    st = N.lib().rpp_decode_batch_ws(
+    o = (options or DecodeOptions()).native()
+    st = N.lib().rpp_decode_batch_ex(
         C.byref(c), C.c_void_p(data.data_ptr()), C.c_void_p(d_in_off.data_ptr()),
         C.c_void_p(d_in_bytes.data_ptr()), nb, C.c_void_p(out.data_ptr()), C.c_void_p(d_out_off.data_ptr()),
         C.c_void_p(d_n.data_ptr()), C.c_void_p(status.data_ptr()), total, longest, C.c_void_p(ws.data_ptr()),
-        ws.numel(), _stream_ptr(stream))
+        ws.numel(), C.byref(o), _stream_ptr(stream))
     _raise_status(st)
     return out, status
 
@@ -260,13 +282,14 @@ def segmented_decode_stats(reset: bool = True) -> dict:
 
 
 def decode_workspace(config: CodecConfig, total_samples: int, nblocks: int, device,
-                     max_stream_samples: Optional[int] = None) -> torch.Tensor:
+                     max_stream_samples: Optional[int] = None, options: Optional[DecodeOptions] = None) -> torch.Tensor:
     """Device workspace of ``rpp_decode_batch_ws`` for a batch of ``nblocks`` streams of ``total_samples``
     samples, the longest ``max_stream_samples`` (default: ``total_samples``, i.e. sized for the segmented
     decode of long streams whenever the batch could need it)."""
     c = _check(config)
     mx = int(total_samples if max_stream_samples is None else max_stream_samples)
-    nbytes = int(N.lib().rpp_decode_workspace_bytes(C.byref(c), int(total_samples), mx, int(nblocks)))
+    o = (options or DecodeOptions()).native()
+    nbytes = int(N.lib().rpp_decode_workspace_bytes_ex(C.byref(c), int(total_samples), mx, int(nblocks), C.byref(o)))
     return torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
 
 

@@ -79,6 +79,7 @@ struct Workspace {
   uint32_t* queue;      // [1]
   uint64_t* cnt2;       // [U_max + 1] exact positions per unit
   uint64_t* off2;       // [U_max + 1]
+  uint32_t* guard;      // [1] 1: the batch exceeds the promised sizes (rpp_dec_guard_kernel)
   uint64_t bytes;
   uint64_t max_tiles;
   uint64_t units_max;
@@ -123,6 +124,7 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint64_t max_str
   w.lvl_base = reinterpret_cast<uint64_t*>(take(((uint64_t)w.levels + 1) * 8));
   w.sb_pos = reinterpret_cast<uint32_t*>(take((max_sb + B) * 4));
   w.counter = reinterpret_cast<uint32_t*>(take(256));
+  w.guard = reinterpret_cast<uint32_t*>(take(256));
   w.max_tiles = max_tiles;
   if (L) {
     // header bits of all streams: at most their worst-case sizes (seg_last_bit)
@@ -156,24 +158,16 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint64_t max_str
 // (units: the segmented decode's units per stream; streams of one unit are
 // the fused kernel's and get no entries)
 __global__ void rpp_dec_count_kernel(const uint64_t* n_samples, uint32_t nblocks, uint32_t chunk_len, uint32_t cs,
-                                     uint64_t* sb_cnt, uint64_t* tile_cnt, const uint64_t* units) {
+                                     uint64_t* sb_cnt, uint64_t* tile_cnt, const uint64_t* units, const uint32_t* guard) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nblocks) return;
   uint64_t nsb = 0;
-  if (i < nblocks) {
+  if (i < nblocks && !*guard) {
     const uint64_t n = n_samples[i];
     if (n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES && (!units || units[i] > 1)) nsb = (n + chunk_len - 1) / chunk_len * cs;
   }
   sb_cnt[i] = i < nblocks ? nsb + 1 : 0;
   tile_cnt[i] = (nsb + kTile - 1) / kTile;
-}
-
-// The caller's max_stream_samples bounds the tile levels: a stream longer
-// than it breaks the contract and is reported, not decoded.
-__global__ void rpp_dec_check_max_kernel(const uint64_t* n_samples, uint32_t nblocks, uint64_t max_stream_samples,
-                                         int32_t* status) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nblocks && n_samples[i] > max_stream_samples) status[i] = RPP_INVALID_ARGUMENT;
 }
 
 // Tiles are handed out level by level: tile l of every stream before tile
@@ -241,7 +235,7 @@ struct ExtractParams {
   const uint64_t* n_samples;
   uint16_t* out;
   const uint64_t* out_off;
-  const int32_t* status;  // of the parse pass: streams that failed are skipped
+  int32_t* status;        // of the parse pass: streams that failed are skipped; RPP_INTERNAL_ERROR on a stalled look-back
   const uint32_t* sb_pos;
   const uint64_t* sb_base;
   const uint64_t* tile_base;
@@ -252,7 +246,7 @@ struct ExtractParams {
   uint32_t* counter;
   uint32_t nblocks;
   uint32_t bs, be, ulsb;
-  uint32_t dbg;  // diagnostics (RICEPP_DEC2_DBG): 1 no fast lanes, 2 fast lanes store sample by sample
+  uint32_t dbg;  // rpp_decode_options::test_flags (RPP_TEST_*)
 };
 
 // pixel traits (ricepp/ricepp_cpuspecific_traits.h:63-75)
@@ -395,7 +389,11 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
   const uint32_t chunk_len = CS * BS;
   const uint64_t total_tiles = *p.n_tiles;
 
-  const bool timing = (p.dbg & 4) && tid < 64;
+  const bool timing = (p.dbg & RPP_TEST_PHASE_TIMERS) && tid < 64;
+  // fault injection: tile 1 of every stream never publishes, its successors
+  // give up after 2^10 polls instead of 2^22
+  const bool stall = p.dbg & RPP_TEST_LOOKBACK_STALL;
+  const uint32_t spin_max = stall ? (1u << 10) : (1u << 22);
   uint64_t tp = timing ? clk() : 0;
   auto stamp = [&](int i) {
     if (timing) {
@@ -463,7 +461,8 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
     // ---- fast lanes: Rice, a full sub-block, staged, every code <= 32 bits ----
     uint32_t hdr = 0;
     if (active) hdr = rd.peek32(start) & 15u;
-    bool fast = active && hdr != 0 && hdr != 15 && n == BS && (end >> 5) + 1 < w0 + nst && !(p.dbg & 1);
+    bool fast = active && hdr != 0 && hdr != 15 && n == BS && (end >> 5) + 1 < w0 + nst &&
+                !(p.dbg & RPP_TEST_NO_FAST_LANES);
     // pairs share one store path (the shuffle outside any condition: a
     // short-circuit && would run it on the fast lanes only)
     if (CS == 2) {
@@ -536,7 +535,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
         e0 = kSet | (uint32_t)(x & 0xFFFFu);
         e1 = kSet | (uint32_t)((x >> 16) & 0xFFFFu);
       } else {
-        if (tid == 0)
+        if (tid == 0 && !(stall && lt == 1))
           __hip_atomic_store(&p.tile_state[t], pack_state(a0, a1, kFlagAgg), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         uint32_t x0 = 0, x1 = 0;  // identity: the tiles after the current window
@@ -547,12 +546,16 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
           if (valid) {
             // (relaxed: the state word carries its payload, no other data is
             // published with it; the load is coherent at agent scope (sc1).
-            // Bounded: a tile that never publishes is a bug, reported in
-            // g_dec2_diag[6], not a hung GPU.)
+            // Bounded: a predecessor that never publishes is a bug or a
+            // stalled GPU.  The stream is then marked RPP_INTERNAL_ERROR --
+            // before anything is built on the missing prefix -- and the tile
+            // goes on with an identity prefix only so that the grid drains.)
             for (uint32_t spin = 0;; ++spin) {
               s = __hip_atomic_load(&p.tile_state[jt - tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               if (s >> 62) break;
-              if (spin == (1u << 22)) {
+              if (spin == spin_max) {
+                __hip_atomic_store(&p.status[b], (int32_t)RPP_INTERNAL_ERROR, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
                 atomicAdd(&g_dec2_diag[6], 1ull);
                 s = kFlagIncl;
                 break;
@@ -577,9 +580,11 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
         e0 = x0;
         e1 = x1;
       }
-      if (tid == 0) {
+      if (tid == 0 && !(stall && lt == 1)) {
         __hip_atomic_store(&p.tile_state[t], pack_state(combine(e0, a0), combine(e1, a1), kFlagIncl),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (tid == 0) {
         sh_carry[0] = e0;
         sh_carry[1] = e1;
       }
@@ -690,6 +695,7 @@ struct SegArgs {
   uint64_t* cnt;  // [U_max + 1] exact positions per unit
   uint64_t* off;  // [U_max + 1] their exclusive scan
   uint32_t* uhit; // [U_max] first overshoot header of the unit before that is a header of the unit
+  const uint32_t* guard;  // rpp_dec_guard_kernel's verdict: 1 = no stream is split
   uint32_t nblocks, bs, cs;
 };
 
@@ -707,7 +713,7 @@ __global__ void rpp_seg_units_kernel(SegArgs a, uint64_t* ucnt) {
   }
   const uint64_t n = a.n_samples[i], nb = a.in_bytes[i];
   uint64_t c = 1;
-  if (seg_stream_ok(n, nb, a.cs))
+  if (!*a.guard && seg_stream_ok(n, nb, a.cs))
     c = (rpp_internal::seg_last_bit((uint32_t)(a.in_off[i] & 3u), nb, n, a.bs, a.cs) >> a.sv.seg_log2) + 1;
   ucnt[i] = c;
 }
@@ -987,51 +993,80 @@ ExtractKernel extract_kernel_for(uint32_t bs) {
 }
 
 // The segmented decode forks the fused launch of a batch's one-unit streams
-// onto a second stream of the device (created once, never destroyed), so that
-// it overlaps the units' parse; events order it after the unit counts and
-// before the batch's end on the caller's stream (graph-capturable).
+// onto a side stream, so that it overlaps the units' parse; events order it
+// after the unit counts and before the batch's end on the caller's stream.
+// Every caller stream has its own side stream and event pair (created once,
+// never destroyed), so concurrent callers never wait on each other's work and
+// a capture of the caller's stream captures the fork and join; the entry's
+// mutex is held from the fork to the join, so two threads sharing one caller
+// stream do not interleave their use of the events.
 constexpr uint32_t kDecSideWaves = 16;  // (full workgroups: the fused launch holds as few CUs as it can)
-hipStream_t side_stream() {
+struct SideStream {
+  hipStream_t s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
+};
+SideStream* side_stream_for(hipStream_t caller) {
   static std::mutex mu;
-  static std::map<int, hipStream_t>* streams = new std::map<int, hipStream_t>;
+  static auto* table = new std::map<std::pair<int, hipStream_t>, SideStream*>;  // (leaked at exit: no HIP calls then)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
-  auto it = streams->find(dev);
-  if (it != streams->end()) return it->second;
-  hipStream_t s2 = nullptr;
-  if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  streams->emplace(dev, s2);
-  return s2;
+  auto it = table->find({dev, caller});
+  if (it != table->end()) return it->second;
+  auto* e = new SideStream;
+  if (hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->join, hipEventDisableTiming) != hipSuccess)
+    return nullptr;  // (a half-built entry is not kept)
+  table->emplace(std::make_pair(dev, caller), e);
+  return e;
 }
+
+// Joins the side stream into the caller's stream on every exit path once
+// forked: after an error the caller's stream still waits for the side work,
+// which writes d_out / d_status.
+class SideFork {
+ public:
+  explicit SideFork(SideStream* e) : e_{e}, lk_{e->mu} {}
+  SideFork(const SideFork&) = delete;
+  SideFork& operator=(const SideFork&) = delete;
+  bool fork(hipStream_t s) {
+    s_ = s;
+    forked_ = hipEventRecord(e_->fork, s) == hipSuccess && hipStreamWaitEvent(e_->s2, e_->fork, 0) == hipSuccess;
+    return forked_;
+  }
+  hipStream_t side() const { return e_->s2; }
+  bool join() {
+    if (!forked_) return true;
+    forked_ = false;
+    return hipEventRecord(e_->join, e_->s2) == hipSuccess && hipStreamWaitEvent(s_, e_->join, 0) == hipSuccess;
+  }
+  ~SideFork() { (void)join(); }
+
+ private:
+  SideStream* e_;
+  std::lock_guard<std::mutex> lk_;
+  hipStream_t s_ = nullptr;
+  bool forked_ = false;
+};
 
 bool extract_bs(uint32_t bs) { return bs == 16 || bs == 32 || bs == 64 || bs == 128; }
 
-// The two-stage decode of every stream is selected by RICEPP_DECODE=two-stage;
-// the default for batches without long streams is the fused
-// one-wave-per-stream kernel (rpp_decode_kernel).  Measured on MI355X
-// (DESIGN.md section 4): the parse pass alone costs 86 VALU per 128-sample
-// sub-block and is VALU-bound at 74 % (196 us for 4096 x 64 KiB), about what
-// the fused kernel needs for parse AND values (258 us), whose value work
-// hides in the parse chain's latency; so splitting the passes does not pay
-// when the batch has enough streams to fill the GPU.
-bool two_stage(const rpp_config* cfg) {
-  const char* e = getenv("RICEPP_DECODE");
-  if (!e || std::string(e) != "two-stage") return false;
-  return extract_bs(cfg->block_size);
-}
+uint32_t path_of(const rpp_decode_options* opt) { return opt ? opt->path : RPP_DECODE_AUTO; }
 
-// Segmented decode (units of 2^L bits; 0 = off): when the batch's longest
-// stream would take longer to parse serially than the whole batch takes at
-// full occupancy (its samples > 1/1024 of the batch's, and >= 2^18).
-// RICEPP_DECODE=segmented forces it, =fused disables it; RICEPP_SEG_LOG2 sets
-// L (tests use small units to split short streams).
-uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples) {
+// Segmented decode (units of 2^L bits; 0 = one wave per stream): by default
+// when the batch's longest stream would take longer to parse serially than
+// the whole batch takes at full occupancy (its samples > 1/1024 of the
+// batch's, and >= 2^18).  Measured on MI355X: for
+// batches of many short streams the fused kernel wins -- its value work
+// hides in the parse chain's latency -- so it is not split.
+uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                      const rpp_decode_options* opt) {
   if (!extract_bs(cfg->block_size)) return 0;
-  const char* e = getenv("RICEPP_DECODE");
-  const std::string mode = e ? e : "";
-  if (mode == "fused" || mode == "two-stage") return 0;
-  if (mode != "segmented") {
+  const uint32_t path = path_of(opt);
+  if (path == RPP_DECODE_FUSED) return 0;
+  if (path != RPP_DECODE_SEGMENTED) {
     if (max_stream_samples < (1u << 18)) return 0;
     if (max_stream_samples * 1024 < total_samples) return 0;
   }
@@ -1042,8 +1077,36 @@ uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t ma
   // kernel
   uint32_t L = 18;
   while (L < 23 && ((total_samples * 8) >> L) > 4096) ++L;
-  if (const char* l = getenv("RICEPP_SEG_LOG2")) L = (uint32_t)std::min(26, std::max(10, atoi(l)));
+  if (opt && opt->seg_log2) L = std::min<uint32_t>(26, std::max<uint32_t>(10, opt->seg_log2));  // (range-checked by the caller)
   return L;
+}
+
+// The batch against the workspace's promise: the sum and the maximum of the
+// (decodable) streams' sample counts.  A batch larger than promised is
+// decoded one wave per stream (guard = 1): the counting kernels then give
+// every stream one unit and no sub-blocks, so no workspace-indexed write
+// happens, and the fused kernel, which needs no workspace, decodes it all.
+constexpr uint32_t kGuardThreads = 1024;
+__global__ __launch_bounds__(kGuardThreads) void rpp_dec_guard_kernel(const uint64_t* n_samples, uint32_t nblocks,
+                                                                      uint32_t cs, uint64_t total_samples,
+                                                                      uint64_t max_stream_samples, uint32_t* guard) {
+  __shared__ uint32_t bad;
+  __shared__ unsigned long long sum;
+  if (threadIdx.x == 0) {
+    bad = 0;
+    sum = 0;
+  }
+  __syncthreads();
+  unsigned long long part = 0;
+  for (uint32_t i = threadIdx.x; i < nblocks; i += kGuardThreads) {
+    const uint64_t n = n_samples[i];
+    if (n % cs != 0 || n >= RPP_MAX_STREAM_SAMPLES) continue;  // (not decodable: reported by the kernels)
+    part += n;
+    if (n > max_stream_samples) bad = 1;
+  }
+  atomicAdd(&sum, part);
+  __syncthreads();
+  if (threadIdx.x == 0) *guard = (bad || sum > total_samples) ? 1u : 0u;
 }
 
 }  // namespace
@@ -1069,56 +1132,69 @@ int rpp_diag_read(unsigned long long* out8, int reset) {
   return RPP_OK;
 }
 
-uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
-                                    uint32_t nblocks) {
+uint64_t rpp_decode_workspace_bytes_ex(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                                       uint32_t nblocks, const rpp_decode_options* opt) {
   if (rpp_check_config(cfg) != RPP_OK) return 0;
-  const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples);
-  if (!L && !two_stage(cfg)) return 0;  // the fused kernel needs none
+  const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples, opt);
+  if (!L) return 0;  // the fused kernel needs none
   return layout(cfg, total_samples, max_stream_samples, nblocks, L, nullptr).bytes;
 }
 
-int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                                    uint32_t nblocks) {
+  return rpp_decode_workspace_bytes_ex(cfg, total_samples, max_stream_samples, nblocks, nullptr);
+}
+
+int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                         const uint64_t* d_n_samples, int32_t* d_status, uint64_t total_samples,
-                        uint64_t max_stream_samples, void* d_workspace, uint64_t workspace_bytes, void* stream) {
+                        uint64_t max_stream_samples, void* d_workspace, uint64_t workspace_bytes,
+                        const rpp_decode_options* opt, void* stream) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
+  if (opt && (opt->path > RPP_DECODE_SEGMENTED || opt->fused_waves > kDecSideWaves ||
+              (opt->seg_log2 && (opt->seg_log2 < 10 || opt->seg_log2 > 26))))
+    return RPP_INVALID_ARGUMENT;
   if (nblocks == 0) return RPP_OK;
   if (!d_in || !d_in_offsets || !d_in_bytes || !d_out || !d_out_offsets || !d_n_samples || !d_status)
     return RPP_INVALID_ARGUMENT;
   hipStream_t s = (hipStream_t)stream;
-  const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples);
-  if (!L && !two_stage(cfg))
+  const uint32_t fused_waves = opt ? opt->fused_waves : 0u;
+  const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples, opt);
+  if (!L)
     return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                             d_n_samples, d_status, s);
+                                             d_n_samples, d_status, s, false, nullptr, fused_waves);
   const Workspace w = layout(cfg, total_samples, max_stream_samples, nblocks, L, static_cast<uint8_t*>(d_workspace));
   if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
+  SideStream* side = side_stream_for(s);
+  if (!side) return RPP_HIP_ERROR;
   const uint32_t chunk_len = cfg->block_size * cfg->component_stream_count;
   const uint32_t g256 = (nblocks + 256) / 256;
-  hipStream_t s2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  const uint32_t test = opt ? opt->test_flags : 0u;
   SegArgs a{};
-  if (L) {
-    a.sv = rpp_internal::SegView{w.unit_map, w.unit_base, w.pl_base, w.plist, w.ovr, w.ustate, w.ulo, w.uov,
-                                 w.sst, w.sflags, w.queue, L, 0, (uint32_t)w.units_max};
-    a.in = d_in;
-    a.in_off = d_in_offsets;
-    a.in_bytes = d_in_bytes;
-    a.n_samples = d_n_samples;
-    a.sb_base = w.sb_base;
-    a.sb_pos = w.sb_pos;
-    a.status = d_status;
-    a.cnt = w.cnt2;
-    a.off = w.off2;
-    a.uhit = w.uhit;
-    a.nblocks = nblocks;
-    a.bs = cfg->block_size;
-    a.cs = cfg->component_stream_count;
-    hipLaunchKernelGGL(rpp_seg_units_kernel, dim3(g256), dim3(256), 0, s, a, w.ucnt);
-    if ((st = rpp_exclusive_scan_u64(w.ucnt, (uint64_t)nblocks + 1, w.unit_base, s)) != RPP_OK) return st;
-  }
+  a.sv = rpp_internal::SegView{w.unit_map, w.unit_base, w.pl_base, w.plist, w.ovr, w.ustate, w.ulo, w.uov,
+                               w.sst, w.sflags, w.queue, L, 0, (uint32_t)w.units_max};
+  a.in = d_in;
+  a.in_off = d_in_offsets;
+  a.in_bytes = d_in_bytes;
+  a.n_samples = d_n_samples;
+  a.sb_base = w.sb_base;
+  a.sb_pos = w.sb_pos;
+  a.status = d_status;
+  a.cnt = w.cnt2;
+  a.off = w.off2;
+  a.uhit = w.uhit;
+  a.guard = w.guard;
+  a.nblocks = nblocks;
+  a.bs = cfg->block_size;
+  a.cs = cfg->component_stream_count;
+  hipLaunchKernelGGL(rpp_dec_guard_kernel, dim3(1), dim3(kGuardThreads), 0, s, d_n_samples, nblocks,
+                     cfg->component_stream_count, total_samples, max_stream_samples, w.guard);
+  hipLaunchKernelGGL(rpp_seg_units_kernel, dim3(g256), dim3(256), 0, s, a, w.ucnt);
+  if ((st = rpp_exclusive_scan_u64(w.ucnt, (uint64_t)nblocks + 1, w.unit_base, s)) != RPP_OK) return st;
   hipLaunchKernelGGL(rpp_dec_count_kernel, dim3(g256), dim3(256), 0, s, d_n_samples, nblocks, chunk_len,
-                     cfg->component_stream_count, w.sb_cnt, w.tile_cnt, L ? (const uint64_t*)w.ucnt : nullptr);
+                     cfg->component_stream_count, w.sb_cnt, w.tile_cnt, (const uint64_t*)w.ucnt,
+                     (const uint32_t*)w.guard);
   if ((st = rpp_exclusive_scan_u64(w.sb_cnt, (uint64_t)nblocks + 1, w.sb_base, s)) != RPP_OK) return st;
   if ((st = rpp_exclusive_scan_u64(w.tile_cnt, (uint64_t)nblocks + 1, w.tile_base, s)) != RPP_OK) return st;
   hipLaunchKernelGGL(rpp_dec_level_count_kernel, dim3(w.levels + 1), dim3(kLvlThreads), 0, s, w.tile_cnt, nblocks,
@@ -1128,48 +1204,40 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
                      w.levels, w.lvl_base, w.tile_map, w.tile_lt);
   if (hipMemsetAsync(w.tile_state, 0, w.max_tiles * 8, s) != hipSuccess) return RPP_HIP_ERROR;
   if (hipMemsetAsync(w.counter, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (!L) {
-    st = rpp_internal::launch_parse(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base, w.sb_pos,
-                                    d_status, s);
-    if (st != RPP_OK) return st;
-  } else {
-    const uint64_t U = w.units_max;
-    // the streams that fit one unit: one wave each, parse and values fused,
-    // on the side stream while the units are parsed
-    s2 = side_stream();
-    if (!s2 || hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess ||
-        hipEventRecord(ev_fork, s) != hipSuccess || hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess)
-      return RPP_HIP_ERROR;
-    st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                           d_n_samples, d_status, s2, false, w.ucnt, kDecSideWaves);
-    if (st != RPP_OK) return st;
-    if (hipEventRecord(ev_join, s2) != hipSuccess) return RPP_HIP_ERROR;
-    if (hipMemsetAsync(w.pl_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
-    if (hipMemsetAsync(w.cnt2, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
-    if (hipMemsetAsync(w.sst, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
-    if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
-    if (hipMemsetAsync(w.queue, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
-    hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.pl_cnt);
-    if ((st = rpp_exclusive_scan_u64(w.pl_cnt, U + 1, w.pl_base, s)) != RPP_OK) return st;
-    if (hipMemsetAsync(w.ustate, 0xFF, U * rpp_internal::kUsWords * 4, s) != hipSuccess) return RPP_HIP_ERROR;
-    const uint32_t gu = (uint32_t)((U + 255) / 256);
-    // pass 0: every unit; three rerun passes; a serial pass for what is left
-    for (uint32_t pass : {0u, 1u, 1u, 1u, 2u}) {
-      a.sv.pass = pass;  // (the stitch counts the reruns it asks this pass for)
-      if (pass != 0) {
-        hipLaunchKernelGGL(rpp_seg_hit_kernel, dim3(gu), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(rpp_seg_stitch_kernel, dim3(nblocks), dim3(64), 0, s, a);
-      }
-      st = rpp_internal::launch_parse_seg(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base,
-                                          w.sb_pos, d_status, a.sv, s);
-      if (st != RPP_OK) return st;
+  // the streams that fit one unit (all of them when the guard tripped): one
+  // wave each, parse and values fused, on the side stream while the units are
+  // parsed
+  SideFork fork{side};
+  if (!fork.fork(s)) return RPP_HIP_ERROR;
+  st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
+                                         d_n_samples, d_status, fork.side(), false, w.ucnt,
+                                         fused_waves ? fused_waves : kDecSideWaves);
+  if (st != RPP_OK) return st;
+  const uint64_t U = w.units_max;
+  if (hipMemsetAsync(w.pl_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (hipMemsetAsync(w.cnt2, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (hipMemsetAsync(w.sst, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (hipMemsetAsync(w.queue, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
+  hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(g256), dim3(256), 0, s, a, w.unit_map, w.pl_cnt);
+  if ((st = rpp_exclusive_scan_u64(w.pl_cnt, U + 1, w.pl_base, s)) != RPP_OK) return st;
+  if (hipMemsetAsync(w.ustate, 0xFF, U * rpp_internal::kUsWords * 4, s) != hipSuccess) return RPP_HIP_ERROR;
+  const uint32_t gu = (uint32_t)((U + 255) / 256);
+  // pass 0: every unit; three rerun passes; a serial pass for what is left
+  for (uint32_t pass : {0u, 1u, 1u, 1u, 2u}) {
+    a.sv.pass = pass;  // (the stitch counts the reruns it asks this pass for)
+    if (pass != 0) {
+      hipLaunchKernelGGL(rpp_seg_hit_kernel, dim3(gu), dim3(256), 0, s, a);
+      hipLaunchKernelGGL(rpp_seg_stitch_kernel, dim3(nblocks), dim3(64), 0, s, a);
     }
-    hipLaunchKernelGGL(rpp_seg_count_kernel, dim3(gu), dim3(256), 0, s, a);
-    if ((st = rpp_exclusive_scan_u64(w.cnt2, U + 1, w.off2, s)) != RPP_OK) return st;
-    hipLaunchKernelGGL(rpp_seg_write_kernel, dim3((uint32_t)U), dim3(kSegThreads), 0, s, a);
-    hipLaunchKernelGGL(rpp_seg_tail_kernel, dim3(g256), dim3(256), 0, s, a);
+    st = rpp_internal::launch_parse_seg(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, w.sb_base,
+                                        w.sb_pos, d_status, a.sv, s);
+    if (st != RPP_OK) return st;
   }
+  hipLaunchKernelGGL(rpp_seg_count_kernel, dim3(gu), dim3(256), 0, s, a);
+  if ((st = rpp_exclusive_scan_u64(w.cnt2, U + 1, w.off2, s)) != RPP_OK) return st;
+  hipLaunchKernelGGL(rpp_seg_write_kernel, dim3((uint32_t)U), dim3(kSegThreads), 0, s, a);
+  hipLaunchKernelGGL(rpp_seg_tail_kernel, dim3(g256), dim3(256), 0, s, a);
   const bool sh = cfg->unused_lsb_count != 0;
   const ExtractKernel k = cfg->component_stream_count == 1
                               ? (sh ? extract_kernel_for<1, true>(cfg->block_size)
@@ -1178,65 +1246,34 @@ int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64
                                     : extract_kernel_for<2, false>(cfg->block_size));
   ExtractParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_out, d_out_offsets, d_status, w.sb_pos, w.sb_base,
                   w.tile_base, w.tile_map, w.tile_lt, w.lvl_base + w.levels, w.tile_state, w.counter, nblocks,
-                  cfg->block_size,
-                  cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count, 0u};
-  if (const char* e = getenv("RICEPP_DEC2_DBG")) p.dbg = (uint32_t)atoi(e);
+                  cfg->block_size, cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count, test};
   const uint32_t grid = (uint32_t)std::min<uint64_t>(w.max_tiles, kMaxExtractGrid);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kTile), 0, s, p);
   if (hipGetLastError() != hipSuccess) return RPP_HIP_ERROR;
-  if (L) {
-    // join the side stream, then the streams whose exact chain left the
-    // region the units cover or whose lists overflowed (the fused kernel)
-    if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return RPP_HIP_ERROR;
-    (void)hipEventDestroy(ev_fork);  // (released once complete)
-    (void)hipEventDestroy(ev_join);
-    st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                           d_n_samples, d_status, s, true);
-    if (st != RPP_OK) return st;
-  }
-  hipLaunchKernelGGL(rpp_dec_check_max_kernel, dim3(g256), dim3(256), 0, s, d_n_samples, nblocks, max_stream_samples,
-                     d_status);
+  // join the side stream, then the streams whose exact chain left the region
+  // the units cover or whose lists overflowed (the fused kernel)
+  if (!fork.join()) return RPP_HIP_ERROR;
+  st = rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
+                                         d_n_samples, d_status, s, true, nullptr, fused_waves);
+  if (st != RPP_OK) return st;
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
-// Without a workspace: the fused kernel (no host synchronisation), or, with
-// RICEPP_DECODE set to two-stage / segmented, the sample counts are read back
-// to size a temporary workspace (this call then synchronises the stream).
+int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                        const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
+                        const uint64_t* d_n_samples, int32_t* d_status, uint64_t total_samples,
+                        uint64_t max_stream_samples, void* d_workspace, uint64_t workspace_bytes, void* stream) {
+  return rpp_decode_batch_ex(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets, d_n_samples,
+                             d_status, total_samples, max_stream_samples, d_workspace, workspace_bytes, nullptr,
+                             stream);
+}
+
+// Without a workspace: always one wave per stream (no host synchronisation).
 int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                      const uint64_t* d_n_samples, int32_t* d_status, void* stream) {
-  int st = rpp_check_config(cfg);
-  if (st != RPP_OK) return st;
-  if (nblocks == 0) return RPP_OK;
-  if (!d_in || !d_in_offsets || !d_in_bytes || !d_out || !d_out_offsets || !d_n_samples || !d_status)
-    return RPP_INVALID_ARGUMENT;
-  hipStream_t s = (hipStream_t)stream;
-  const char* e = getenv("RICEPP_DECODE");
-  const std::string mode = e ? e : "";
-  if ((mode != "two-stage" && mode != "segmented") || !extract_bs(cfg->block_size))
-    return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                             d_n_samples, d_status, s);
-  uint64_t* h = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&h), (size_t)nblocks * 8, hipHostMallocDefault) != hipSuccess)
-    return RPP_HIP_ERROR;
-  uint64_t total = 0, mx = 0;
-  bool ok = hipMemcpyAsync(h, d_n_samples, (size_t)nblocks * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
-            hipStreamSynchronize(s) == hipSuccess;
-  if (ok)
-    for (uint32_t i = 0; i < nblocks; ++i)
-      if (h[i] < RPP_MAX_STREAM_SAMPLES) {
-        total += h[i];
-        mx = std::max<uint64_t>(mx, h[i]);
-      }
-  (void)hipHostFree(h);
-  if (!ok) return RPP_HIP_ERROR;
-  const uint64_t bytes = rpp_decode_workspace_bytes(cfg, total, mx, nblocks);
-  void* ws = nullptr;
-  if (bytes && hipMallocAsync(&ws, bytes, s) != hipSuccess) return RPP_HIP_ERROR;
-  st = rpp_decode_batch_ws(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets, d_n_samples, d_status,
-                           total, mx, ws, bytes, s);
-  if (ws) (void)hipFreeAsync(ws, s);
-  return st;
+  return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
+                                           d_n_samples, d_status, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -75,14 +75,9 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
                         const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback = false,
                         const uint64_t* d_units = nullptr, uint32_t waves = 0);
 
-// rpp_parse_kernel: sub-block start positions of every stream into sb_pos
-// (stream b's entries from sb_base[b]: nsb_b header positions, then the end).
-int launch_parse(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets, const uint64_t* d_in_bytes,
-                 uint32_t nblocks, const uint64_t* d_n_samples, const uint64_t* d_sb_base, uint32_t* d_sb_pos,
-                 int32_t* d_status, hipStream_t stream);
-
-// The same kernel over units (SegView): the units of split streams, into the
-// bitmaps and overshoot lists (single-unit streams are left to the fused kernel).
+// rpp_parse_kernel over units (SegView): the units of split streams, into
+// their position and overshoot lists (single-unit streams are left to the
+// fused kernel).
 int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples,
                      const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,

@@ -179,7 +179,14 @@ struct EncParams {
   uint64_t* seg_bits;        // [units] bits a segment wrote (multi-segment streams)
   uint8_t* scratch;          // segments >= 1 of a stream: slot u - b - 1
   uint64_t slot_bytes;
+  // units the workspace holds: a batch with more (its samples exceed the
+  // caller's total_samples) is encoded one wave per stream, nothing split
+  uint64_t max_units;
 };
+// segment mode and the batch fits the workspace
+__device__ __forceinline__ bool enc_split_ok(const EncParams& p) {
+  return p.seg_map && p.seg_base[p.nblocks] <= p.max_units;
+}
 
 // Segment mode: a stream of more than kEncSegChunks chunks is encoded by
 // several waves, one per run of kEncSegChunks chunks.  Every sub-block's codes
@@ -564,10 +571,13 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t win[kEncWin];
   constexpr uint32_t spw = kWave / G;  // sub-blocks per iteration
   uint32_t b = blockIdx.x, seg = 0;
-  if (p.seg_map) {
+  const bool split = enc_split_ok(p);
+  if (split) {
     if (blockIdx.x >= p.seg_base[p.nblocks]) return;
     b = p.seg_map[blockIdx.x];
     seg = blockIdx.x - (uint32_t)p.seg_base[b];
+  } else if (b >= p.nblocks) {
+    return;
   }
   const uint32_t lane = lane_id();
   const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
@@ -585,7 +595,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint16_t* in = p.in + p.in_off[b];
   const uint32_t chunk_len = CS * bs;
   const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
-  const bool multi = p.seg_map && nchunks > kEncSegChunks;
+  const bool multi = split && nchunks > kEncSegChunks;
   // this unit's chunks [c_lo, c_hi)
   const uint32_t c_lo = multi ? seg * kEncSegChunks : 0u;
   const uint32_t c_hi = multi ? min(nchunks, c_lo + kEncSegChunks) : nchunks;
@@ -730,9 +740,10 @@ __global__ void rpp_enc_units_kernel(const uint64_t* n_samples, uint32_t nblocks
   units[i] = u;
 }
 
-__global__ void rpp_enc_unit_map_kernel(const uint64_t* seg_base, uint32_t nblocks, uint32_t* seg_map) {
+__global__ void rpp_enc_unit_map_kernel(const uint64_t* seg_base, uint32_t nblocks, uint64_t max_units,
+                                        uint32_t* seg_map) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nblocks) return;
+  if (i >= nblocks || seg_base[nblocks] > max_units) return;  // (over the workspace: nothing is split)
   for (uint64_t u = seg_base[i]; u < seg_base[i + 1]; ++u) seg_map[u] = i;
 }
 
@@ -745,7 +756,7 @@ __global__ void rpp_enc_unit_map_kernel(const uint64_t* seg_base, uint32_t nbloc
 // (bitstream_writer.h:139-145); the last segment writes size and status.
 __global__ __launch_bounds__(256) void rpp_enc_concat_kernel(EncParams p, const uint64_t* seg_off) {
   const uint32_t u = blockIdx.x;
-  if (u >= p.seg_base[p.nblocks]) return;
+  if (!enc_split_ok(p) || u >= p.seg_base[p.nblocks]) return;
   const uint32_t b = p.seg_map[u];
   const uint32_t first = (uint32_t)p.seg_base[b], nseg = (uint32_t)(p.seg_base[b + 1] - first);
   const uint32_t k = u - first;
@@ -2240,10 +2251,12 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
   return kSegNone;
 }
 
-// SEG = false: one wave per stream (launch_parse).  SEG = true: one wave per
-// unit of rpp_internal::SegView; a stream of one unit is parsed exactly as
-// with SEG = false, a unit of a split stream (ricepp_internal.h) records into
-// its position list / overshoot list instead of sb_pos.
+// One wave per unit of rpp_internal::SegView (SEG = true, the only
+// instantiation launched: launch_parse_seg): a unit of a split stream
+// (ricepp_internal.h) records into its position list / overshoot list; a
+// stream of one unit is left to the fused kernel.  (SEG = false, one wave per
+// stream writing sb_pos, was the whole-batch two-stage decode, measured
+// slower than the fused kernel on every workload and removed.)
 template <uint32_t CS, bool SEG>
 __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParseParams p) {
   using namespace rpp_internal;
@@ -2868,7 +2881,7 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
     return RPP_INVALID_ARGUMENT;
   EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count, nullptr, nullptr, nullptr, nullptr, 0};
+              cfg->unused_lsb_count, nullptr, nullptr, nullptr, nullptr, 0, 0};
   hipLaunchKernelGGL(enc_kernel(cfg), dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
@@ -2900,10 +2913,10 @@ int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint6
                      chunk_len, w.units);
   if ((st = rpp_exclusive_scan_u64(w.units, (uint64_t)nblocks + 1, w.seg_base, s)) != RPP_OK) return st;
   hipLaunchKernelGGL(rpp_enc_unit_map_kernel, dim3((nblocks + 255) / 256), dim3(256), 0, s, w.seg_base, nblocks,
-                     w.seg_map);
+                     w.max_units, w.seg_map);
   EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count, w.seg_map, w.seg_base, w.seg_bits, w.scratch, w.slot_bytes};
+              cfg->unused_lsb_count, w.seg_map, w.seg_base, w.seg_bits, w.scratch, w.slot_bytes, w.max_units};
   hipLaunchKernelGGL(enc_kernel(cfg), dim3((uint32_t)w.max_units), dim3(kWave), 0, s, p);
   if (w.max_units > nblocks) {  // streams long enough to be split: place the segments
     if ((st = rpp_exclusive_scan_u64(w.seg_bits, w.max_units, w.seg_off, s)) != RPP_OK) return st;
@@ -2930,7 +2943,6 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
   // transfer tables, fewer when the batch cannot fill the 256 CUs anyway
   uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
   if (waves) W = std::min<uint32_t>(kDecMaxWaves, waves);
-  if (const char* e = getenv("RICEPP_DEC_WAVES")) W = std::min<uint32_t>(kDecMaxWaves, std::max(1, atoi(e)));  // diagnostics
   const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
   static void (*const kernels[4])(DecParams) = {rpp_decode_kernel<1, false>, rpp_decode_kernel<1, true>,
                                                  rpp_decode_kernel<2, false>, rpp_decode_kernel<2, true>};
@@ -2948,29 +2960,6 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
               cfg->unused_lsb_count, W, only_fallback ? 1u : 0u, d_units};
   const auto k = kernels[2 * (cfg->component_stream_count - 1) + (cfg->unused_lsb_count ? 1 : 0)];
   hipLaunchKernelGGL(k, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, stream, p);
-  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
-}
-
-int launch_parse(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets, const uint64_t* d_in_bytes,
-                 uint32_t nblocks, const uint64_t* d_n_samples, const uint64_t* d_sb_base, uint32_t* d_sb_pos,
-                 int32_t* d_status, hipStream_t stream) {
-  if (nblocks == 0) return RPP_OK;
-  uint32_t W = std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (nblocks + 255) / 256));
-  const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
-  static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1, false>, rpp_parse_kernel<2, false>};
-  static std::once_flag attr_once;
-  static hipError_t attr_err = hipSuccess;
-  std::call_once(attr_once, [] {
-    const int mx = (int)(kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4);
-    for (auto k : kernels)
-      if (attr_err == hipSuccess)
-        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-  });
-  if (attr_err != hipSuccess) return RPP_HIP_ERROR;
-  ParseParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_sb_base, d_sb_pos, d_status, nblocks,
-                cfg->block_size, W};
-  hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3((nblocks + W - 1) / W), dim3(kWave * W), lds,
-                     stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 

@@ -61,6 +61,11 @@ extern "C" {
 #define RPP_INVALID_ARGUMENT (-3)
 #define RPP_OUTPUT_TOO_SMALL (-4)
 #define RPP_HIP_ERROR (-5)
+/* A device-side consistency bound tripped (a decode tile waited longer than
+ * its bound for a predecessor's prefix): the block's output is invalid.  Never
+ * returned for well-formed or malformed input; it reports a bug or a stalled
+ * GPU instead of returning wrong samples as RPP_OK. */
+#define RPP_INTERNAL_ERROR (-6)
 
 /* ricepp::codec_config (ricepp/include/ricepp/codec_config.h:36-41). */
 typedef struct rpp_config {
@@ -135,12 +140,12 @@ int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint6
  *   d_n_samples   [nblocks] samples to decode (multiple of cs)
  *   d_status      [nblocks] RPP_OK, RPP_TRUNCATED_INPUT (the reference's
  *                 std::out_of_range) or RPP_INVALID_ARGUMENT
- * One wave decodes one stream (parse and values fused), asynchronously on
- * `stream`.  This form does not know the batch's longest stream: batches with
- * long streams (a few streams of MiBs) should use rpp_decode_batch_ws, which
- * splits them.  (With RICEPP_DECODE=two-stage or =segmented set, this form
- * reads d_n_samples back to size a temporary workspace: it then synchronises
- * `stream` once.)
+ * This workspace-free form ALWAYS decodes one stream per wavefront (parse
+ * and values fused), fully asynchronously on `stream`.  That is the fast
+ * path for batches of many short streams (thousands of 64 KiB blocks), but a
+ * long stream then decodes at one wave's speed (a 16 MiB block: ~30 ms).
+ * Batches with long streams should use rpp_decode_batch_ws, which splits
+ * them over many waves.
  */
 int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
@@ -160,17 +165,49 @@ uint64_t rpp_decode_workspace_bytes(const rpp_config* cfg, uint64_t total_sample
  * workspace of at least rpp_decode_workspace_bytes(cfg, total_samples,
  * max_stream_samples, nblocks) bytes, where total_samples >= the sum of
  * d_n_samples and max_stream_samples >= the largest.  Fully asynchronous on
- * `stream` (graph-capturable).  A batch whose longest stream holds more than
- * 1/1024 of its samples (and >= 2^18) is decoded segmented (bs 16/32/64/128):
- * long streams are cut into units of 2^18..2^23 bits parsed by one wave each
- * from a guessed first header, stitched exactly, then every sub-block of
- * every stream is decoded by its own lane; other batches one wave per stream.
+ * `stream` (graph-capturable: no host synchronisation; a segmented call forks
+ * part of its work onto a side stream private to `stream` and joins it before
+ * returning).  A batch whose longest stream holds more than 1/1024 of its
+ * samples (and >= 2^18) is decoded segmented: long streams are cut into units
+ * of 2^18..2^23 bits parsed by one wave each from a guessed first header,
+ * stitched exactly, then every sub-block of every stream is decoded by its
+ * own lane; other batches one wave per stream.  If the device finds the
+ * batch larger than total_samples / max_stream_samples promised, it decodes
+ * the whole batch one wave per stream instead (correct, never out of the
+ * workspace's bounds).
  */
 int rpp_decode_batch_ws(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
                         const uint64_t* d_out_offsets, const uint64_t* d_n_samples, int32_t* d_status,
                         uint64_t total_samples, uint64_t max_stream_samples, void* d_workspace,
                         uint64_t workspace_bytes, void* stream);
+
+/*
+ * Explicit decode path selection (tests, diagnostics, tuning).  A NULL
+ * options pointer or a zeroed struct is exactly rpp_decode_batch_ws.
+ */
+#define RPP_DECODE_AUTO 0      /* segmented when the batch has long streams */
+#define RPP_DECODE_FUSED 1     /* one wave per stream, never segmented */
+#define RPP_DECODE_SEGMENTED 2 /* every stream longer than one unit is split */
+/* test_flags: fault injection and diagnostics, 0 in production */
+#define RPP_TEST_NO_FAST_LANES 1u   /* extraction: every lane takes the general path */
+#define RPP_TEST_LOOKBACK_STALL 2u  /* extraction: tile 1 of each stream never publishes its prefix,
+                                       and the look-back gives up after 2^10 polls (-> RPP_INTERNAL_ERROR) */
+#define RPP_TEST_PHASE_TIMERS 4u    /* extraction: per-phase cycle counters (diagnostic builds' tools) */
+typedef struct rpp_decode_options {
+  uint32_t path;        /* RPP_DECODE_AUTO / _FUSED / _SEGMENTED */
+  uint32_t seg_log2;    /* units of 2^seg_log2 bits, 10..26; 0: chosen from the batch */
+  uint32_t fused_waves; /* streams per workgroup of the one-wave-per-stream kernel, 1..16; 0: auto */
+  uint32_t test_flags;  /* RPP_TEST_* */
+} rpp_decode_options;
+
+uint64_t rpp_decode_workspace_bytes_ex(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
+                                       uint32_t nblocks, const rpp_decode_options* opt);
+int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                        const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out,
+                        const uint64_t* d_out_offsets, const uint64_t* d_n_samples, int32_t* d_status,
+                        uint64_t total_samples, uint64_t max_stream_samples, void* d_workspace,
+                        uint64_t workspace_bytes, const rpp_decode_options* opt, void* stream);
 
 /*
  * Unused least-significant bits of 16-bit images (the FITS categorizer's

@@ -23,9 +23,18 @@ def ocfg(c: codec.CodecConfig):
     return O.cfg(c.block_size, c.component_stream_count, c.byteorder == "big", c.unused_lsb_count)
 
 
-def run_batch(cfg, blocks, in_align=8):
+def seg(log2=0, **kw):
+    """Decode options forcing the segmented decode (units of 2**log2 bits; 0: chosen from the batch)."""
+    return codec.DecodeOptions(path="segmented", seg_log2=log2, **kw)
+
+
+FUSED = codec.DecodeOptions(path="fused")
+
+
+def run_batch(cfg, blocks, in_align=8, dec=None):
     """Encodes the list of stored-sample arrays on the GPU, checks every
-    stream against the oracle, decodes on the GPU and checks the samples."""
+    stream against the oracle, decodes on the GPU (decode options `dec`) and
+    checks the samples."""
     oc = ocfg(cfg)
     offs, pos = [], 0
     for b in blocks:
@@ -49,7 +58,7 @@ def run_batch(cfg, blocks, in_align=8):
         if got != w:
             diff = next((k for k in range(min(len(got), len(w))) if got[k] != w[k]), None)
             raise AssertionError(f"block {i} (n={ns[i]}): GPU {len(got)} B vs oracle {len(w)} B, first diff at {diff}")
-    out, dst = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns)
+    out, dst = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns, options=dec)
     torch.cuda.synchronize()
     assert (dst.cpu().numpy() == 0).all(), dst
     outn = out.cpu().numpy().view(np.uint16)
@@ -121,8 +130,7 @@ def test_high_rice_parameters(bs, cs, ulsb):
     # the same streams split into 4 Kib / 32 Kib units (the segmented
     # decode's parse runs the same loop per unit)
     for log2 in (12, 15):
-        with _decode_mode("segmented", log2):
-            run_batch(cfg, blocks)
+        run_batch(cfg, blocks, dec=seg(log2))
 
 
 @pytest.mark.parametrize("bs", [16, 32, 64, 128])
@@ -142,8 +150,7 @@ def test_low_bit_depth_fs1_fs2_mix(bs, cs):
     for ulsb, blocks in cases:
         cfg = codec.CodecConfig(bs, cs, "big", ulsb)
         run_batch(cfg, blocks)
-        with _decode_mode("segmented", 12):
-            run_batch(cfg, blocks)
+        run_batch(cfg, blocks, dec=seg(12))
 
 
 @pytest.mark.parametrize("ulsb", list(range(0, 16)))
@@ -214,7 +221,7 @@ def _oracle_status(oc, data, n):
         return e.status, None
 
 
-def test_truncated_input_status_matches_oracle():
+def test_truncated_input_status_matches_oracle(dec=None):
     rng = np.random.default_rng(11)
     cfg = codec.CodecConfig(128, 1, "big", 0)
     oc = ocfg(cfg)
@@ -228,7 +235,7 @@ def test_truncated_input_status_matches_oracle():
         offs[i] = len(buf)
         buf += s + bytes((-len(s)) % 16 + 16)
     d = torch.from_numpy(np.frombuffer(bytes(buf), np.uint8).copy()).to(DEV)
-    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], [x.size] * len(streams))
+    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], [x.size] * len(streams), options=dec)
     torch.cuda.synchronize()
     st = st.cpu().numpy()
     outn = out.cpu().numpy().view(np.uint16)
@@ -240,7 +247,7 @@ def test_truncated_input_status_matches_oracle():
 
 
 @pytest.mark.parametrize("bs,cs", [(128, 1), (16, 2), (29, 1)])
-def test_corrupt_streams_match_oracle(bs, cs):
+def test_corrupt_streams_match_oracle(bs, cs, dec=None):
     """Random bytes decode to whatever the reference decodes them to (or fail
     the same way): the decoder follows the reference bit for bit."""
     rng = np.random.default_rng(bs + cs)
@@ -260,7 +267,7 @@ def test_corrupt_streams_match_oracle(bs, cs):
         offs[i] = len(buf)
         buf += s + bytes((-len(s)) % 16 + 16)
     d = torch.from_numpy(np.frombuffer(bytes(buf), np.uint8).copy()).to(DEV)
-    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], [n] * nstreams)
+    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], [n] * nstreams, options=dec)
     torch.cuda.synchronize()
     st = st.cpu().numpy()
     outn = out.cpu().numpy().view(np.uint16)
@@ -345,7 +352,7 @@ def test_configs3_block_mix_in_one_launch(cs):
     run_batch(codec.CodecConfig(128, cs, "big", 0), blocks)
 
 
-def _decode_oracle_streams(cfg, blocks, ragged=False):
+def _decode_oracle_streams(cfg, blocks, ragged=False, dec=None):
     """Decode-only (BASELINE configs[2]): streams produced by the CPU oracle, decoded on the GPU.
     ragged: streams start at arbitrary byte offsets (a DwarFS payload follows a 13-18 byte header)."""
     oc = ocfg(cfg)
@@ -361,7 +368,7 @@ def _decode_oracle_streams(cfg, blocks, ragged=False):
         buf[o:o + len(s)] = np.frombuffer(s, np.uint8)
     d = torch.from_numpy(buf).to(DEV)
     ns = [len(b) for b in blocks]
-    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], ns)
+    out, st = codec.decode_batch(cfg, d, offs, [len(s) for s in streams], ns, options=dec)
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
     outn = out.cpu().numpy().view(np.uint16)
@@ -387,90 +394,42 @@ def test_decode_oracle_encoded_32mib_frame():
     _decode_oracle_streams(codec.CodecConfig(128, 1, "big", 0), [frame])
 
 
-# ---- the two-stage decode (RICEPP_DECODE=two-stage: parse pass + lane-per-sub-block extraction) ----
-
-class _decode_mode:
-    """Selects the decode path for the block (RICEPP_DECODE, and RICEPP_SEG_LOG2 for the unit size of the
-    segmented decode: small units split even short streams into many)."""
-
-    def __init__(self, mode, seg_log2=None):
-        self.env = {"RICEPP_DECODE": mode, "RICEPP_SEG_LOG2": None if seg_log2 is None else str(seg_log2)}
-
-    def __enter__(self):
-        import os
-        self.old = {k: os.environ.get(k) for k in self.env}
-        for k, v in self.env.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-    def __exit__(self, *a):
-        import os
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
-def _two_stage():
-    return _decode_mode("two-stage")
-
+# ---- the lane-per-sub-block extraction (the second half of the segmented decode) on every stream ----
 
 @pytest.mark.parametrize("bs", [16, 32, 64, 128])
 @pytest.mark.parametrize("cs", [1, 2])
-def test_two_stage_decode_config_matrix(bs, cs):
+@pytest.mark.parametrize("general", [False, True])
+def test_extraction_config_matrix(bs, cs, general):
+    """Every stream longer than 1 Kib split (segmented, 2**10-bit units), so nearly every sub-block of every
+    data kind goes through the extraction kernel; general=True sends every lane down its exact runtime-loop
+    path (RPP_TEST_NO_FAST_LANES) instead of the unrolled fast lanes."""
     rng = np.random.default_rng(7000 + bs + cs)
-    with _two_stage():
-        for be, ulsb in ((True, 0), (False, 3)):
-            cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
-            blocks = []
-            for kind in ("poisson", "benchmark", "codec_test", "constant", "full_range", "spiky", "zeros"):
-                n = int(rng.integers(1, 6000)) // cs * cs
-                if kind == "poisson":
-                    blocks.append(datagen.poisson_data(rng, n, ulsb=ulsb, big_endian=be))
-                elif kind == "benchmark":
-                    blocks.append(datagen.benchmark_data(rng, n, ulsb=ulsb, big_endian=be))
-                elif kind == "codec_test":
-                    blocks.append(datagen.codec_test_data(rng, n, ulsb=ulsb, big_endian=be))
-                elif kind == "constant":
-                    blocks.append(datagen.constant_data(n, ulsb=ulsb, big_endian=be))
-                elif kind == "full_range":
-                    blocks.append(datagen.full_range_data(rng, n, ulsb=ulsb, big_endian=be))
-                elif kind == "spiky":
-                    blocks.append(datagen.spiky_data(rng, n, ulsb=ulsb, big_endian=be))
-                else:
-                    blocks.append(np.zeros(n, np.uint16))
-            run_batch(cfg, blocks)
-            _decode_oracle_streams(cfg, blocks)
+    dec = seg(10, test_flags=codec.N.RPP_TEST_NO_FAST_LANES if general else 0)
+    for be, ulsb in ((True, 0), (False, 3)):
+        cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
+        sizes = rng.integers(1, 6000, 7)
+        blocks = _kind_blocks(rng, sizes, cs, ulsb, be)
+        run_batch(cfg, blocks, dec=dec)
+        _decode_oracle_streams(cfg, blocks, dec=dec)
 
 
-def test_two_stage_decode_long_streams_and_mix():
+def test_segmented_decode_long_streams_and_mix():
     rng = np.random.default_rng(77)
     blocks = [datagen.poisson_data(rng, m * (1 << 19)) for m in (1, 4, 1)] + [datagen.benchmark_data(rng, 300000)]
-    with _two_stage():
-        run_batch(codec.CodecConfig(128, 1, "big", 0), blocks)
-        run_batch(codec.CodecConfig(128, 2, "big", 0), blocks[:2])
+    run_batch(codec.CodecConfig(128, 1, "big", 0), blocks, dec=seg(14))
+    run_batch(codec.CodecConfig(128, 2, "big", 0), blocks[:2], dec=seg(14))
 
 
-def test_two_stage_decode_errors_match_oracle():
-    with _two_stage():
-        test_truncated_input_status_matches_oracle()
-        for bs, cs in ((128, 1), (16, 2)):
-            test_corrupt_streams_match_oracle(bs, cs)
-
-
-@pytest.mark.parametrize("two_stage", [False, True])
-def test_decode_streams_at_any_byte_offset(two_stage):
-    """rpp_decode_batch takes streams at any byte offset (no repack of DwarFS payloads)."""
+@pytest.mark.parametrize("path", ["auto", "segmented"])
+def test_decode_streams_at_any_byte_offset(path):
+    """Decode takes streams at any byte offset (no repack of DwarFS payloads): the fused kernel (auto on
+    these short streams) and the segmented decode with 1 Kib units."""
     rng = np.random.default_rng(99)
-    ctx = _two_stage() if two_stage else __import__("contextlib").nullcontext()
-    with ctx:
-        for bs, cs in ((128, 1), (16, 2), (29, 1), (64, 2)):
-            blocks = [datagen.poisson_data(rng, int(n) // cs * cs) for n in rng.integers(0, 40000, 9)]
-            blocks += [datagen.benchmark_data(rng, 3000 // cs * cs), datagen.full_range_data(rng, 1000 // cs * cs)]
-            _decode_oracle_streams(codec.CodecConfig(bs, cs, "big", 0), blocks, ragged=True)
+    dec = seg(10) if path == "segmented" else None
+    for bs, cs in ((128, 1), (16, 2), (29, 1), (64, 2)):
+        blocks = [datagen.poisson_data(rng, int(n) // cs * cs) for n in rng.integers(0, 40000, 9)]
+        blocks += [datagen.benchmark_data(rng, 3000 // cs * cs), datagen.full_range_data(rng, 1000 // cs * cs)]
+        _decode_oracle_streams(codec.CodecConfig(bs, cs, "big", 0), blocks, ragged=True, dec=dec)
 
 
 @pytest.mark.parametrize("bs,cs", [(128, 1), (16, 1), (32, 2), (13, 2), (512, 1)])
@@ -536,12 +495,11 @@ def test_segmented_decode_config_matrix(bs, cs, seg_log2):
     rng = np.random.default_rng(9000 + 100 * seg_log2 + bs + cs)
     sizes = [rng.integers(1, 400) * cs, 40000, 70001, 123457, 5000, 31, 65536 + 3, 90000, 200000]
     codec.segmented_decode_stats(reset=True)
-    with _decode_mode("segmented", seg_log2):
-        for be, ulsb in ((True, 0), (False, 3)):
-            cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
-            blocks = _kind_blocks(rng, sizes, cs, ulsb, be)
-            run_batch(cfg, blocks)
-            _decode_oracle_streams(cfg, blocks, ragged=True)
+    for be, ulsb in ((True, 0), (False, 3)):
+        cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
+        blocks = _kind_blocks(rng, sizes, cs, ulsb, be)
+        run_batch(cfg, blocks, dec=seg(seg_log2))
+        _decode_oracle_streams(cfg, blocks, ragged=True, dec=seg(seg_log2))
     stats = codec.segmented_decode_stats(reset=True)
     assert stats["met"] > 0, stats  # the units were split and stitched
     diag = (__import__("ctypes").c_ulonglong * 8)()
@@ -555,10 +513,9 @@ def test_segmented_decode_errors_match_oracle():
     """Truncated and corrupt streams, split into 1 Kib units: the status and the output are the oracle's
     (a corrupt chain that runs past the region a stream's sample count allows is decoded by the fused kernel)."""
     for log2 in (10, 12):
-        with _decode_mode("segmented", log2):
-            test_truncated_input_status_matches_oracle()
-            for bs, cs in ((128, 1), (16, 2)):
-                test_corrupt_streams_match_oracle(bs, cs)
+        test_truncated_input_status_matches_oracle(dec=seg(log2))
+        for bs, cs in ((128, 1), (16, 2)):
+            test_corrupt_streams_match_oracle(bs, cs, dec=seg(log2))
 
 
 def test_segmented_decode_is_chosen_for_long_streams():
@@ -573,8 +530,7 @@ def test_segmented_decode_is_chosen_for_long_streams():
     run_batch(cfg, blocks)
     stats = codec.segmented_decode_stats(reset=True)
     assert stats["met"] > 0 and stats["fallback"] == 0, stats
-    with _decode_mode("fused"):
-        _decode_oracle_streams(cfg, blocks[1:3])
+    _decode_oracle_streams(cfg, blocks[1:3], dec=FUSED)
 
 
 def test_segmented_decode_of_a_64mib_stream():

@@ -66,6 +66,35 @@ def test_empty_batch_is_ok_without_gpu():
     assert N.lib().rpp_encode_batch(C.byref(bad), null, null, null, 5, null, null, null, null, null) == -1
 
 
+def test_decode_options_validated_without_gpu():
+    """rpp_decode_batch_ex: a NULL or zeroed options struct is rpp_decode_batch_ws; out-of-range options are
+    RPP_INVALID_ARGUMENT before anything is launched; the workspace size follows the forced path."""
+    c = N.RppConfig(128, 1, 1, 0)
+    null = C.c_void_p(0)
+    L = N.lib()
+
+    def call(o):
+        return L.rpp_decode_batch_ex(C.byref(c), null, null, null, 0, null, null, null, null, 0, 0, null, 0,
+                                     C.byref(o) if o is not None else None, null)
+
+    assert call(None) == N.RPP_OK
+    assert call(N.RppDecodeOptions(0, 0, 0, 0)) == N.RPP_OK
+    assert call(N.RppDecodeOptions(3, 0, 0, 0)) == N.RPP_INVALID_ARGUMENT
+    assert call(N.RppDecodeOptions(2, 9, 0, 0)) == N.RPP_INVALID_ARGUMENT
+    assert call(N.RppDecodeOptions(2, 27, 0, 0)) == N.RPP_INVALID_ARGUMENT
+    assert call(N.RppDecodeOptions(1, 0, 17, 0)) == N.RPP_INVALID_ARGUMENT
+
+    def ws(o, total, mx, nb):
+        return L.rpp_decode_workspace_bytes_ex(C.byref(c), total, mx, nb, C.byref(o) if o is not None else None)
+
+    # 4096 x 64 KiB: one wave per stream by default, no workspace
+    assert ws(None, 4096 * 32768, 32768, 4096) == 0 == L.rpp_decode_workspace_bytes(C.byref(c), 4096 * 32768, 32768, 4096)
+    assert ws(N.RppDecodeOptions(2, 12, 0, 0), 4096 * 32768, 32768, 4096) > 0
+    # one 16 MiB block: segmented by default, never when fused is forced
+    assert ws(None, 1 << 23, 1 << 23, 1) > 0
+    assert ws(N.RppDecodeOptions(1, 0, 0, 0), 1 << 23, 1 << 23, 1) == 0
+
+
 @pytest.mark.parametrize("size,bs,cs,ulsb,be", [(65536, 128, 1, 0, True), (65536, 128, 1, 0, False),
                                                (0, 16, 2, 8, True), (2**40 + 3, 512, 2, 6, False)])
 def test_frame_header_matches_oracle_and_roundtrips(size, bs, cs, ulsb, be):

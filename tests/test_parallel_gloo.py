@@ -118,3 +118,46 @@ def test_world2_size_gather_cached_uniform_and_ragged(tmp_path):
             want = [v for r, c in enumerate(counts) for v in (np.arange(c) + 1000 * r + 100 * step).tolist()]
             assert sizes == want, name
             assert offs == [0] + np.cumsum(want)[:-1].tolist() if want else offs == [], name
+
+
+def _mix_worker(rank, world, port, out_path):
+    """bench.py --workload mix on one rank, without the codec: its byte-balanced share of the configs[3]
+    block list, a stand-in encoded size per block (a function of the block index alone), the all-gather of
+    the sizes and the image offsets."""
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mix = bench.mix_block_mib(32)
+    ranges = parallel.partition_blocks([m << 20 for m in mix], world)
+    lo, hi = ranges[rank]
+    sizes = torch.tensor([(mix[i] << 19) + 7 * i for i in range(lo, hi)], dtype=torch.int64)
+    gather = parallel.SizeGather(hi - lo, "cpu", dist.group.WORLD)
+    all_sizes = gather(sizes)
+    offs = parallel.global_offsets(all_sizes)
+    if rank == 0:
+        json.dump({"ranges": ranges, "sizes": all_sizes.tolist(), "offsets": offs.tolist()}, open(out_path, "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mix_workload_partition_and_offsets(tmp_path, world):
+    """configs[3] strong-scaling mode: the ranks' shards cover the 32 GiB mix exactly once, in order,
+    balanced by bytes; the gathered sizes and image offsets are those of the whole list."""
+    import bench
+
+    out = tmp_path / "mix.json"
+    mp.spawn(_mix_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
+    res = json.loads(out.read_text())
+    mix = bench.mix_block_mib(32)
+    assert sum(mix) == 32 * 1024 and len(mix) == 5120
+    ranges = res["ranges"]
+    assert ranges[0][0] == 0 and ranges[-1][1] == len(mix)
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    share = [sum(mix[a:b]) for a, b in ranges]
+    assert max(share) - min(share) <= 32  # MiB: within two 16 MiB blocks
+    want = [(m << 19) + 7 * i for i, m in enumerate(mix)]
+    assert res["sizes"] == want
+    assert res["offsets"] == list(np.concatenate([[0], np.cumsum(want)[:-1]]).astype(int))
