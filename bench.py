@@ -209,6 +209,8 @@ def main() -> None:
     ap.add_argument("--workload", choices=("blocks", "mix"), default="blocks",
                     help="blocks: configs[1] (default, weak scaling); mix: configs[3] (strong scaling)")
     ap.add_argument("--mix-gib", type=int, default=32, help="total size of the configs[3] mix")
+    ap.add_argument("--decode-path", choices=("auto", "fused", "segmented"), default="auto",
+                    help="force a decode path (A/B measurements; the default is the library's own choice)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -221,18 +223,20 @@ def main() -> None:
 
     cfg = codec.CodecConfig(block_size=128, component_stream_count=1, byteorder="big", unused_lsb_count=0)
     group = dist.group.WORLD if world > 1 else None
+    dopt = codec.DecodeOptions(path=args.decode_path)
     if args.workload == "mix":
         mix = mix_block_mib(args.mix_gib)
         lo, hi = parallel.partition_blocks([m << 20 for m in mix], world)[rank]
         x, in_offsets, ns = make_mix_shard(mix, lo, hi, dev)
         nblocks, n = hi - lo, 0
-        pipe = parallel.ShardPipeline(cfg, x, in_offsets, ns, group=group)
+        pipe = parallel.ShardPipeline(cfg, x, in_offsets, ns, group=group, decode_options=dopt)
         shard_bytes = int(ns.sum()) * 2
     else:
         nblocks, n = args.blocks, args.block_bytes // 2
         x = make_poisson_blocks(nblocks, n, 1000.0, 42 + rank, dev)
         in_offsets = np.arange(nblocks, dtype=np.int64) * n
-        pipe = parallel.ShardPipeline(cfg, x, in_offsets, np.full(nblocks, n, np.int64), group=group)
+        pipe = parallel.ShardPipeline(cfg, x, in_offsets, np.full(nblocks, n, np.int64), group=group,
+                                      decode_options=dopt)
         shard_bytes = nblocks * n * 2
 
     # correctness gate before timing: round trip must be exact

@@ -376,6 +376,8 @@ __device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t sel, uint32_t
   return __builtin_amdgcn_perm(v, v, sel);
 }
 
+// BS: the block size of the fast lanes' unrolled decode (16..128); BS = 0 is
+// any other block size (the run-time p.bs), decoded by general lanes only.
 template <uint32_t CS, uint32_t BS, bool SH>
 __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t stage[kStageWords + kStagePad];
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
   const uint32_t lane = __lane_id();
   const uint32_t be = p.be, ulsb = p.ulsb;
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;  // byte-swap each half
-  const uint32_t chunk_len = CS * BS;
+  const uint32_t chunk_len = CS * (BS ? BS : p.bs);
   const uint64_t total_tiles = *p.n_tiles;
 
   const bool timing = (p.dbg & RPP_TEST_PHASE_TIMERS) && tid < 64;
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
     // ---- fast lanes: Rice, a full sub-block, staged, every code <= 32 bits ----
     uint32_t hdr = 0;
     if (active) hdr = rd.peek32(start) & 15u;
-    bool fast = active && hdr != 0 && hdr != 15 && n == BS && (end >> 5) + 1 < w0 + nst &&
+    bool fast = BS != 0 && active && hdr != 0 && hdr != 15 && n == BS && (end >> 5) + 1 < w0 + nst &&
                 !(p.dbg & RPP_TEST_NO_FAST_LANES);
     // pairs share one store path (the shuffle outside any condition: a
     // short-circuit && would run it on the fast lanes only)
@@ -469,7 +471,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
       const int pf = __shfl_xor((int)fast, 1);
       fast = fast && pf;
     }
-    uint32_t r[BS / 2];
+    uint32_t r[BS ? BS / 2 : 1];
     uint32_t agg = 0;
     if (fast) {
       const uint32_t fs = hdr - 1;
@@ -600,7 +602,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
     if (active && !fast) decode_general<true>(rd, start, n, carry, out + cbase + comp, CS, be, ulsb);
     // fast lanes: their BS samples, in output order (lane k's BS samples are
     // output samples [k BS, (k+1) BS) of the tile for either CS)
-    uint32_t o32[CS == 1 ? 1 : BS / 2];  // (cs 1: the words are r itself)
+    uint32_t o32[CS == 1 || !BS ? 1 : BS / 2];  // (cs 1: the words are r itself)
     if (fast) {
       const uint32_t c2 = carry * 0x10001u;
 #pragma unroll
@@ -629,13 +631,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
       if constexpr (CS == 1) return r[i];
       else return o32[i];
     };
-    if (p.dbg & 2) {
-      if (fast)
-        for (uint32_t i = 0; i < BS / 2; ++i) {
-          out[(size_t)k * BS + 2 * i] = (uint16_t)word(i);
-          out[(size_t)k * BS + 2 * i + 1] = (uint16_t)(word(i) >> 16);
-        }
-    } else if constexpr (BS >= 64) {
+    if constexpr (BS >= 64) {
       // Through LDS, so that every store instruction writes whole 128-byte
       // lines: each wave puts 128 bytes of each lane in a row of its own
       // quarter of the stage (rows padded to 144 bytes), then eight lanes
@@ -988,7 +984,7 @@ ExtractKernel extract_kernel_for(uint32_t bs) {
     case 32: return rpp_extract_kernel<CS, 32, SH>;
     case 64: return rpp_extract_kernel<CS, 64, SH>;
     case 128: return rpp_extract_kernel<CS, 128, SH>;
-    default: return nullptr;
+    default: return rpp_extract_kernel<CS, 0, SH>;  // (general lanes: bs 256 / 512 / not a power of two)
   }
 }
 
@@ -1051,7 +1047,12 @@ class SideFork {
   bool forked_ = false;
 };
 
-bool extract_bs(uint32_t bs) { return bs == 16 || bs == 32 || bs == 64 || bs == 128; }
+// Block sizes the segmented decode takes: every bs >= 16 (16/32/64/128 with
+// unrolled fast lanes in the extraction, the others -- 256, 512, odd sizes --
+// with its exact general lanes).  Below 16 samples a sub-block codes to too
+// few bits for the units' position lists (one entry per 32 bits): such
+// streams are decoded one wave per stream.
+bool extract_bs(uint32_t bs) { return bs >= 16; }
 
 uint32_t path_of(const rpp_decode_options* opt) { return opt ? opt->path : RPP_DECODE_AUTO; }
 

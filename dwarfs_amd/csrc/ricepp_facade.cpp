@@ -48,6 +48,7 @@ rpp_config to_rpp(codec_config const& c) {
     case RPP_TRUNCATED_INPUT: throw std::out_of_range("bitstream_reader::read_packet");
     case RPP_INVALID_ARGUMENT: throw std::invalid_argument("ricepp_amd: invalid argument");
     case RPP_OUTPUT_TOO_SMALL: throw std::length_error("ricepp_amd: output buffer too small");
+    case RPP_INTERNAL_ERROR: throw std::runtime_error("ricepp_amd: internal error (device consistency bound)");
     default: throw std::runtime_error("ricepp_amd: HIP error");
   }
 }
@@ -80,9 +81,15 @@ class device_guard {
   int prev_ = 0;
 };
 
-// A private stream plus grow-only device and pinned host buffers, bound to
-// one device.  Contexts are pooled and never freed while the process runs
-// (no hipFree, which would wait for the whole device, on any call path).
+// A private stream plus device and pinned host buffers, bound to one device.
+// Device buffers come from the stream-ordered allocator (hipMallocAsync /
+// hipFreeAsync on the context's stream), so growing one never synchronises the
+// device.  Pinned buffers are mapped into the device's address space (the
+// encoder packs its output straight into them) and grow geometrically; a
+// context going back to the pool drops pinned buffers above kPinnedKeep, so a
+// burst of huge batches does not keep GiBs of host memory pinned.
+constexpr size_t kPinnedKeep = size_t{64} << 20;
+
 class device_ctx {
  public:
   explicit device_ctx(int dev) : dev_{dev} {
@@ -95,27 +102,53 @@ class device_ctx {
 
   int device() const { return dev_; }
   hipStream_t stream() const { return stream_; }
-  uint8_t* dev(size_t bytes) { return grow(dbuf_, dcap_, bytes, false); }
-  uint8_t* workspace(size_t bytes) { return grow(wbuf_, wcap_, bytes, false); }
-  uint8_t* pin_in(size_t bytes) { return grow(hin_, hin_cap_, bytes, true); }
-  uint8_t* pin_out(size_t bytes) { return grow(hout_, hout_cap_, bytes, true); }
+  uint8_t* dev(size_t bytes) { return grow_dev(dbuf_, dcap_, bytes); }
+  uint8_t* workspace(size_t bytes) { return grow_dev(wbuf_, wcap_, bytes); }
+  uint8_t* pin_in(size_t bytes) { return grow_pinned(hin_, hin_cap_, bytes); }
+  uint8_t* pin_out(size_t bytes) { return grow_pinned(hout_, hout_cap_, bytes); }
+  // the device-side address of a pinned buffer
+  uint8_t* device_view(uint8_t* pinned) {
+    void* d = nullptr;
+    hip_check(hipHostGetDevicePointer(&d, pinned, 0), "hipHostGetDevicePointer");
+    return static_cast<uint8_t*>(d);
+  }
   void sync() { hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
+  // on release (the stream is idle: every batch ends with a sync)
+  void trim() {
+    for (auto* q : {&hin_, &hout_}) {
+      size_t& cap = q == &hin_ ? hin_cap_ : hout_cap_;
+      if (cap > kPinnedKeep) {
+        (void)hipHostFree(*q);
+        *q = nullptr;
+        cap = 0;
+      }
+    }
+  }
 
  private:
-  // geometric growth, so that a warm context no longer allocates
-  static uint8_t* grow(uint8_t*& p, size_t& cap, size_t bytes, bool pinned) {
+  uint8_t* grow_dev(uint8_t*& p, size_t& cap, size_t bytes) {
     if (bytes <= cap && p) return p;
     size_t n = cap ? cap : size_t{1} << 20;
     while (n < bytes) n *= 2;
-    if (p) {
-      if (pinned) (void)hipHostFree(p);
-      else (void)hipFree(p);
-      p = nullptr;
-      cap = 0;
-    }
+    if (p) (void)hipFreeAsync(p, stream_);  // (stream-ordered: after the work that used it)
+    p = nullptr;
+    cap = 0;
     void* q = nullptr;
-    if (pinned) hip_check(hipHostMalloc(&q, n, hipHostMallocDefault), "hipHostMalloc");
-    else hip_check(hipMalloc(&q, n), "hipMalloc");
+    hip_check(hipMallocAsync(&q, n, stream_), "hipMallocAsync");
+    p = static_cast<uint8_t*>(q);
+    cap = n;
+    return p;
+  }
+  // (pinned buffers only grow between batches: the stream is idle then)
+  static uint8_t* grow_pinned(uint8_t*& p, size_t& cap, size_t bytes) {
+    if (bytes <= cap && p) return p;
+    size_t n = cap ? cap : size_t{1} << 20;
+    while (n < bytes) n *= 2;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    void* q = nullptr;
+    hip_check(hipHostMalloc(&q, n, hipHostMallocMapped), "hipHostMalloc");
     p = static_cast<uint8_t*>(q);
     cap = n;
     return p;
@@ -154,6 +187,7 @@ class ctx_pool {
     return new device_ctx(dev);
   }
   void release(device_ctx* c) {
+    c->trim();
     std::lock_guard<std::mutex> lk(mu_);
     free_[c->device()].push_back(c);
   }
@@ -169,6 +203,7 @@ class ctx_lease {
   ~ctx_lease() { ctx_pool::get().release(c_); }
   ctx_lease(ctx_lease const&) = delete;
   ctx_lease& operator=(ctx_lease const&) = delete;
+  device_ctx& operator*() const { return *c_; }
   device_ctx* operator->() const { return c_; }
 
  private:
@@ -183,7 +218,9 @@ class ctx_lease {
 // The first waiting caller that finds a free launch slot takes everything
 // queued (up to the batch caps) and drives the launch; every caller does its
 // own host copies, in parallel.  The leader only touches a request through
-// the batch's counters once the request may have returned.
+// the batch's counters once the request may have returned.  Up to kMaxActive
+// batches of one queue are in flight at once, each on its own pooled context
+// (stream), and each costs one host synchronisation.
 enum req_state { QUEUED, TAKEN, ASSIGNED, STAGED, RESULT, DONE };
 
 struct batch_counts {
@@ -212,8 +249,12 @@ struct request {
 };
 
 constexpr size_t kMaxBatchBlocks = 8192;
-constexpr size_t kMaxBatchBytes = size_t{512} << 20;  // input bytes per launch
-constexpr int kMaxActive = 4;                         // launches in flight per queue
+constexpr size_t kMaxBatchBytes = size_t{512} << 20;  // input + output bytes per launch
+// launches in flight per queue: HIP maps a process's streams onto
+// GPU_MAX_HW_QUEUES hardware queues (4 by default), so more concurrent launches
+// only queue behind each other on the device (measured: 16 in flight took the
+// 64-thread decode from 4.5 to 1.4 GiB/s); fewer, bigger batches win
+constexpr int kMaxActive = 4;
 
 class batch_queue {
  public:
@@ -240,6 +281,10 @@ class batch_queue {
   }
 
  private:
+  // bytes a request moves through a launch (input, and output capacity)
+  size_t footprint(request const* q) const {
+    return q->in_bytes + (encode_ ? rpp_worst_case_bytes(&cfg_, q->n_samples) : q->out_cap);
+  }
   void copy_in(std::unique_lock<std::mutex>& lk, request& r) {
     lk.unlock();
     if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
@@ -258,14 +303,16 @@ class batch_queue {
 
   // Takes a batch from the queue and drives it (lk held on entry and exit).
   // `self` is the leader's own request, which may or may not be in the batch.
+  // Every exit path publishes a result to every request of the batch, waits
+  // until all of them are DONE, and gives the launch slot back.
   void lead(std::unique_lock<std::mutex>& lk, request& self) {
     std::vector<request*> b;
     size_t bytes = 0;
     while (!pending_.empty() && b.size() < kMaxBatchBlocks &&
-           (b.empty() || bytes + pending_.front()->in_bytes <= kMaxBatchBytes)) {
+           (b.empty() || bytes + footprint(pending_.front()) <= kMaxBatchBytes)) {
       request* q = pending_.front();
       pending_.pop_front();
-      bytes += q->in_bytes;
+      bytes += footprint(q);
       q->state = TAKEN;
       b.push_back(q);
     }
@@ -276,33 +323,34 @@ class batch_queue {
     // another caller may lead the next batch meanwhile
     if (!pending_.empty() && active_ < kMaxActive) pending_.front()->cv.notify_one();
     lk.unlock();
-    {
-      ctx_lease ctx{dev_};
-      try {
-        device_guard g{dev_};
-        if (encode_) launch_encode(lk, b, self, *ctx.operator->());
-        else launch_decode(lk, b, self, *ctx.operator->());
-      } catch (std::exception const& e) {
-        lk.lock();
-        // requests still waiting for their slot: nothing to copy in
-        for (request* q : b)
-          if (q->state == TAKEN) {
-            q->state = STAGED;
-            --counts.to_stage;
-          }
-        counts.cv.wait(lk, [&] { return counts.to_stage == 0; });
-        for (request* q : b) {
-          q->status = RPP_HIP_ERROR;
-          q->error = e.what();
-          q->result_bytes = 0;
-          q->state = RESULT;
-          q->cv.notify_one();
-        }
-        lk.unlock();
-      }
+    try {
+      ctx_lease ctx{dev_};  // (may throw: no request has a slot yet)
+      device_guard g{dev_};
+      if (encode_) launch_encode(lk, b, self, *ctx);
+      else launch_decode(lk, b, self, *ctx);
       lk.lock();
       // the leader copies its own result out, then waits for the others
-      // before the staging buffers go back to the pool
+      // before the pinned buffers go back to the pool (with the lease)
+      if (self.state == RESULT && self.counts == &counts) copy_out(lk, self);
+      counts.cv.wait(lk, [&] { return counts.to_finish == 0; });
+      lk.unlock();
+    } catch (std::exception const& e) {
+      // thrown before stage_in handed out slots or after every request was
+      // STAGED (launch_* only throws outside stage_in): no caller is copying
+      lk.lock();
+      for (request* q : b)
+        if (q->state == TAKEN) {
+          q->state = STAGED;
+          --counts.to_stage;
+        }
+      for (request* q : b) {
+        if (q->state == RESULT || q->state == DONE) continue;
+        q->status = RPP_HIP_ERROR;
+        q->error = e.what();
+        q->result_bytes = 0;
+        q->state = RESULT;
+        if (q != &self) q->cv.notify_one();
+      }
       if (self.state == RESULT && self.counts == &counts) copy_out(lk, self);
       counts.cv.wait(lk, [&] { return counts.to_finish == 0; });
       lk.unlock();
@@ -329,93 +377,99 @@ class batch_queue {
   }
 
   // Publishes the results (lk not held on entry or exit).
-  void publish(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b) {
+  void publish(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self) {
     lk.lock();
     for (request* q : b) {
       q->state = RESULT;
-      q->cv.notify_one();
+      if (q != &self) q->cv.notify_one();
     }
     lk.unlock();
   }
 
+  // One synchronisation per batch: the packed encoded bytes go straight from
+  // the pack kernel into mapped pinned memory, the sizes and statuses follow
+  // in one small copy.
   void launch_encode(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self,
                      device_ctx& ctx) {
     const size_t nb = b.size();
     std::vector<size_t> in_off(nb), out_off(nb);
     size_t in_total = 0, out_total = 0;
+    uint64_t total_samples = 0, max_samples = 0;
     for (size_t i = 0; i < nb; ++i) {
       in_off[i] = in_total;
       in_total += align16(b[i]->in_bytes);
       out_off[i] = out_total;
       out_total += align16(rpp_worst_case_bytes(&cfg_, b[i]->n_samples)) + 16;
+      total_samples += b[i]->n_samples;
+      max_samples = std::max<uint64_t>(max_samples, b[i]->n_samples);
     }
-    // device: [in][out slots][packed][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status]
-    const size_t a_off = in_total + 2 * out_total;
-    const size_t arr_bytes = (5 * nb + 1) * 8 + nb * 4;
-    uint8_t* d = ctx.dev(a_off + arr_bytes + 64);
-    uint8_t* pin = ctx.pin_in(in_total + arr_bytes + 64);
+    // device: [in][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status][out slots]
+    // pinned in: [in][u64 in_off | n | out_off]   (one H2D copy)
+    // pinned out: [packed bytes][u64 out_bytes | dst_off | total][i32 status]
+    const size_t arr = (6 * nb + 1) * 8 + align16(nb * 4);
+    uint8_t* d = ctx.dev(in_total + arr + out_total + 64);
+    uint8_t* pin = ctx.pin_in(in_total + 3 * nb * 8 + 64);
+    uint8_t* pout = ctx.pin_out(out_total + arr + 64);
     auto* h64 = reinterpret_cast<uint64_t*>(pin + in_total);
     for (size_t i = 0; i < nb; ++i) {
       h64[i] = in_off[i] / 2;
       h64[nb + i] = b[i]->n_samples;
       h64[2 * nb + i] = out_off[i];
     }
-    stage_in(lk, b, self, pin, in_off);
-    auto* d64 = reinterpret_cast<uint64_t*>(d + a_off);
-    auto* dst = reinterpret_cast<int32_t*>(d + a_off + (5 * nb + 1) * 8);
-    hipStream_t s = ctx.stream();
-    if (in_total) hip_check(hipMemcpyAsync(d, pin, in_total, hipMemcpyHostToDevice, s), "H2D encode input");
-    hip_check(hipMemcpyAsync(d64, h64, 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode params");
-    // long blocks (16 MiB DwarFS blocks) are encoded by several waves
-    uint64_t total_samples = 0, max_samples = 0;
-    for (request* q : b) {
-      total_samples += q->n_samples;
-      max_samples = std::max<uint64_t>(max_samples, q->n_samples);
-    }
     const uint64_t ws_bytes = rpp_encode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
+    uint8_t* pout_dev = ctx.device_view(pout);
+    stage_in(lk, b, self, pin, in_off);
+    auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
+    auto* dst = reinterpret_cast<int32_t*>(d + in_total + (6 * nb + 1) * 8);
+    uint8_t* dslots = d + in_total + arr;
+    hipStream_t s = ctx.stream();
+    hip_check(hipMemcpyAsync(d, pin, in_total + 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode input");
     int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
-                                 d + in_total, d64 + 2 * nb, d64 + 3 * nb, dst, total_samples, max_samples, ws,
-                                 ws_bytes, s);
+                                 dslots, d64 + 2 * nb, d64 + 3 * nb, dst, total_samples, max_samples, ws, ws_bytes, s);
     if (st != RPP_OK) throw_status(st);
-    st = rpp_pack_batch(d + in_total, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb),
-                        d + in_total + out_total, d64 + 4 * nb, d64 + 5 * nb, s);
+    st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
+                        d64 + 5 * nb, s);
     if (st != RPP_OK) throw_status(st);
+    hip_check(hipMemcpyAsync(pout + out_total, d64 + 3 * nb, arr - 3 * nb * 8, hipMemcpyDeviceToHost, s),
+              "D2H encode sizes");
     g_enc_launches.fetch_add(1, std::memory_order_relaxed);
     g_enc_blocks.fetch_add(nb, std::memory_order_relaxed);
-    // sizes, packed offsets, total and status back, then the packed bytes
-    hip_check(hipMemcpyAsync(h64 + 3 * nb, d64 + 3 * nb, (2 * nb + 1) * 8 + nb * 4, hipMemcpyDeviceToHost, s),
-              "D2H encode sizes");
     ctx.sync();
-    const uint64_t total = h64[5 * nb];
-    uint8_t* pout = ctx.pin_out(total + 16);
-    if (total) hip_check(hipMemcpyAsync(pout, d + in_total + out_total, total, hipMemcpyDeviceToHost, s), "D2H encoded");
-    ctx.sync();
-    auto const* hst = reinterpret_cast<int32_t const*>(h64 + 5 * nb + 1);
+    auto const* r64 = reinterpret_cast<uint64_t const*>(pout + out_total);  // out_bytes | dst_off | total
+    auto const* hst = reinterpret_cast<int32_t const*>(pout + out_total + (3 * nb + 1) * 8);
     for (size_t i = 0; i < nb; ++i) {
       b[i]->status = hst[i];
-      b[i]->result_bytes = hst[i] == RPP_OK ? h64[3 * nb + i] : 0;
-      b[i]->pin_out = pout + h64[4 * nb + i];
+      b[i]->result_bytes = hst[i] == RPP_OK ? r64[i] : 0;
+      b[i]->pin_out = pout + r64[nb + i];
       if (b[i]->status == RPP_OK && b[i]->result_bytes > b[i]->out_cap) b[i]->status = RPP_OUTPUT_TOO_SMALL;
     }
-    publish(lk, b);
+    publish(lk, b, self);
   }
 
+  // One synchronisation per batch: one H2D copy (streams and parameters),
+  // one D2H copy (statuses and samples).
   void launch_decode(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self,
                      device_ctx& ctx) {
     const size_t nb = b.size();
     std::vector<size_t> in_off(nb), out_off(nb);
     size_t in_total = 0, out_total = 0;
+    uint64_t total_samples = 0, max_samples = 0;
     for (size_t i = 0; i < nb; ++i) {
       in_off[i] = in_total;
       in_total += align16(b[i]->in_bytes);
       out_off[i] = out_total;
       out_total += align16(b[i]->out_cap);
+      total_samples += b[i]->n_samples;
+      max_samples = std::max<uint64_t>(max_samples, b[i]->n_samples);
     }
-    // device: [in][out][u64 in_off | in_bytes | out_off | n][i32 status]
-    const size_t a_off = in_total + out_total;
-    uint8_t* d = ctx.dev(a_off + 4 * nb * 8 + nb * 4 + 64);
+    // device: [in][u64 in_off | in_bytes | out_off | n][i32 status][out samples]
+    // pinned in: [in][u64 in_off | in_bytes | out_off | n]   (one H2D copy)
+    // pinned out: [i32 status][out samples]                  (one D2H copy)
+    const size_t st_bytes = align16(nb * 4);
+    uint8_t* d = ctx.dev(in_total + 4 * nb * 8 + st_bytes + out_total + 64);
     uint8_t* pin = ctx.pin_in(in_total + 4 * nb * 8 + 64);
+    uint8_t* pout = ctx.pin_out(st_bytes + out_total + 64);
     auto* h64 = reinterpret_cast<uint64_t*>(pin + in_total);
     for (size_t i = 0; i < nb; ++i) {
       h64[i] = in_off[i];
@@ -423,37 +477,29 @@ class batch_queue {
       h64[2 * nb + i] = out_off[i] / 2;
       h64[3 * nb + i] = b[i]->n_samples;
     }
-    stage_in(lk, b, self, pin, in_off);
-    auto* d64 = reinterpret_cast<uint64_t*>(d + a_off);
-    auto* dst = reinterpret_cast<int32_t*>(d + a_off + 4 * nb * 8);
-    hipStream_t s = ctx.stream();
-    if (in_total) hip_check(hipMemcpyAsync(d, pin, in_total, hipMemcpyHostToDevice, s), "H2D decode input");
-    hip_check(hipMemcpyAsync(d64, h64, 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode params");
     // long blocks (16 MiB DwarFS blocks) are parsed in segments by several waves
-    uint64_t total_samples = 0, max_samples = 0;
-    for (request* q : b) {
-      total_samples += q->n_samples;
-      max_samples = std::max<uint64_t>(max_samples, q->n_samples);
-    }
     const uint64_t ws_bytes = rpp_decode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
-    int st = rpp_decode_batch_ws(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb),
-                                 reinterpret_cast<uint16_t*>(d + in_total), d64 + 2 * nb, d64 + 3 * nb, dst,
-                                 total_samples, max_samples, ws, ws_bytes, s);
+    stage_in(lk, b, self, pin, in_off);
+    auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
+    auto* dst = reinterpret_cast<int32_t*>(d + in_total + 4 * nb * 8);
+    uint8_t* dout = d + in_total + 4 * nb * 8 + st_bytes;
+    hipStream_t s = ctx.stream();
+    hip_check(hipMemcpyAsync(d, pin, in_total + 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode input");
+    int st = rpp_decode_batch_ws(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb), reinterpret_cast<uint16_t*>(dout),
+                                 d64 + 2 * nb, d64 + 3 * nb, dst, total_samples, max_samples, ws, ws_bytes, s);
     if (st != RPP_OK) throw_status(st);
+    hip_check(hipMemcpyAsync(pout, dst, st_bytes + out_total, hipMemcpyDeviceToHost, s), "D2H decoded");
     g_dec_launches.fetch_add(1, std::memory_order_relaxed);
     g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);
-    uint8_t* pout = ctx.pin_out(out_total + nb * 4 + 64);
-    if (out_total) hip_check(hipMemcpyAsync(pout, d + in_total, out_total, hipMemcpyDeviceToHost, s), "D2H decoded");
-    auto* hst = reinterpret_cast<int32_t*>(pout + out_total);
-    hip_check(hipMemcpyAsync(hst, dst, nb * 4, hipMemcpyDeviceToHost, s), "D2H decode status");
     ctx.sync();
+    auto const* hst = reinterpret_cast<int32_t const*>(pout);
     for (size_t i = 0; i < nb; ++i) {
       b[i]->status = hst[i];
       b[i]->result_bytes = hst[i] == RPP_OK ? b[i]->out_cap : 0;
-      b[i]->pin_out = pout + out_off[i];
+      b[i]->pin_out = pout + st_bytes + out_off[i];
     }
-    publish(lk, b);
+    publish(lk, b, self);
   }
 
   int dev_;

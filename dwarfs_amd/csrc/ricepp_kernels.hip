@@ -1281,6 +1281,13 @@ __device__ __forceinline__ uint32_t stream_word(const uint8_t* in, uint32_t nbyt
 template <uint32_t CS, bool SH>
 __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
+  // ---- this wave's stream, and whether the workgroup has anything to do (the
+  //      fallback launch skips most streams: leave before the table copy) ----
+  const uint32_t b = blockIdx.x * p.waves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  bool mine = b < p.nblocks;
+  if (mine && p.only_fallback) mine = p.status[b] == rpp_internal::kSegFallback;
+  if (mine && p.units && p.units[b] > 1) mine = false;
+  if (!__syncthreads_or(mine)) return;
   // ---- the transfer tables, one copy per workgroup ----
   {
     const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
@@ -1300,10 +1307,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
   const uint32_t selpack = be ? 0x04050001u : 0x05040100u;  // v_perm(hi, lo): pack two samples (+ swap)
   const uint32_t lane24 = kSegBits * lane;
-  const uint32_t b = blockIdx.x * p.waves + wv;
-  if (b >= p.nblocks) return;  // no barrier below this point
-  if (p.only_fallback && p.status[b] != rpp_internal::kSegFallback) return;
-  if (p.units && p.units[b] > 1) return;
+  if (!mine) return;  // no barrier below this point
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
   unsigned long long tprev_;
@@ -2525,7 +2529,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       // ends (the ragged last chunk is re-parsed by rpp_seg_tail_kernel)
       const uint32_t nsb = multi ? 0xFFFFFFFFu : nchunks * CS;
       const bool fast_bs = bs == 2 * kWave || bs == 16 || bs == 32 || bs == 64;
-      const uint32_t nsb_fast = multi ? 0xFFFFFFFFu : fast_bs ? (N / chunk_len) * CS : 0u;
+      // (a unit runs the window loop for any bs <= 128: it only needs the
+      // sub-block's end; longer sub-blocks never end in a 1536-bit window)
+      const uint32_t nsb_fast = multi ? (bs <= 2 * kWave ? 0xFFFFFFFFu : 0u) : fast_bs ? (N / chunk_len) * CS : 0u;
       ScanRegs sreg;
 
       uint32_t s = 0;

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native as N
-from .codec import CodecConfig, _check, _raise_status, decode_workspace, encode_workspace
+from .codec import CodecConfig, DecodeOptions, _check, _raise_status, decode_workspace, encode_workspace
 
 
 def partition_blocks(block_bytes: Sequence[int], world: int) -> List[Tuple[int, int]]:
@@ -126,8 +126,11 @@ class ShardPipeline:
     array preallocated so one step is encode, size all-gather + image-offset
     scan, decode, and no host-device synchronisation."""
 
-    def __init__(self, config: CodecConfig, samples: torch.Tensor, in_offsets, n_samples, group=None):
+    def __init__(self, config: CodecConfig, samples: torch.Tensor, in_offsets, n_samples, group=None,
+                 decode_options: Optional[DecodeOptions] = None):
         self.cfg = _check(config)
+        self.decode_options = decode_options or DecodeOptions()
+        self._dopt = self.decode_options.native()
         self.config = config
         self.group = group
         self.samples = samples
@@ -154,7 +157,8 @@ class ShardPipeline:
         self.dec_status = torch.zeros(self.nblocks, dtype=torch.int32, device=dev)
         self.total_samples = int(n_samples.sum())
         self.max_samples = int(n_samples.max()) if self.nblocks else 0
-        self.workspace = decode_workspace(config, self.total_samples, self.nblocks, dev, self.max_samples)
+        self.workspace = decode_workspace(config, self.total_samples, self.nblocks, dev, self.max_samples,
+                                          self.decode_options)
         self.enc_workspace = encode_workspace(config, self.total_samples, self.max_samples, self.nblocks, dev)
         self.all_sizes: Optional[torch.Tensor] = None
         self.image_offsets: Optional[torch.Tensor] = None
@@ -179,12 +183,12 @@ class ShardPipeline:
             self.enc_workspace.numel(), self._stream()))
 
     def decode(self) -> None:
-        _raise_status(N.lib().rpp_decode_batch_ws(
+        _raise_status(N.lib().rpp_decode_batch_ex(
             C.byref(self.cfg), C.c_void_p(self.data.data_ptr()), C.c_void_p(self.d_out_off.data_ptr()),
             C.c_void_p(self.sizes.data_ptr()), self.nblocks, C.c_void_p(self.decoded.data_ptr()),
             C.c_void_p(self.d_dec_off.data_ptr()), C.c_void_p(self.d_n.data_ptr()),
             C.c_void_p(self.dec_status.data_ptr()), self.total_samples, self.max_samples,
-            C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), self._stream()))
+            C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), C.byref(self._dopt), self._stream()))
 
     def gather(self) -> None:
         self.all_sizes = self.size_gather(self.sizes)

@@ -325,7 +325,8 @@ int bench(int argc, char** argv) {
       for (auto& th : pool) th.join();
       return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     };
-    run(true);  // warm the contexts
+    run(true);  // warm the contexts (both directions: decode grows their buffers differently)
+    run(false);
     auto s0 = ricepp_amd::get_facade_stats();
     double te = run(true);
     auto s1 = ricepp_amd::get_facade_stats();

@@ -255,6 +255,9 @@ def test_stalled_lookback_reports_internal_error():
     assert np.array_equal(dec[ns[0]:ns[0] + ns[1]], blocks[1])
     with pytest.raises(codec.CodecError, match="INTERNAL_ERROR"):
         codec._raise_status(int(st[0]))
+    diag = (C.c_ulonglong * 8)()
+    N.lib().rpp_diag_read(diag, 1)  # the stalled look-backs were counted; clear for later tests
+    assert diag[6] > 0
     # without the fault the same call is exact
     dec, st = _ws_decode(cfg, torch.from_numpy(buf).to(DEV), offs, [len(s) for s in streams], ns, sum(ns), max(ns),
                          codec.DecodeOptions(path="segmented", seg_log2=12))

@@ -278,7 +278,7 @@ def test_corrupt_streams_match_oracle(bs, cs, dec=None):
             assert np.array_equal(outn[i * n:(i + 1) * n], want), i
 
 
-def _full_size(kind, nblocks=4096, n=32768, bs=128, cs=1, nthreads=8):
+def _full_size(kind, nblocks=4096, n=32768, bs=128, cs=1, nthreads=8, dec=None):
     rng = np.random.default_rng(42)
     if kind == "poisson":
         x = datagen.poisson_data(rng, nblocks * n)
@@ -301,7 +301,7 @@ def _full_size(kind, nblocks=4096, n=32768, bs=128, cs=1, nthreads=8):
         a = data[enc.offsets[i]:enc.offsets[i] + sizes[i]]
         b = ob[int(oo[i]):int(oo[i]) + int(osz[i])]
         assert np.array_equal(a, b), f"block {i} differs"
-    out, st = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, [n] * nblocks)
+    out, st = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, [n] * nblocks, options=dec)
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
     assert torch.equal(out[: nblocks * n], d), "round trip mismatch"
@@ -495,6 +495,8 @@ def test_segmented_decode_config_matrix(bs, cs, seg_log2):
     rng = np.random.default_rng(9000 + 100 * seg_log2 + bs + cs)
     sizes = [rng.integers(1, 400) * cs, 40000, 70001, 123457, 5000, 31, 65536 + 3, 90000, 200000]
     codec.segmented_decode_stats(reset=True)
+    diag = (__import__("ctypes").c_ulonglong * 8)()
+    __import__("dwarfs_amd._native", fromlist=["lib"]).lib().rpp_diag_read(diag, 1)  # (clear earlier tests' counts)
     for be, ulsb in ((True, 0), (False, 3)):
         cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
         blocks = _kind_blocks(rng, sizes, cs, ulsb, be)
@@ -502,7 +504,6 @@ def test_segmented_decode_config_matrix(bs, cs, seg_log2):
         _decode_oracle_streams(cfg, blocks, ragged=True, dec=seg(seg_log2))
     stats = codec.segmented_decode_stats(reset=True)
     assert stats["met"] > 0, stats  # the units were split and stitched
-    diag = (__import__("ctypes").c_ulonglong * 8)()
     __import__("dwarfs_amd._native", fromlist=["lib"]).lib().rpp_diag_read(diag, 1)
     assert diag[6] == 0, "an extraction tile waited for a predecessor that never published"
     if seg_log2 == 10:
@@ -541,3 +542,33 @@ def test_segmented_decode_of_a_64mib_stream():
     codec.segmented_decode_stats(reset=True)
     run_batch(codec.CodecConfig(128, 2, "little", 1), [x])
     assert codec.segmented_decode_stats(reset=True)["met"] > 0
+
+
+@pytest.mark.parametrize("bs", [17, 99, 200, 256, 512])
+@pytest.mark.parametrize("cs", [1, 2])
+def test_segmented_decode_other_block_sizes(bs, cs):
+    """The segmented decode for block sizes without unrolled fast lanes (256, 512 and sizes that are not a
+    power of two, all allowed by ricepp:block_size, src/compression/ricepp.cpp:284-286): the units parse
+    them, the extraction decodes them with its exact general lanes; every data kind, both byte orders."""
+    rng = np.random.default_rng(31000 + bs + cs)
+    sizes = [rng.integers(1, 400) * cs, 40000, 70001, 123457, 5000, 65536 + 3, 200000]
+    codec.segmented_decode_stats(reset=True)
+    for be, ulsb in ((True, 0), (False, 2)):
+        cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
+        blocks = _kind_blocks(rng, sizes, cs, ulsb, be)
+        for log2 in (12, 15):
+            run_batch(cfg, blocks, dec=seg(log2))
+        _decode_oracle_streams(cfg, blocks, ragged=True, dec=seg(13))
+    assert codec.segmented_decode_stats(reset=True)["met"] > 0
+
+
+def test_segmented_decode_default_16mib_bs512_block():
+    """A 16 MiB DwarFS block written with ricepp:block_size=512 is decoded segmented by default (not by one
+    wave), bit-exact, in a batch with short blocks."""
+    rng = np.random.default_rng(512)
+    blocks = [datagen.poisson_data(rng, 8 << 20, lam=900.0)] + [datagen.poisson_data(rng, int(n))
+                                                               for n in rng.integers(1, 30000, 4)]
+    codec.segmented_decode_stats(reset=True)
+    run_batch(codec.CodecConfig(512, 1, "big", 0), blocks)
+    st = codec.segmented_decode_stats(reset=True)
+    assert st["met"] > 0 and st["fallback"] == 0, st
