@@ -799,6 +799,14 @@ __global__ void rpp_seg_hit_kernel(SegArgs a) {
 // there; else the unit is parsed again from the last overshoot header (a
 // rerun pass) and the stitch resumes there next time.  ulo = the list index
 // where the unit's exact positions start.
+// Before a rerun pass every later unit without a meeting whose predecessor
+// met its own is rerun as well, from that predecessor's last overshoot
+// header: exact once the units before are, so one rerun pass settles all of
+// a stream's isolated failed guesses.  (Rerunning also the units after a
+// failed one measured a cascade: a wrong chain that never meets the true one
+// hands its successor a wrong start, breaking a good guess in every pass.)  A rerun is taken as exact only when its
+// start is the (by then exact) previous unit's last overshoot header; else
+// its chain is stitched like a guessed one.
 __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
   using namespace rpp_internal;
   const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -819,25 +827,37 @@ __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
     j0 = 1;
   }
   enum { kOk, kEnd, kFail };
+  // unit u's class against the previous unit's chain, taken as exact
+  auto classify = [&](uint32_t u, uint32_t& lo, uint32_t& uovp) -> uint32_t {
+    const uint32_t prev = u - 1;
+    const uint32_t np = us_word(a, prev, kUsNovr);
+    const uint32_t h = a.uhit[u];
+    if ((us_word(a, u, kUsFlags) & kUfRerunDone) && np == kSegOvr &&
+        us_word(a, u, kUsStart) == a.sv.ovr[kSegOvr * prev + kSegOvr - 1]) {
+      lo = 0;  // parsed from the previous unit's last overshoot header
+      uovp = kSegOvr - 1;
+      return kOk;
+    }
+    if (h != kSegNone) {
+      lo = a.uhit[a.sv.units_max + u];
+      uovp = h;
+      return kOk;
+    }
+    lo = 0;
+    uovp = np;
+    return np < kSegOvr ? kEnd : kFail;
+  };
+  auto request = [&](uint32_t u) {
+    a.sv.ustate[kUsWords * u + kUsRerun] = a.sv.ovr[kSegOvr * (u - 1) + kSegOvr - 1];
+    atomicAdd(&g_seg_diag[a.sv.pass == 2 ? 2 : 1], 1ull);
+    if (us_word(a, u, kUsFlags) & kUfNoGuess) atomicAdd(&g_seg_diag[4], 1ull);
+  };
   for (; j0 < nu; j0 += 64) {
     const uint32_t j = j0 + lane;
     const bool in = j < nu;
     const uint32_t u = u0 + j, prev = u - 1;
     uint32_t cls = kOk, lo = 0, uovp = 0;
-    if (in) {
-      const uint32_t np = us_word(a, prev, kUsNovr);
-      const uint32_t h = a.uhit[u];
-      if (us_word(a, u, kUsFlags) & kUfRerunDone) {  // parsed from the previous unit's last overshoot header
-        lo = 0;
-        uovp = kSegOvr - 1;
-      } else if (h != kSegNone) {
-        lo = a.uhit[a.sv.units_max + u];
-        uovp = h;
-      } else {
-        cls = np < kSegOvr ? kEnd : kFail;
-        uovp = np;
-      }
-    }
+    if (in) cls = classify(u, lo, uovp);
     const uint64_t ev = __ballot(in && cls != kOk);
     const uint32_t e = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
     if (in && lane < e) {
@@ -849,10 +869,25 @@ __global__ __launch_bounds__(64) void rpp_seg_stitch_kernel(SegArgs a) {
     const uint32_t ce = __shfl((int)cls, (int)e);
     if (ce == kFail) {
       if (lane == e) {
-        a.sv.ustate[kUsWords * u + kUsRerun] = a.sv.ovr[kSegOvr * prev + kSegOvr - 1];
+        request(u);
         a.sv.sst[b] = j;
-        atomicAdd(&g_seg_diag[a.sv.pass == 2 ? 2 : 1], 1ull);
-        if (us_word(a, u, kUsFlags) & kUfNoGuess) atomicAdd(&g_seg_diag[4], 1ull);
+      }
+      // (a rerun pass next: the later units without a meeting whose
+      // predecessor met its own, speculatively -- a unit after another
+      // failed one keeps its chain, which may well be the true one)
+      if (a.sv.pass != 2) {
+        uint32_t pc = (uint32_t)__shfl_up((int)cls, 1);
+        if (in && lane > e && cls == kFail && pc == kOk) request(u);
+        uint32_t carry = (uint32_t)__shfl((int)cls, 63);
+        for (uint32_t k0 = j0 + 64; k0 < nu; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          uint32_t c2 = kEnd, lo2, uovp2;
+          if (k < nu) c2 = classify(u0 + k, lo2, uovp2);
+          pc = (uint32_t)__shfl_up((int)c2, 1);
+          if (lane == 0) pc = carry;
+          if (k < nu && c2 == kFail && pc == kOk) request(u0 + k);
+          carry = (uint32_t)__shfl((int)c2, 63);
+        }
       }
       return;
     }
@@ -1070,6 +1105,10 @@ uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t ma
   if (path != RPP_DECODE_SEGMENTED) {
     if (max_stream_samples < (1u << 18)) return 0;
     if (max_stream_samples * 1024 < total_samples) return 0;
+    // bs 256 / 512: a unit's guess parses lane by lane only (2-8 Kib
+    // sub-blocks), so units cost several times more; 1 MiB streams decode
+    // faster one wave each (16 x 1 MiB at bs 512: 3.8 ms fused, 21 ms split)
+    if (cfg->block_size > 128 && max_stream_samples < (1u << 21)) return 0;
   }
   // about 4096 units for the batch (8 bits per sample: Poisson-like data
   // compresses to 7-8), 2^18..2^23 bits (a unit's guess costs about as much
@@ -1224,6 +1263,10 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
   if ((st = rpp_exclusive_scan_u64(w.pl_cnt, U + 1, w.pl_base, s)) != RPP_OK) return st;
   if (hipMemsetAsync(w.ustate, 0xFF, U * rpp_internal::kUsWords * 4, s) != hipSuccess) return RPP_HIP_ERROR;
   const uint32_t gu = (uint32_t)((U + 255) / 256);
+  // few units: their first guesses by several waves each, before pass 0
+  if ((st = rpp_internal::launch_seg_guess(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, a.sv, s)) !=
+      RPP_OK)
+    return st;
   // pass 0: every unit; three rerun passes; a serial pass for what is left
   for (uint32_t pass : {0u, 1u, 1u, 1u, 2u}) {
     a.sv.pass = pass;  // (the stitch counts the reruns it asks this pass for)

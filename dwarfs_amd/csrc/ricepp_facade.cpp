@@ -56,6 +56,7 @@ rpp_config to_rpp(codec_config const& c) {
 size_t align16(size_t v) { return (v + 15) & ~size_t{15}; }
 
 std::atomic<uint64_t> g_enc_launches{0}, g_enc_blocks{0}, g_dec_launches{0}, g_dec_blocks{0}, g_ctx_created{0};
+std::atomic<uint32_t> g_ctx_faults{0};  // inject_context_failures
 
 int current_device() {
   int d = 0;
@@ -93,6 +94,8 @@ constexpr size_t kPinnedKeep = size_t{64} << 20;
 class device_ctx {
  public:
   explicit device_ctx(int dev) : dev_{dev} {
+    for (uint32_t n = g_ctx_faults.load(); n;)
+      if (g_ctx_faults.compare_exchange_weak(n, n - 1)) throw std::runtime_error("hipStreamCreate: injected failure");
     device_guard g{dev_};
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     g_ctx_created.fetch_add(1, std::memory_order_relaxed);
@@ -654,6 +657,8 @@ std::unique_ptr<decoder_interface<uint16_t>> create_decoder<uint16_t>(codec_conf
   if (rpp_check_config(&c) != RPP_OK) throw std::runtime_error("Unsupported configuration");
   return std::make_unique<decoder_impl>(c, current_device());
 }
+
+void inject_context_failures(uint32_t n) { g_ctx_faults.store(n); }
 
 facade_stats get_facade_stats() {
   return facade_stats{g_enc_launches.load(), g_enc_blocks.load(), g_dec_launches.load(), g_dec_blocks.load(),

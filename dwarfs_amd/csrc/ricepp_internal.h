@@ -32,7 +32,10 @@ constexpr int32_t kSegFallback = 0x7F5E0001;  // internal status: decode this st
 // per-unit state words (SegView::ustate[kUsWords u + i]): overshoot entries,
 // the chain's first header, a pending rerun's start, flags, positions listed
 constexpr uint32_t kUsWords = 8;
-enum : uint32_t { kUsNovr = 0, kUsStart = 1, kUsRerun = 2, kUsFlags = 3, kUsNpos = 4 };
+// kUsGuess: the unit's first guess when rpp_seg_guess_kernel searched it
+// (kSegNone: not searched; kSegNoGuess: searched, no candidate survived)
+enum : uint32_t { kUsNovr = 0, kUsStart = 1, kUsRerun = 2, kUsFlags = 3, kUsNpos = 4, kUsGuess = 5 };
+constexpr uint32_t kSegNoGuess = 0xFFFFFFFEu;
 enum : uint32_t { kUfRerunDone = 1, kUfNoGuess = 2, kUfTrunc = 4 };
 // per-stream flags (SegView::sflags)
 enum : uint32_t { kSfPastRegion = 1, kSfListFull = 2 };
@@ -78,6 +81,14 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
 // rpp_parse_kernel over units (SegView): the units of split streams, into
 // their position and overshoot lists (single-unit streams are left to the
 // fused kernel).
+// rpp_seg_guess_kernel: the first guesses of the units of split streams,
+// several waves per unit (for batches of few units, whose parse would leave
+// most wave slots idle); pass 0 of the parse then starts from them.  Returns
+// RPP_OK without launching anything when the batch has too many units.
+int launch_seg_guess(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                     const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples, const SegView& sv,
+                     hipStream_t stream);
+
 int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples,
                      const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,

@@ -981,7 +981,8 @@ constexpr uint32_t kDecMaxWaves = 16;            // waves per workgroup (one tab
 constexpr uint32_t kRingPad = 64;               // ring words 0..63 mirrored after the ring end
 constexpr uint32_t kListDump = 512;            // list slot written by masked-off lanes
 constexpr uint32_t kListWords = kListDump + 24;  // terminator positions of one sub-block (bs <= 512), dump pairs (MT <= 12)
-constexpr uint32_t kWaveLdsWords = kRingWords + kRingPad + kListWords;
+constexpr uint32_t kListLead = 4;  // words before a decode list: pair -1 = (0, 0), a_(-1) of the fast loop's deltas
+constexpr uint32_t kWaveLdsWords = kRingWords + kRingPad + kListLead + kListWords;
 constexpr uint32_t kTabBytes = kMapEntries * 16;
 
 __device__ __forceinline__ uint32_t wave_last(uint32_t v) { return readlane(v, kWave - 1); }
@@ -1094,6 +1095,9 @@ __device__ __forceinline__ uint32_t jshift(uint32_t x, uint32_t& keep) {
 #endif
 #ifndef RPP_PRIO_MID
 #define RPP_PRIO_MID 0  // diagnostics: drop it for the previous sub-block's stores inside the parse
+#endif
+#ifndef RPP_END_SCALAR
+#define RPP_END_SCALAR 0  // 1: fs 5-7 loop end by one packed readlane + scalar bit clearing (measured 245 vs 239 us, profiles/r03_decode_ab.jsonl)
 #endif
 #ifndef RPP_JACOBI
 #define RPP_JACOBI 0  // measured: rounds 4 / 6 / 8 = 286 / 267 / 265 us vs 262 us with the scan (bench decode)
@@ -1302,7 +1306,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   uint32_t ring_w = kTabBytes / 4 + wv * kWaveLdsWords;
   asm("" : "+s"(ring_w));
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + ring_w;
-  uint32_t* list = ring + kRingWords + kRingPad;  // terminator positions of the current sub-block
+  uint32_t* list = ring + kRingWords + kRingPad + kListLead;  // terminator positions of the current sub-block
+  if (lane < kListLead) list[(int)lane - (int)kListLead] = 0u;  // (never written again)
   const uint32_t bs = p.bs, be = p.be, ulsb = p.ulsb;
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
   const uint32_t selpack = be ? 0x04050001u : 0x05040100u;  // v_perm(hi, lo): pack two samples (+ swap)
@@ -1585,6 +1590,21 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         }
         const uint32_t excl = incl - cnt;
         RPP_TSTAMP(7);
+        // the next sub-block starts after code n-1's remainder: terminator
+        // n-1-excl (< MT) of the first lane whose inclusive count reaches n.
+        // (bit 63 set: a defined lane when no lane ends the sub-block; Pe is
+        // then unused)
+        const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
+        constexpr bool kEndScalar = RPP_END_SCALAR && !W32 && MT == 4;
+        if constexpr (kEndScalar) {
+          // that lane's mask and exclusive count in one readlane (24 + 8 bits:
+          // excl < n <= 128 there), its r-th set bit found by the scalar unit
+          const uint32_t x = readlane(tm | (excl << 24), (int)lz);
+          const uint32_t r = n - 1 - (x >> 24);
+          const uint32_t m0 = x & 0xFFFFFFu, m1 = m0 & (m0 - 1u), m2 = m1 & (m1 - 1u), m3 = m2 & (m2 - 1u);
+          const uint32_t m = r == 0 ? m0 : r == 1 ? m1 : r == 2 ? m2 : m3;
+          Pe = q + SB * lz + (uint32_t)__builtin_ctz(m | 0x80000000u) + k;
+        }
         // terminator positions t0 < t1 < ... in the segment (garbage past
         // cnt)
         uint32_t t[MT];
@@ -1593,26 +1613,22 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           t[j] = ffbl(tm);
           tm &= tm - 1;
         }
-        // the next sub-block starts after code n-1's remainder: terminator
-        // n-1-excl (< MT) of the first lane whose inclusive count reaches n
-        // (positions <= 23 packed in bytes and picked by one bit-field
-        // extract: a few vector ops rather than a chain of scalar ones,
-        // the scalar unit being shared by the CU's 16 waves)
-        const uint32_t r = n - 1 - excl;
-        uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
-        if constexpr (MT > 4) {
-          const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
-          tpk = r < 4 ? tpk : tpk1;
+        if constexpr (!kEndScalar) {
+          // (positions <= 23 packed in bytes and picked by one bit-field
+          // extract: a few vector ops rather than a chain of scalar ones)
+          const uint32_t r = n - 1 - excl;
+          uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
+          if constexpr (MT > 4) {
+            const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
+            tpk = r < 4 ? tpk : tpk1;
+          }
+          if constexpr (MT > 8) {
+            const uint32_t tpk2 = t[8] | (t[9] << 8) | ((t[10] | (t[11] << 8)) << 16);
+            tpk = r < 8 ? tpk : tpk2;
+          }
+          const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
+          Pe = q + SB * lz + readlane(tend, (int)lz) + k;
         }
-        if constexpr (MT > 8) {
-          const uint32_t tpk2 = t[8] | (t[9] << 8) | ((t[10] | (t[11] << 8)) << 16);
-          tpk = r < 8 ? tpk : tpk2;
-        }
-        const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
-        // (bit 63 set: a defined lane when no lane ends the sub-block; Pe is
-        // then unused)
-        const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
-        Pe = q + SB * lz + readlane(tend, (int)lz) + k;
 #if RPP_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1639,21 +1655,18 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       };
       // codes 2c, 2c+1 of a sub-block on lane c -> zig-zag deltas
       // (decode.h:66-69): d1 and the lane's sum d0 + d1
-      auto deltas = [&](uint4 tt, uint32_t fs, uint32_t& d1, uint32_t& dsum) {
+      // (aprev: a of the code before this lane's first, read from the list;
+      // a_(-1) = 0 lies in the list's lead words)
+      auto deltas = [&](uint4 tt, uint32_t aprev, uint32_t fs, uint32_t& d1, uint32_t& dsum) {
         if constexpr (TWO) {
-          // a of code 2c-1: lane c-1's tt.z by a wave rotate (a wave_shr
-          // leaves lane 0 unwritten instead of reading 0, so it cannot be
-          // fused into the subtraction); lane 0 takes a_(-1) = 0
-          const uint32_t u0 = tt.x - dpp<kDppWaveRor1>(tt.z);
-          const uint32_t df0 = lshl_or(lane ? u0 : tt.x, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
+          const uint32_t df0 = lshl_or(tt.x - aprev, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
           const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
           d1 = (df1 >> 1) ^ neg_lsb(df1);
           dsum = d0 + d1;
         } else {
           // code c on lane c (pair c in tt.x, tt.y); lanes past the
           // sub-block contribute nothing to the prefix
-          const uint32_t u0 = tt.x - dpp<kDppWaveRor1>(tt.x);
-          const uint32_t df = lshl_or(lane ? u0 : tt.x, fs, tt.y);
+          const uint32_t df = lshl_or(tt.x - aprev, fs, tt.y);
           d1 = (df >> 1) ^ neg_lsb(df);
           dsum = lane < n ? d1 : 0u;
         }
@@ -1731,11 +1744,14 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
         uint4 tt;
+        uint32_t aprev;
         if constexpr (TWO) {
           tt = list4[lane];
+          aprev = list[4 * lane - 2];
         } else {
           const uint2 t2 = list2[lane];
           tt = make_uint4(t2.x, t2.y, 0u, 0u);
+          aprev = list[2 * lane - 2];
         }
         uint32_t xhB;
 #if RPP_PRIO && RPP_PRIO_TOP
@@ -1748,7 +1764,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t fsB = fs_of(hB);
         lookups(xlB, fsB, e0, e1, e2, e3);
         uint32_t d1A, sumA, incA;
-        deltas(tt, fs, d1A, sumA);
+        deltas(tt, aprev, fs, d1A, sumA);
         if (RPP_ABLATE & 1024) asm volatile(".rept 20\n\tv_nop\n\t.endr" ::: "memory");
         if (RPP_ABLATE & 2048) asm volatile(".rept 20\n\ts_nop 0\n\t.endr" ::: "memory");
         if (RPP_ABLATE & 4096) {  // 20 independent integer VALU ops
@@ -2029,7 +2045,15 @@ struct ParseParams {
   uint32_t bs;
   uint32_t waves;  // waves (streams or units) per workgroup
   rpp_internal::SegView sv;  // SEG: the units of the segmented decode
+  uint32_t wave_words;       // LDS words per wave (kWaveLdsWords, or more for a long-sub-block guess)
 };
+// Per-wave LDS of the units' parse: bs >= 256 sub-blocks are 2-8 Kib long, so
+// a guess that chains kSpecSteps of them needs ~60-90 Kib of the stream
+// staged: such launches run 8 waves per workgroup with twice the words each.
+constexpr uint32_t kLongSbBs = 256;
+__host__ __device__ constexpr uint32_t parse_wave_words(uint32_t bs) {
+  return bs >= kLongSbBs ? 2 * kWaveLdsWords : kWaveLdsWords;
+}
 
 // segmented-decode parse diagnostics (rpp_parse_diag_read): cycles in the
 // guess, cycles in the chain, sub-blocks parsed, units
@@ -2092,12 +2116,22 @@ __device__ __forceinline__ uint32_t seg_sb_end_wave(const uint32_t* st, const ui
 // accepts those.  Candidates are parsed lane by lane out of LDS, up to four
 // chains per lane and three codes per read, 256 candidates at a time; after
 // every sub-block the survivors are compacted into `list` (512 words of LDS).
+// Long sub-blocks (bs 256 / 512: 2-8 Kib each) do not fit kSpecSteps of them
+// in the staged words: a chain that reaches their end after kGuessMinSteps
+// sub-blocks is finished (a survivor that is checked no further here).
 // A wrong guess costs time, never a wrong result.
 constexpr uint32_t kGuessWaveMax = 12;  // survivors below which seg_guess parses wave-parallel
+constexpr uint32_t kGuessMinSteps = 4;  // sub-blocks a chain must pass before the staged words may end it
+constexpr uint32_t kGuessFin = 1u << 31;  // (list word 2: the chain is finished)
+// (chunk0, chunk_step: this wave's share of the 256-candidate chunks when
+// several waves search one unit -- rpp_seg_guess_kernel -- with `best`, the
+// lowest survivor any of them found so far, in LDS: a wave stops at chunks
+// beyond it)
 __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_rel, uint32_t bs,
-                                              uint32_t lane, uint32_t c_first, uint32_t range, const uint4* tab) {
+                                              uint32_t lane, uint32_t c_first, uint32_t range, const uint4* tab,
+                                              uint32_t chunk0 = 0, uint32_t chunk_step = 1, uint32_t* best = nullptr,
+                                              uint32_t steps = rpp_internal::kSpecSteps) {
   using rpp_internal::kSegNone;
-  using rpp_internal::kSpecSteps;
   constexpr uint32_t kSlots = 4;
   const uint32_t maxsb = 4u + 16u * bs;
   auto peek = [&](uint32_t r) {
@@ -2105,28 +2139,36 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
     return __builtin_amdgcn_alignbit(w[1], w[0], r & 31u);
   };
   uint32_t n_chunks = 0, n_steps = 0, n_slotsteps = 0;
-  for (uint32_t c0 = c_first; c0 < maxsb; c0 += kSlots * kWave) {
+  auto found = [&](uint32_t m) {
+    if (best && lane == 0) atomicMin(best, m);
+    return m;
+  };
+  for (uint32_t c0 = c_first + kSlots * kWave * chunk0; c0 < maxsb; c0 += kSlots * kWave * chunk_step) {
+    if (best && c0 >= __builtin_amdgcn_readfirstlane(__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+      break;
     ++n_chunks;
     uint32_t cur[kSlots], org[kSlots], rng[kSlots];  // rng: lowest header | highest << 4
-    bool alive[kSlots];
+    bool alive[kSlots], fin[kSlots];
     uint32_t nslots = kSlots;
 #pragma unroll
     for (uint32_t i = 0; i < kSlots; ++i) {
       org[i] = c0 + lane + kWave * i;
       alive[i] = org[i] < maxsb && org[i] + 4 <= end_rel;
+      fin[i] = false;
       cur[i] = alive[i] ? org[i] : 0u;
       rng[i] = 0x0Fu;
     }
-    for (uint32_t step = 0; step < kSpecSteps; ++step) {
+    for (uint32_t step = 0; step < steps; ++step) {
       ++n_steps;
       n_slotsteps += nslots;
+      const bool may_finish = step >= kGuessMinSteps;
       uint32_t fsv[kSlots];
       bool rice[kSlots];
 #pragma unroll
       for (uint32_t i = 0; i < kSlots; ++i) {
         rice[i] = false;
         fsv[i] = 0;
-        if (i < nslots) {
+        if (i < nslots && !fin[i]) {
           const uint32_t v = peek(cur[i]) & 15u;
           const uint32_t lo = min(rng[i] & 15u, v), hi = max(rng[i] >> 4, v);
           rng[i] = lo | (hi << 4);
@@ -2134,10 +2176,12 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
           // (zero sub-blocks only in an all-zero run: chains of small
           // headers through the zero high bits of small remainders are the
           // common false survivors)
-          alive[i] = alive[i] && hi - lo <= range && (lo != 0 || hi == 0) && nc + 4 <= end_rel;
-          rice[i] = alive[i] && v - 1u < 14u;
+          const bool inside = nc + 4 <= end_rel;
+          alive[i] = alive[i] && hi - lo <= range && (lo != 0 || hi == 0) && (inside || may_finish);
+          fin[i] = alive[i] && !inside;
+          rice[i] = alive[i] && !fin[i] && v - 1u < 14u;
           fsv[i] = v - 1;
-          cur[i] = alive[i] ? nc : 0u;
+          cur[i] = alive[i] && !fin[i] ? nc : 0u;
         }
       }
       // the codes of the Rice sub-blocks, branch-free, up to three per LDS
@@ -2168,7 +2212,8 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
         const bool bad = r && nxt + 4 > end_rel;
         cur[i] = r ? (bad ? 0u : nxt) : cur[i];
         ncode[i] += r ? n : 0u;
-        alive[i] = alive[i] && !bad;
+        alive[i] = alive[i] && (!bad || may_finish);
+        fin[i] = fin[i] || (bad && may_finish);
         rice[i] = r && !bad && ncode[i] < bs;
       };
       for (;;) {
@@ -2181,6 +2226,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
       }
       // compact the survivors (in candidate order) into the first slots
       uint32_t cnt = 0;
+      bool all_fin = true;
 #pragma unroll
       for (uint32_t i = 0; i < kSlots; ++i) {
         if (i < nslots) {
@@ -2188,29 +2234,38 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
           const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
           if (alive[i]) {
             list[2 * at] = cur[i];
-            list[2 * at + 1] = org[i] | (rng[i] << 16);
+            list[2 * at + 1] = org[i] | (rng[i] << 16) | (fin[i] ? kGuessFin : 0u);
           }
           cnt += (uint32_t)__builtin_popcountll(m);
+          all_fin = all_fin && __ballot(alive[i] && !fin[i]) == 0;
         }
       }
       lds_fence();
-      if (cnt == 0) break;
+      if (cnt == 0 || all_fin) break;
       // few survivors: the remaining steps survivor by survivor (candidate
       // order) with the wave-parallel parse, ~1/20 of a lane-serial step each
-      if (cnt <= kGuessWaveMax && step + 1 < kSpecSteps) {
+      // (sub-blocks that end within one 2048-bit window: bs <= 128)
+      if (cnt <= kGuessWaveMax && step + 1 < steps && bs <= 2 * kWave) {
         ScanRegs sreg;
         for (uint32_t idx = 0; idx < cnt; ++idx) {
           uint32_t cur = __builtin_amdgcn_readfirstlane(list[2 * idx]);
           const uint32_t o = __builtin_amdgcn_readfirstlane(list[2 * idx + 1]);
           uint32_t lo = (o >> 16) & 15u, hi = (o >> 20) & 15u;
           bool ok = true;
-          for (uint32_t st2 = step + 1; st2 < kSpecSteps && ok; ++st2) {
+          for (uint32_t st2 = step + 1; st2 < steps && ok && !(o & kGuessFin); ++st2) {
             const uint32_t* w = st + (cur >> 5);
             const uint32_t v = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], cur & 31u)) & 15u;
             lo = min(lo, v);
             hi = max(hi, v);
             const uint32_t nc = seg_sb_end_wave(st, tab, cur, bs, lane, sreg);
-            ok = hi - lo <= range && (lo != 0 || hi == 0) && nc != rpp_internal::kSegNone && nc + 4 <= end_rel;
+            // (a sub-block that does not end in the window drops the candidate:
+            // accepting those as finished let false chains through random bits
+            // survive -- 150 reruns per 16 MiB generator stream)
+            ok = hi - lo <= range && (lo != 0 || hi == 0) && nc != rpp_internal::kSegNone;
+            if (ok && nc + 4 > end_rel) {  // the staged words end: finished (as above) after kGuessMinSteps
+              ok = st2 >= kGuessMinSteps;
+              break;
+            }
             cur = nc;
           }
           if (ok) {
@@ -2219,7 +2274,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
               atomicAdd(&g_parse_diag[5], (unsigned long long)n_steps);
               atomicAdd(&g_parse_diag[6], (unsigned long long)n_slotsteps);
             }
-            return o & 0xFFFFu;
+            return found(o & 0xFFFFu);
           }
         }
 #pragma unroll
@@ -2234,7 +2289,8 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
         cur[i] = alive[i] ? list[2 * idx] : 0u;
         const uint32_t o = alive[i] ? list[2 * idx + 1] : 0u;
         org[i] = o & 0xFFFFu;
-        rng[i] = o >> 16;
+        rng[i] = (o >> 16) & 0xFFu;
+        fin[i] = (o & kGuessFin) != 0;
       }
       lds_fence();
     }
@@ -2249,7 +2305,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
         atomicAdd(&g_parse_diag[5], (unsigned long long)n_steps);
         atomicAdd(&g_parse_diag[6], (unsigned long long)n_slotsteps);
       }
-      if (m != kSegNone) return m;
+      if (m != kSegNone) return found(m);
     }
   }
   return kSegNone;
@@ -2281,11 +2337,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
   const uint4* tab = dsm;
   const uint32_t lane = lane_id();
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  uint32_t ring_w = kTabBytes / 4 + wv * kWaveLdsWords;
+  uint32_t ring_w = kTabBytes / 4 + wv * p.wave_words;
   asm("" : "+s"(ring_w));
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + ring_w;
   const uint32_t bs = p.bs;
   const uint32_t lane24 = kSegBits * lane;
+  // guess staging: the wave's words but the 540 of the candidate list
+  const uint32_t stage_w = p.wave_words - (kListLead + kListWords);
   // One work item: a stream (SEG = false) or a unit.  Pass 0 of the
   // segmented decode takes units from a queue (one 16-wave workgroup per CU,
   // each wave unit after unit), so that every CU parses whatever the stream
@@ -2350,18 +2408,22 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     // ---- SEG: the first header of the unit ----
     // A guess: the first candidate bit in [S + c_first, S + max sub-block) whose
     // chain of kSpecSteps sub-blocks looks like ricepp output (seg_guess).
+    uint32_t grange = 3;  // the header range of the guess's chains (seg_guess), which the parse checks
     auto do_guess = [&](uint32_t c_first) -> uint32_t {
-      constexpr uint32_t kStW = kRingWords + kRingPad;
+      const uint32_t kStW = stage_w;
       const uint32_t w0 = S >> 5;
       for (uint32_t i = lane; i < kStW; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
       lds_fence();
       const uint64_t tg = memtime();
       uint32_t g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, c_first, 3, tab);
-    // none: the true chain's headers may span a wider range for a few
-    // sub-blocks; a second search with range 5 (its candidates are checked
-    // by the parse as any other)
-    if (g == kSegNone && c_first == 0)
-      g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, 0, 5, tab);
+      grange = 3;
+      // none: the true chain's headers may span a wider range for a few
+      // sub-blocks; a second search with range 5 (its candidates are checked
+      // by the parse with that range)
+      if (g == kSegNone && c_first == 0) {
+        g = seg_guess(ring, ring + kStW, min(32u * kStW - 64u, lim - S), bs, lane, 0, 5, tab);
+        grange = 5;
+      }
       if (lane == 0) atomicAdd(&g_parse_diag[0], (unsigned long long)(memtime() - tg));
       lds_fence();  // (the ring is refilled next)
       return g == kSegNone ? kSegNone : S + g;
@@ -2376,8 +2438,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
         P = us[kUsRerun];  // a header of the exact chain (stitch)
         flags = kUfRerunDone;
       } else if (ju != 0) {
-        P = P_first = do_guess(0);
-        guessed = true;
+        // (searched beforehand by several waves: rpp_seg_guess_kernel)
+        const uint32_t pre = __builtin_amdgcn_readfirstlane(us[kUsGuess]);
+        // (a guess of rpp_seg_guess_kernel is not checked again here: a wrong
+        // one costs a rerun of the unit, in parallel with any others, where a
+        // one-wave re-guess would hold up the whole pass)
+        P = P_first = pre == kSegNone ? do_guess(0) : pre == kSegNoGuess ? kSegNone : pre;
+        guessed = pre == kSegNone;
         if (P == kSegNone) flags = kUfNoGuess;
       }
       if (lane == 0) {
@@ -2520,7 +2587,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
           ++vcnt;
           vlo = min(vlo, v);
           vhi = max(vhi, v);
-          if (vhi - vlo > 3 || (vlo == 0 && vhi != 0)) vfail = stop = true;
+          if (vhi - vlo > grange || (vlo == 0 && vhi != 0)) vfail = stop = true;
         }
       };
 
@@ -2831,6 +2898,72 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
 
 }  // namespace
 
+// The first guess of every unit j >= 1 of a split stream, searched by
+// kGuessWaves waves at once (one workgroup per unit): wave w takes the
+// 256-candidate chunks w, w + kGuessWaves, ... of seg_guess's search and
+// stops at chunks beyond the lowest survivor any wave has found (LDS); the
+// unit's guess is that lowest survivor, the candidate the one-wave search
+// returns.  For batches of few units (single long streams), where
+// the parse's work queue would run one wave per CU and the lane-serial guess
+// is most of a unit's time.
+constexpr uint32_t kGuessWaves = 8;
+template <uint32_t CS>
+__global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(ParseParams p) {
+  using namespace rpp_internal;
+  extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
+  __shared__ uint32_t best;
+  const uint32_t u = blockIdx.x;
+  if (u >= p.sv.units_max || u >= (uint32_t)p.sv.unit_base[p.nblocks]) return;  // (uniform: one unit per workgroup)
+  const uint32_t b = p.sv.unit_map[u];
+  const uint32_t u0 = (uint32_t)p.sv.unit_base[b], nunits = (uint32_t)p.sv.unit_base[b + 1] - u0;
+  const uint32_t ju = u - u0;
+  if (nunits <= 1 || ju == 0) return;
+  const uint64_t n64 = p.n_samples[b], ioff = p.in_off[b], nb64 = p.in_bytes[b];
+  if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) return;
+  {
+    const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
+    for (uint32_t i = threadIdx.x; i < kMapEntries; i += blockDim.x) dsm[i] = gt[i];
+  }
+  if (threadIdx.x == 0) best = kSegNone;
+  __syncthreads();
+  const uint4* tab = dsm;
+  const uint32_t lane = lane_id();
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + kTabBytes / 4 + wv * p.wave_words;
+  const uint32_t stage_w = p.wave_words - (kListLead + kListWords);
+  const uint32_t mis = (uint32_t)(ioff & 3u);
+  const uint32_t nbytes = (uint32_t)nb64 + mis;
+  const uint8_t* in = p.in + (ioff - mis);
+  const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
+  const uint32_t S = ju << p.sv.seg_log2;
+  const uint32_t w0 = S >> 5;
+  for (uint32_t i = lane; i < stage_w; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
+  lds_fence();
+  const uint32_t end_rel = S < lim ? min(32u * stage_w - 64u, lim - S) : 0u;
+  const uint64_t tg = memtime();
+  // chains of kSpecVerify sub-blocks, the check the one-wave parse makes of a
+  // guess: the lowest survivor is the candidate that parse would settle on
+  // after rejecting the ones before it (the parse trusts this guess); range 5
+  // when none keeps range 3; failing both, the kSpecSteps survivor the parse
+  // would take unchecked in the end
+  uint32_t g = kSegNone;
+  for (uint32_t k = 0; k < 4 && g == kSegNone; ++k) {
+    if (k != 0) {
+      if (threadIdx.x == 0) best = kSegNone;
+      __syncthreads();
+    }
+    (void)seg_guess(ring, ring + stage_w, end_rel, p.bs, lane, 0, k & 1 ? 5u : 3u, tab, wv, kGuessWaves, &best,
+                    k < 2 ? kSpecVerify : kSpecSteps);
+    __syncthreads();
+    g = best;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    p.sv.ustate[kUsWords * u + kUsGuess] = g == kSegNone ? kSegNoGuess : S + g;
+    atomicAdd(&g_parse_diag[0], (unsigned long long)(memtime() - tg));
+  }
+}
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -2969,6 +3102,32 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
+// (below this many units the parse's work queue leaves wave slots idle: each
+// unit's guess gets kGuessWaves waves of its own)
+constexpr uint32_t kGuessKernelMaxUnits = 2048;
+int launch_seg_guess(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                     const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples, const SegView& sv,
+                     hipStream_t stream) {
+  if (nblocks == 0 || sv.units_max == 0 || sv.units_max > kGuessKernelMaxUnits) return RPP_OK;
+  const uint32_t wave_words = parse_wave_words(cfg->block_size);
+  const size_t lds = kTabBytes + (size_t)kGuessWaves * wave_words * 4;
+  static void (*const kernels[2])(ParseParams) = {rpp_seg_guess_kernel<1>, rpp_seg_guess_kernel<2>};
+  static std::once_flag attr_once;
+  static hipError_t attr_err = hipSuccess;
+  std::call_once(attr_once, [] {
+    const int mx = (int)(kTabBytes + (size_t)kGuessWaves * parse_wave_words(kLongSbBs) * 4);
+    for (auto k : kernels)
+      if (attr_err == hipSuccess)
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+  });
+  if (attr_err != hipSuccess) return RPP_HIP_ERROR;
+  ParseParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, nullptr, nullptr, nullptr, nblocks,
+                cfg->block_size, kGuessWaves, sv, wave_words};
+  hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3(sv.units_max), dim3(kWave * kGuessWaves), lds,
+                     stream, p);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
 int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples,
                      const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,
@@ -2985,10 +3144,12 @@ int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   }
   // (pass 0: as many waves per workgroup as the unit bound needs to give every
   // CU some, at most 16, so that a batch of few units still spreads over all CUs)
-  const uint32_t W = sv.pass == 0 ? std::min<uint32_t>(kDecMaxWaves, std::max<uint32_t>(1, (sv.units_max + cus - 1) / cus))
+  const uint32_t wave_words = parse_wave_words(cfg->block_size);
+  const uint32_t wmax = (uint32_t)((kTabBytes + (size_t)kDecMaxWaves * kWaveLdsWords * 4 - kTabBytes) / (wave_words * 4));
+  const uint32_t W = sv.pass == 0 ? std::min<uint32_t>(wmax, std::max<uint32_t>(1, (sv.units_max + cus - 1) / cus))
                                   : 1u;
   const uint32_t grid = sv.pass == 0 ? std::min<uint32_t>((uint32_t)cus, (sv.units_max + W - 1) / W) : sv.units_max;
-  const size_t lds = kTabBytes + (size_t)W * kWaveLdsWords * 4;
+  const size_t lds = kTabBytes + (size_t)W * wave_words * 4;
   static void (*const kernels[2])(ParseParams) = {rpp_parse_kernel<1, true>, rpp_parse_kernel<2, true>};
   static std::once_flag attr_once;
   static hipError_t attr_err = hipSuccess;
@@ -3000,7 +3161,7 @@ int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   });
   if (attr_err != hipSuccess) return RPP_HIP_ERROR;
   ParseParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_sb_base, d_sb_pos, d_status, nblocks,
-                cfg->block_size, W, sv};
+                cfg->block_size, W, sv, wave_words};
   hipLaunchKernelGGL(kernels[cfg->component_stream_count - 1], dim3(grid), dim3(kWave * W), lds, stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }

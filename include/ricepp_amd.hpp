@@ -183,4 +183,8 @@ struct facade_stats {
 };
 facade_stats get_facade_stats();
 
+// Test only: the next `n` pooled-context creations fail (as a failed
+// hipStreamCreate would), to exercise the error paths of the batch queue.
+void inject_context_failures(uint32_t n);
+
 }  // namespace ricepp_amd

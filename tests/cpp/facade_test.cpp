@@ -2,6 +2,7 @@
 // path: ricepp/test/codec_test.cpp (round trips, worst-case KATs, error
 // contract) and test/ricepp_compressor_test.cpp (block_compressor spec
 // round trip), checking every stream against the CPU oracle byte for byte.
+#include <atomic>
 #include <bit>
 #include <chrono>
 #include <cstdio>
@@ -93,6 +94,29 @@ int bench(int argc, char** argv);
 
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "--bench") return bench(argc, argv);
+  // the batch queue's error paths (round-2 review): the first pooled context
+  // fails to come up; the callers of that batch get an exception, none hangs,
+  // and the queue and pool work afterwards
+  {
+    ricepp_amd::inject_context_failures(1);
+    auto c = cfg(128, 1, true, 0);
+    auto x = make_data(65536, 0, true, 50, 21);
+    std::atomic<int> errs{0}, oks{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; ++t)
+      th.emplace_back([&] {
+        try {
+          auto bytes = ricepp_amd::create_encoder<uint16_t>(c)->encode(x);
+          ++oks;
+        } catch (std::runtime_error const&) {
+          ++errs;
+        }
+      });
+    for (auto& t : th) t.join();
+    CHECK(errs.load() >= 1);
+    CHECK(errs.load() + oks.load() == 8);
+    roundtrip(c, 65536, 50, 22);
+  }
   // codec_test.cpp:65-152
   roundtrip(cfg(16, 1, true, 0), 12345, 50, 1);
   roundtrip(cfg(13, 1, true, 4), 4321, 50, 2);
@@ -292,12 +316,18 @@ int main(int argc, char** argv) {
 // DwarFS's worker_group shape: T threads, each compressing / decompressing
 // its share of B independent 64 KiB blocks through the facade (host spans in
 // and out, so PCIe and host copies are included).  One JSON line per T.
+// (--kib=K: blocks of K KiB instead of 64; DwarFS's own block size is
+// 16 MiB at mkdwarfs' default -S 24)
 int bench(int argc, char** argv) {
   size_t const blocks = argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 4096;
   std::vector<int> threads;
-  for (int i = 3; i < argc; ++i) threads.push_back(std::atoi(argv[i]));
+  size_t kib = 64;
+  for (int i = 3; i < argc; ++i) {
+    if (std::string(argv[i]).rfind("--kib=", 0) == 0) kib = std::strtoul(argv[i] + 6, nullptr, 10);
+    else threads.push_back(std::atoi(argv[i]));
+  }
   if (threads.empty()) threads = {1, 8, 64};
-  size_t const n = 32768;  // 64 KiB of samples
+  size_t const n = kib * 512;  // samples per block
   auto c = cfg(128, 1, true, 0);
   std::vector<std::vector<uint16_t>> in(blocks);
   std::mt19937_64 rng(42);

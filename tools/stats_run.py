@@ -9,8 +9,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 os.environ["RICEPP_AMD_LIB"] = str(ROOT / "dwarfs_amd" / "lib" / "libricepp_amd_stats.so")
 nblocks = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-if len(sys.argv) > 2:
-    os.environ["RICEPP_DEC_WAVES"] = sys.argv[2]
+waves = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -21,7 +20,8 @@ L = _native.lib()
 L.rpp_stats_fetch.argtypes = [C.c_void_p, C.c_int]
 n = 32768
 x = make_poisson_blocks(nblocks, n, 1000.0, 42, torch.device("cuda:0"))
-pipe = parallel.ShardPipeline(codec.CodecConfig(128, 1, "big", 0), x, np.arange(nblocks) * n, np.full(nblocks, n))
+pipe = parallel.ShardPipeline(codec.CodecConfig(128, 1, "big", 0), x, np.arange(nblocks) * n, np.full(nblocks, n),
+                              decode_options=codec.DecodeOptions(fused_waves=waves))
 pipe.encode()
 torch.cuda.synchronize()
 st = np.zeros(16, np.uint64)
@@ -31,7 +31,7 @@ torch.cuda.synchronize()
 pipe.check(x)
 L.rpp_stats_fetch(st.ctypes.data, 1)
 it = float(st[0])
-print(f"nblocks {nblocks} waves {os.environ.get('RICEPP_DEC_WAVES', 'auto')}: fast iterations {int(it)}")
+print(f"nblocks {nblocks} waves {waves or 'auto'}: fast iterations {int(it)}")
 for i in range(1, 16):
     if st[i]:
         print(f"slot {i:2d} cycles/iteration {st[i] / it:8.1f}")
