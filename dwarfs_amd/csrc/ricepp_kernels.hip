@@ -2073,10 +2073,13 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // The end (next header) of the sub-block with its header at bit r of the
 // staged words st (relative positions), parsed by the whole wave: one 2048-bit
 // window of 32-bit lane segments with exact entry states (w32_count, byte maps
-// for any fs), kSegNone when its codes do not end in that window (a guess
-// candidate is then dropped: a missed guess costs time, never a result).
+// for any fs).  A sub-block longer than the window (fs 11-13 with outliers:
+// ~2 Kib) continues code by code from the end of the window's last complete
+// code; past `lim` (the staged words' end) it returns `lim`.  kSegNone: a
+// unary run past the window's end that the walk cannot follow (never for a
+// well-formed chain).
 __device__ __forceinline__ uint32_t seg_sb_end_wave(const uint32_t* st, const uint4* tab, uint32_t r, uint32_t bs,
-                                                    uint32_t lane, ScanRegs& sreg) {
+                                                    uint32_t lane, ScanRegs& sreg, uint32_t lim) {
   const uint32_t* w = st + (r >> 5) + lane;
   const uint32_t x = __builtin_amdgcn_alignbit(w[1], w[0], r & 31u);
   const uint32_t v = __builtin_amdgcn_readfirstlane(x) & 15u;
@@ -2089,7 +2092,28 @@ __device__ __forceinline__ uint32_t seg_sb_end_wave(const uint32_t* st, const ui
   uint32_t tm, cnt, incl, unused;
   uint64_t finm;
   w32_count(e0, e1, e2, e3, bs, 0u, sreg, tm, cnt, incl, finm, unused);
-  if (finm == 0) return rpp_internal::kSegNone;
+  if (finm == 0) {
+    // codes past the window: from the end of its last complete code (its
+    // terminator + fs + 1), one code per step (a zero word: 32 more unary bits)
+    const uint64_t has = __ballot(cnt != 0);
+    uint32_t c = readlane(incl, kWave - 1), cur = r + 4u;
+    if (has) {
+      const uint32_t L = 63u - (uint32_t)__builtin_clzll(has);
+      cur = r + 32u * L + (31u - (uint32_t)__builtin_clz(readlane(tm, (int)L))) + v;
+    }
+    while (c < bs) {
+      if (cur + 64u > lim) return lim;
+      const uint32_t* w = st + (cur >> 5);
+      const uint32_t y = __builtin_amdgcn_alignbit(w[1], w[0], cur & 31u);
+      if (y == 0) {
+        cur += 32u;
+      } else {
+        cur += ffbl(y) + v;
+        ++c;
+      }
+    }
+    return cur;
+  }
   const uint32_t lz = (uint32_t)__builtin_ctzll(finm);
   uint32_t t = readlane(tm, (int)lz);
   const uint32_t rr = bs - 1u - (readlane(incl, (int)lz) - readlane(cnt, (int)lz));
@@ -2120,6 +2144,7 @@ __device__ __forceinline__ uint32_t seg_sb_end_wave(const uint32_t* st, const ui
 // in the staged words: a chain that reaches their end after kGuessMinSteps
 // sub-blocks is finished (a survivor that is checked no further here).
 // A wrong guess costs time, never a wrong result.
+constexpr uint32_t kSlotsPerGuess = 4;  // candidates per lane of a 256-candidate chunk
 constexpr uint32_t kGuessWaveMax = 12;  // survivors below which seg_guess parses wave-parallel
 constexpr uint32_t kGuessMinSteps = 4;  // sub-blocks a chain must pass before the staged words may end it
 constexpr uint32_t kGuessFin = 1u << 31;  // (list word 2: the chain is finished)
@@ -2132,7 +2157,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
                                               uint32_t chunk0 = 0, uint32_t chunk_step = 1, uint32_t* best = nullptr,
                                               uint32_t steps = rpp_internal::kSpecSteps) {
   using rpp_internal::kSegNone;
-  constexpr uint32_t kSlots = 4;
+  constexpr uint32_t kSlots = kSlotsPerGuess;
   const uint32_t maxsb = 4u + 16u * bs;
   auto peek = [&](uint32_t r) {
     const uint32_t* w = st + (r >> 5);
@@ -2257,10 +2282,10 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
             const uint32_t v = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], cur & 31u)) & 15u;
             lo = min(lo, v);
             hi = max(hi, v);
-            const uint32_t nc = seg_sb_end_wave(st, tab, cur, bs, lane, sreg);
-            // (a sub-block that does not end in the window drops the candidate:
-            // accepting those as finished let false chains through random bits
-            // survive -- 150 reruns per 16 MiB generator stream)
+            const uint32_t nc = seg_sb_end_wave(st, tab, cur, bs, lane, sreg, end_rel);
+            // (accepting sub-blocks longer than the window as a finished chain,
+            // before the walk past it existed, let false chains through random
+            // bits survive: 150 reruns per 16 MiB generator stream)
             ok = hi - lo <= range && (lo != 0 || hi == 0) && nc != rpp_internal::kSegNone;
             if (ok && nc + 4 > end_rel) {  // the staged words end: finished (as above) after kGuessMinSteps
               ok = st2 >= kGuessMinSteps;
@@ -2907,6 +2932,11 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
 // the parse's work queue would run one wave per CU and the lane-serial guess
 // is most of a unit's time.
 constexpr uint32_t kGuessWaves = 8;
+constexpr uint32_t kGuessListWords = 2 * kSlotsPerGuess * kWave;  // a wave's survivors: (position, origin | range)
+__host__ __device__ constexpr size_t guess_lds_bytes(uint32_t bs) {
+  // (the staged words of parse_wave_words, once per workgroup: 76 KiB at bs <= 128, two workgroups per CU)
+  return kTabBytes + 4 * ((size_t)parse_wave_words(bs) - (kListLead + kListWords) + kGuessWaves * kGuessListWords);
+}
 template <uint32_t CS>
 __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(ParseParams p) {
   using namespace rpp_internal;
@@ -2929,16 +2959,18 @@ __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(Parse
   const uint4* tab = dsm;
   const uint32_t lane = lane_id();
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + kTabBytes / 4 + wv * p.wave_words;
+  // the unit's staged words, shared by the waves, then a survivor list per wave
   const uint32_t stage_w = p.wave_words - (kListLead + kListWords);
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + kTabBytes / 4;
+  uint32_t* list = ring + stage_w + wv * kGuessListWords;
   const uint32_t mis = (uint32_t)(ioff & 3u);
   const uint32_t nbytes = (uint32_t)nb64 + mis;
   const uint8_t* in = p.in + (ioff - mis);
   const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
   const uint32_t S = ju << p.sv.seg_log2;
   const uint32_t w0 = S >> 5;
-  for (uint32_t i = lane; i < stage_w; i += kWave) ring[i] = stream_word(in, nbytes, w0 + i);
-  lds_fence();
+  for (uint32_t i = threadIdx.x; i < stage_w; i += blockDim.x) ring[i] = stream_word(in, nbytes, w0 + i);
+  __syncthreads();
   const uint32_t end_rel = S < lim ? min(32u * stage_w - 64u, lim - S) : 0u;
   const uint64_t tg = memtime();
   // chains of kSpecVerify sub-blocks, the check the one-wave parse makes of a
@@ -2952,7 +2984,7 @@ __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(Parse
       if (threadIdx.x == 0) best = kSegNone;
       __syncthreads();
     }
-    (void)seg_guess(ring, ring + stage_w, end_rel, p.bs, lane, 0, k & 1 ? 5u : 3u, tab, wv, kGuessWaves, &best,
+    (void)seg_guess(ring, list, end_rel, p.bs, lane, 0, k & 1 ? 5u : 3u, tab, wv, kGuessWaves, &best,
                     k < 2 ? kSpecVerify : kSpecSteps);
     __syncthreads();
     g = best;
@@ -3110,12 +3142,12 @@ int launch_seg_guess(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
                      hipStream_t stream) {
   if (nblocks == 0 || sv.units_max == 0 || sv.units_max > kGuessKernelMaxUnits) return RPP_OK;
   const uint32_t wave_words = parse_wave_words(cfg->block_size);
-  const size_t lds = kTabBytes + (size_t)kGuessWaves * wave_words * 4;
+  const size_t lds = guess_lds_bytes(cfg->block_size);
   static void (*const kernels[2])(ParseParams) = {rpp_seg_guess_kernel<1>, rpp_seg_guess_kernel<2>};
   static std::once_flag attr_once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(attr_once, [] {
-    const int mx = (int)(kTabBytes + (size_t)kGuessWaves * parse_wave_words(kLongSbBs) * 4);
+    const int mx = (int)guess_lds_bytes(kLongSbBs);
     for (auto k : kernels)
       if (attr_err == hipSuccess)
         attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
