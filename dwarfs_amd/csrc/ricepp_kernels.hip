@@ -2269,8 +2269,8 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
       if (cnt == 0 || all_fin) break;
       // few survivors: the remaining steps survivor by survivor (candidate
       // order) with the wave-parallel parse, ~1/20 of a lane-serial step each
-      // (sub-blocks that end within one 2048-bit window: bs <= 128)
-      if (cnt <= kGuessWaveMax && step + 1 < steps && bs <= 2 * kWave) {
+      // (any bs: codes past its 2048-bit window are walked one by one)
+      if (cnt <= kGuessWaveMax && step + 1 < steps) {
         ScanRegs sreg;
         for (uint32_t idx = 0; idx < cnt; ++idx) {
           uint32_t cur = __builtin_amdgcn_readfirstlane(list[2 * idx]);
