@@ -1174,9 +1174,11 @@ __device__ __forceinline__ Map16 scan_step16(const Map16& m) {
 // the terminator mask tm of the lane's segment; then the counts (inclusive
 // prefix incl, the lanes reaching n codes in finm) and the rider's prefix as
 // in the fused fast loop.
+// (exit_state: each lane's state after its segment, in replicated form, for a
+// parse that continues in the next window)
 __device__ __forceinline__ void w32_count(uint4 e0, uint4 e1, uint4 e2, uint4 e3, uint32_t n, uint32_t rider,
                                           ScanRegs& sreg, uint32_t& tm, uint32_t& cnt, uint32_t& incl,
-                                          uint64_t& finm, uint32_t& rider_incl) {
+                                          uint64_t& finm, uint32_t& rider_incl, uint32_t* exit_state = nullptr) {
   // lanes up to the first one that ends the sub-block (all when none does)
   auto upto_end = [](uint64_t fm) { return (2ull << (uint32_t)__builtin_ctzll(fm | (1ull << 63))) - 1ull; };
   uint32_t S1, S2, S3;
@@ -1218,6 +1220,7 @@ __device__ __forceinline__ void w32_count(uint4 e0, uint4 e1, uint4 e2, uint4 e3
     incl = wave_incl_sum(cnt);
     finm = __ballot(incl >= n);
   }
+  if (exit_state) *exit_state = eval(Sold);
 }
 
 // Orders this wave's LDS accesses without waiting on its global stores
@@ -2071,54 +2074,42 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 }
 
 // The end (next header) of the sub-block with its header at bit r of the
-// staged words st (relative positions), parsed by the whole wave: one 2048-bit
-// window of 32-bit lane segments with exact entry states (w32_count, byte maps
-// for any fs).  A sub-block longer than the window (fs 11-13 with outliers:
-// ~2 Kib) continues code by code from the end of the window's last complete
-// code; past `lim` (the staged words' end) it returns `lim`.  kSegNone: a
-// unary run past the window's end that the walk cannot follow (never for a
-// well-formed chain).
+// staged words st (relative positions), parsed by the whole wave in 2048-bit
+// windows of 32-bit lane segments with exact entry states (w32_count, byte
+// maps for any fs): the first window enters after the 4-bit header, a later
+// one in the state the previous window's last lane left (sub-blocks longer
+// than a window: fs 11-13 with outliers, bs 256 / 512).  Returns `lim` when
+// the sub-block runs past lim - 64 (the staged words' end).
 __device__ __forceinline__ uint32_t seg_sb_end_wave(const uint32_t* st, const uint4* tab, uint32_t r, uint32_t bs,
-                                                    uint32_t lane, ScanRegs& sreg, uint32_t lim) {
+                                                    uint32_t lane, const ScanRegs& sreg0, uint32_t lim) {
   const uint32_t* w = st + (r >> 5) + lane;
-  const uint32_t x = __builtin_amdgcn_alignbit(w[1], w[0], r & 31u);
+  uint32_t x = __builtin_amdgcn_alignbit(w[1], w[0], r & 31u);
   const uint32_t v = __builtin_amdgcn_readfirstlane(x) & 15u;
   if (v == 0) return r + 4u;
   if (v == 15) return r + 4u + 16u * bs;
-  const uint32_t fs = v - 1u;
-  const uint4* tb = tab + 256u * fs;
-  const uint4 e0 = tb[x & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(x, 8, 8)], e2 = tb[__builtin_amdgcn_ubfe(x, 16, 8)],
-              e3 = tb[x >> 24];
-  uint32_t tm, cnt, incl, unused;
-  uint64_t finm;
-  w32_count(e0, e1, e2, e3, bs, 0u, sreg, tm, cnt, incl, finm, unused);
-  if (finm == 0) {
-    // codes past the window: from the end of its last complete code (its
-    // terminator + fs + 1), one code per step (a zero word: 32 more unary bits)
-    const uint64_t has = __ballot(cnt != 0);
-    uint32_t c = readlane(incl, kWave - 1), cur = r + 4u;
-    if (has) {
-      const uint32_t L = 63u - (uint32_t)__builtin_clzll(has);
-      cur = r + 32u * L + (31u - (uint32_t)__builtin_clz(readlane(tm, (int)L))) + v;
+  const uint4* tb = tab + 256u * (v - 1u);
+  ScanRegs sreg = sreg0;  // (lane 0's entry state: the header's 4 bits, then the carried state)
+  uint32_t base = r, need = bs;
+  for (;;) {
+    const uint4 e0 = tb[x & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(x, 8, 8)], e2 = tb[__builtin_amdgcn_ubfe(x, 16, 8)],
+                e3 = tb[x >> 24];
+    uint32_t tm, cnt, incl, unused, ex;
+    uint64_t finm;
+    w32_count(e0, e1, e2, e3, need, 0u, sreg, tm, cnt, incl, finm, unused, &ex);
+    if (finm != 0) {
+      const uint32_t lz = (uint32_t)__builtin_ctzll(finm);
+      uint32_t t = readlane(tm, (int)lz);
+      const uint32_t rr = need - 1u - (readlane(incl, (int)lz) - readlane(cnt, (int)lz));
+      for (uint32_t i = 0; i < rr; ++i) t &= t - 1u;  // (scalar: the rr-th terminator of lane lz)
+      return base + 32u * lz + (uint32_t)__builtin_ctz(t) + v;
     }
-    while (c < bs) {
-      if (cur + 64u > lim) return lim;
-      const uint32_t* w = st + (cur >> 5);
-      const uint32_t y = __builtin_amdgcn_alignbit(w[1], w[0], cur & 31u);
-      if (y == 0) {
-        cur += 32u;
-      } else {
-        cur += ffbl(y) + v;
-        ++c;
-      }
-    }
-    return cur;
+    need -= readlane(incl, kWave - 1);
+    base += 32u * kWave;
+    if (base + 32u * kWave + 64u > lim) return lim;
+    sreg.ja = sreg.jb = readlane(ex, kWave - 1);
+    w = st + (base >> 5) + lane;
+    x = __builtin_amdgcn_alignbit(w[1], w[0], base & 31u);
   }
-  const uint32_t lz = (uint32_t)__builtin_ctzll(finm);
-  uint32_t t = readlane(tm, (int)lz);
-  const uint32_t rr = bs - 1u - (readlane(incl, (int)lz) - readlane(cnt, (int)lz));
-  for (uint32_t i = 0; i < rr; ++i) t &= t - 1u;  // (scalar: the rr-th terminator of lane lz)
-  return r + 32u * lz + (uint32_t)__builtin_ctz(t) + v;
 }
 
 // Segmented decode, the first header of a unit (ricepp_internal.h): the
