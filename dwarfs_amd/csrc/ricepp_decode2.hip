@@ -43,7 +43,10 @@
 namespace {
 
 constexpr uint32_t kTile = 256;          // sub-blocks (lanes) per tile
-constexpr uint32_t kStageWords = 9216;   // 36 KiB of the stream per tile in LDS
+// 64 KiB of the stream per tile in LDS: a tile's 256 sub-blocks at bs 128
+// take up to 16 bits per sample; with 36 KiB, generator data (14 bits per
+// sample) left 40 % of each tile's lanes unstaged, on the general path
+constexpr uint32_t kStageWords = 16384;
 // slack after the staged words: a lane whose codes run past their window
 // (then decoded again by the general path) reads at most 128 * 45 bits on
 constexpr uint32_t kStagePad = 192;

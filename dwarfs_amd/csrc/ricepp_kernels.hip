@@ -496,15 +496,36 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
     const uint32_t k = fs + 1;
     const uint32_t m2 = ((2u << fs) - 1u) * 0x10001u;
     uint32_t e = pos - k;
+    us2 qv[SPL / 2];
+    us2 qmax = {0, 0};
 #pragma unroll
     for (uint32_t h = 0; h < SPL / 2; ++h) {
-      const us2 dd = P.d[h];
-      const uint32_t qq = as_u32(dd >> (us2)(unsigned short)fs);
-      const uint32_t cc = (as_u32(dd << (us2)1) & m2) | 0x10001u;
-      e += k + (qq & 0xFFFFu);
-      emit_bits64(st.win, e, cc & 0xFFFFu);
-      e += k + (qq >> 16);
-      emit_bits64(st.win, e, cc >> 16);
+      qv[h] = P.d[h] >> (us2)(unsigned short)fs;
+      qmax = __builtin_elementwise_max(qmax, qv[h]);
+    }
+    // the pair (2h, 2h+1) spans k + q_(2h+1) + k bits from code 2h's '1':
+    // when that fits 32 bits for every pair of the wave (fs <= 13 and unary
+    // runs short: Poisson data), one 64-bit shift and two ds_or_b32 per pair
+    if (!__any(2u * k + (as_u32(qmax) >> 16) > 32u) && !(RPP_EABLATE & 4)) {
+#pragma unroll
+      for (uint32_t h = 0; h < SPL / 2; ++h) {
+        const uint32_t qq = as_u32(qv[h]);
+        const uint32_t cc = (as_u32(P.d[h] << (us2)1) & m2) | 0x10001u;
+        e += k + (qq & 0xFFFFu);
+        const uint32_t d = k + (qq >> 16);
+        emit_bits64(st.win, e, (cc & 0xFFFFu) | ((cc >> 16) << d));
+        e += d;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t h = 0; h < SPL / 2; ++h) {
+        const uint32_t qq = as_u32(qv[h]);
+        const uint32_t cc = (as_u32(P.d[h] << (us2)1) & m2) | 0x10001u;
+        e += k + (qq & 0xFFFFu);
+        emit_bits64(st.win, e, cc & 0xFFFFu);
+        e += k + (qq >> 16);
+        emit_bits64(st.win, e, cc >> 16);
+      }
     }
   } else if (mode == 1 && !(RPP_EABLATE & 1)) {
     const uint32_t lowmask = (1u << fs) - 1u;
@@ -2060,7 +2081,9 @@ __host__ __device__ constexpr uint32_t parse_wave_words(uint32_t bs) {
 
 // segmented-decode parse diagnostics (rpp_parse_diag_read): cycles in the
 // guess, cycles in the chain, sub-blocks parsed, units
-__device__ unsigned long long g_parse_diag[8];
+// (8..11: the guess's lane-serial steps and wave-parallel tail: cycles,
+// cycles, tail sub-blocks, tail windows)
+__device__ unsigned long long g_parse_diag[16];
 __device__ __forceinline__ uint64_t memtime() {
   uint64_t t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -2163,6 +2186,8 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
     if (best && c0 >= __builtin_amdgcn_readfirstlane(__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
       break;
     ++n_chunks;
+    const uint64_t t_serial = memtime();
+    bool tailed = false;
     uint32_t cur[kSlots], org[kSlots], rng[kSlots];  // rng: lowest header | highest << 4
     bool alive[kSlots], fin[kSlots];
     uint32_t nslots = kSlots;
@@ -2262,6 +2287,10 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
       // order) with the wave-parallel parse, ~1/20 of a lane-serial step each
       // (any bs: codes past its 2048-bit window are walked one by one)
       if (cnt <= kGuessWaveMax && step + 1 < steps) {
+        const uint64_t t_tail = memtime();
+        uint32_t n_tail = 0;
+        tailed = true;
+        if (lane == 0) atomicAdd(&g_parse_diag[8], (unsigned long long)(t_tail - t_serial));
         ScanRegs sreg;
         for (uint32_t idx = 0; idx < cnt; ++idx) {
           uint32_t cur = __builtin_amdgcn_readfirstlane(list[2 * idx]);
@@ -2274,6 +2303,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
             lo = min(lo, v);
             hi = max(hi, v);
             const uint32_t nc = seg_sb_end_wave(st, tab, cur, bs, lane, sreg, end_rel);
+            ++n_tail;
             // (accepting sub-blocks longer than the window as a finished chain,
             // before the walk past it existed, let false chains through random
             // bits survive: 150 reruns per 16 MiB generator stream)
@@ -2286,12 +2316,18 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
           }
           if (ok) {
             if (lane == 0) {
+              atomicAdd(&g_parse_diag[9], (unsigned long long)(memtime() - t_tail));
+              atomicAdd(&g_parse_diag[10], (unsigned long long)n_tail);
               atomicAdd(&g_parse_diag[4], (unsigned long long)n_chunks);
               atomicAdd(&g_parse_diag[5], (unsigned long long)n_steps);
               atomicAdd(&g_parse_diag[6], (unsigned long long)n_slotsteps);
             }
             return found(o & 0xFFFFu);
           }
+        }
+        if (lane == 0) {
+          atomicAdd(&g_parse_diag[9], (unsigned long long)(memtime() - t_tail));
+          atomicAdd(&g_parse_diag[10], (unsigned long long)n_tail);
         }
 #pragma unroll
         for (uint32_t i = 0; i < kSlots; ++i) alive[i] = false;  // (none survived)
@@ -2310,6 +2346,7 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
       }
       lds_fence();
     }
+    if (!tailed && lane == 0) atomicAdd(&g_parse_diag[8], (unsigned long long)(memtime() - t_serial));
     uint32_t m = kSegNone;
 #pragma unroll
     for (uint32_t i = 0; i < kSlots; ++i)
@@ -2995,10 +3032,10 @@ extern "C" {
 uint32_t rpp_abi_version(void) { return 1; }
 
 // diagnostics only (not in the C ABI header): the segmented parse's counters
-int rpp_parse_diag_read(unsigned long long* out8, int reset) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_parse_diag), sizeof(g_parse_diag)) != hipSuccess) return RPP_HIP_ERROR;
+int rpp_parse_diag_read(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_parse_diag), sizeof(g_parse_diag)) != hipSuccess) return RPP_HIP_ERROR;
   if (reset) {
-    unsigned long long z[8] = {0};
+    unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_parse_diag), z, sizeof(z)) != hipSuccess) return RPP_HIP_ERROR;
   }
   return RPP_OK;

@@ -27,7 +27,7 @@ def run(name, blocks):
     enc = codec.encode_batch(cfg, x, offs, ns)
     codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns)
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 8)()
+    buf = (C.c_ulonglong * 16)()
     N.lib().rpp_parse_diag_read(buf, 1)
     codec.segmented_decode_stats(reset=True)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -36,12 +36,14 @@ def run(name, blocks):
     ev[1].record()
     torch.cuda.synchronize()
     N.lib().rpp_parse_diag_read(buf, 1)
-    g, ch, sb, un, nch, nst, nsl, reg = map(int, buf)
+    g, ch, sb, un, nch, nst, nsl, reg, cser, ctail, ntail = map(int, buf[:11])
     # (s_memtime counts shader-clock cycles on gfx950)
     print(f"{name}: {ev[0].elapsed_time(ev[1]):.3f} ms, units {un}, sub-blocks {sb}, "
           f"guess {g / max(un, 1) / 1e3:.0f} K cycles/unit, chain {ch / max(un, 1) / 1e3:.0f} K cycles/unit = "
           f"{ch / max(sb, 1):.0f} cycles/sub-block; per guess {nch / max(un, 1):.2f} chunks {nst / max(un, 1):.1f} steps "
-          f"{nsl / max(un, 1):.1f} slot-steps, re-guesses {reg}, exact {torch.equal(out[:sum(ns)], x)}, "
+          f"{nsl / max(un, 1):.1f} slot-steps; lane-serial {cser / max(un, 1) / 1e3:.0f} K cycles/unit, tail "
+          f"{ctail / max(un, 1) / 1e3:.0f} K cycles/unit ({ntail / max(un, 1):.1f} sub-blocks, "
+          f"{ctail / max(ntail, 1):.0f} cycles each); re-guesses {reg}, exact {torch.equal(out[:sum(ns)], x)}, "
           f"{codec.segmented_decode_stats()}", flush=True)
 
 
