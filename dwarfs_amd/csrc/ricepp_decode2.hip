@@ -82,7 +82,7 @@ struct Workspace {
   uint32_t* queue;      // [1]
   uint64_t* cnt2;       // [U_max + 1] exact positions per unit
   uint64_t* off2;       // [U_max + 1]
-  uint32_t* guard;      // [1] 1: the batch exceeds the promised sizes (rpp_dec_guard_kernel)
+  uint32_t* guard;      // [1] 1: the batch exceeds the promised sizes (rpp_seg_plan_kernel)
   uint64_t bytes;
   uint64_t max_tiles;
   uint64_t units_max;
@@ -156,23 +156,6 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint64_t max_str
   return w;
 }
 
-// sub-blocks + 1 (the end entry) and tiles of each stream; entry B is 0 so
-// that the exclusive scans end in the totals
-// (units: the segmented decode's units per stream; streams of one unit are
-// the fused kernel's and get no entries)
-__global__ void rpp_dec_count_kernel(const uint64_t* n_samples, uint32_t nblocks, uint32_t chunk_len, uint32_t cs,
-                                     uint64_t* sb_cnt, uint64_t* tile_cnt, const uint64_t* units, const uint32_t* guard) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > nblocks) return;
-  uint64_t nsb = 0;
-  if (i < nblocks && !*guard) {
-    const uint64_t n = n_samples[i];
-    if (n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES && (!units || units[i] > 1)) nsb = (n + chunk_len - 1) / chunk_len * cs;
-  }
-  sb_cnt[i] = i < nblocks ? nsb + 1 : 0;
-  tile_cnt[i] = (nsb + kTile - 1) / kTile;
-}
-
 // Tiles are handed out level by level: tile l of every stream before tile
 // l + 1 of any (a stream's tiles stay in order, as the look-back needs, and a
 // long stream has few tiles in flight at once, so its inclusive prefixes keep
@@ -193,22 +176,6 @@ __device__ __forceinline__ uint32_t block_excl_scan_flag(bool f, uint32_t* sh, u
   }
   __syncthreads();
   return off + before;
-}
-
-__global__ __launch_bounds__(kLvlThreads) void rpp_dec_level_count_kernel(const uint64_t* tile_cnt, uint32_t nblocks,
-                                                                          uint32_t levels, uint64_t* lvl_cnt) {
-  __shared__ uint32_t sh[kLvlThreads / 64];
-  const uint32_t l = blockIdx.x;
-  if (l > levels) return;
-  uint64_t n = 0;
-  if (l < levels)
-    for (uint32_t b0 = 0; b0 < nblocks; b0 += kLvlThreads) {
-      const uint32_t b = b0 + threadIdx.x;
-      uint32_t total;
-      block_excl_scan_flag(b < nblocks && tile_cnt[b] > l, sh, total);
-      n += total;
-    }
-  if (threadIdx.x == 0) lvl_cnt[l] = n;
 }
 
 __global__ __launch_bounds__(kLvlThreads) void rpp_dec_level_map_kernel(const uint64_t* tile_cnt, uint32_t nblocks,
@@ -694,27 +661,12 @@ struct SegArgs {
   uint64_t* cnt;  // [U_max + 1] exact positions per unit
   uint64_t* off;  // [U_max + 1] their exclusive scan
   uint32_t* uhit; // [U_max] first overshoot header of the unit before that is a header of the unit
-  const uint32_t* guard;  // rpp_dec_guard_kernel's verdict: 1 = no stream is split
+  const uint32_t* guard;  // rpp_seg_plan_kernel's verdict: 1 = no stream is split
   uint32_t nblocks, bs, cs;
 };
 
 __device__ __forceinline__ bool seg_stream_ok(uint64_t n, uint64_t nb, uint32_t cs) {
   return n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES && nb < (UINT64_C(1) << 29);
-}
-
-// units of each stream: 1, or one per 2^L bits of its header range
-__global__ void rpp_seg_units_kernel(SegArgs a, uint64_t* ucnt) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > a.nblocks) return;
-  if (i == a.nblocks) {
-    ucnt[i] = 0;
-    return;
-  }
-  const uint64_t n = a.n_samples[i], nb = a.in_bytes[i];
-  uint64_t c = 1;
-  if (!*a.guard && seg_stream_ok(n, nb, a.cs))
-    c = (rpp_internal::seg_last_bit((uint32_t)(a.in_off[i] & 3u), nb, n, a.bs, a.cs) >> a.sv.seg_log2) + 1;
-  ucnt[i] = c;
 }
 
 // unit -> stream, and the list capacity of each unit of a split stream: one
@@ -1130,32 +1082,144 @@ uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t ma
   return L;
 }
 
-// The batch against the workspace's promise: the sum and the maximum of the
-// (decodable) streams' sample counts.  A batch larger than promised is
-// decoded one wave per stream (guard = 1): the counting kernels then give
-// every stream one unit and no sub-blocks, so no workspace-indexed write
-// happens, and the fused kernel, which needs no workspace, decodes it all.
-constexpr uint32_t kGuardThreads = 1024;
-__global__ __launch_bounds__(kGuardThreads) void rpp_dec_guard_kernel(const uint64_t* n_samples, uint32_t nblocks,
-                                                                      uint32_t cs, uint64_t total_samples,
-                                                                      uint64_t max_stream_samples, uint32_t* guard) {
+
+
+// ---- the segmented decode's set-up in one workgroup (rpp_seg_plan_kernel) ----
+// It replaces eight small launches and nine fills (~100 us of launch gaps for
+// a single long stream): the workspace promise check (guard), units per
+// stream and their prefix, sub-blocks and tiles per stream and their
+// prefixes, the tiles per hand-out level and their prefix (a histogram of the
+// streams' tile counts), and the zeroed / 0xFF-filled state of the passes.
+constexpr uint32_t kPlanThreads = 1024;
+
+// out[i] = sum_{j<i} in[j] over n entries, by the whole workgroup (4096 per
+// pass: wave scans by shuffles, the wave totals by wave 0, a carried total)
+__device__ void plan_exscan(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* sh) {
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  constexpr uint32_t kPer = 4, kTileN = kPlanThreads * kPer, kW = kPlanThreads / 64;
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < n; base += kTileN) {
+    const uint64_t i0 = base + (uint64_t)kPer * t;
+    uint64_t v[kPer], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      v[k] = i0 + k < n ? in[i0 + k] : 0u;
+      sum += v[k];
+    }
+    uint64_t incl = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint64_t u = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += u;
+    }
+    if (lane == 63) sh[wv] = incl;
+    __syncthreads();
+    if (wv == 0) {
+      const uint64_t x = lane < kW ? sh[lane] : 0u;
+      uint64_t xi = x;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t u = __shfl_up(xi, d, 64);
+        if (lane >= d) xi += u;
+      }
+      if (lane < kW) sh[lane] = xi - x;
+      if (lane == kW - 1) sh[kW] = xi;
+    }
+    __syncthreads();
+    uint64_t run = carry + sh[wv] + incl - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      if (i0 + k < n) out[i0 + k] = run;
+      run += v[k];
+    }
+    carry += sh[kW];
+    __syncthreads();
+  }
+}
+
+struct PlanArgs {
+  SegArgs a;
+  uint64_t total_samples, max_stream_samples;
+  uint32_t* guard;
+  uint64_t *ucnt, *sb_cnt, *tile_cnt, *tile_base, *lvl_cnt, *lvl_base;
+  uint32_t levels, chunk_len;
+  uint64_t* tile_state;
+  uint64_t max_tiles;
+  uint32_t* counter;
+  uint64_t *pl_cnt, *cnt2;
+};
+
+__global__ __launch_bounds__(kPlanThreads) void rpp_seg_plan_kernel(PlanArgs q) {
+  using namespace rpp_internal;
+  __shared__ uint64_t sh[kPlanThreads / 64 + 1];
   __shared__ uint32_t bad;
   __shared__ unsigned long long sum;
-  if (threadIdx.x == 0) {
+  const SegArgs& a = q.a;
+  const uint32_t t = threadIdx.x, B = a.nblocks;
+  const uint64_t U = a.sv.units_max;
+  // the pass state: tile look-back states and counters zeroed, unit states
+  // 0xFF (a unit's guess word kSegNone = not searched)
+  for (uint64_t i = t; i < q.max_tiles; i += kPlanThreads) q.tile_state[i] = 0;
+  for (uint64_t i = t; i <= U; i += kPlanThreads) {
+    q.pl_cnt[i] = 0;
+    q.cnt2[i] = 0;
+  }
+  for (uint64_t i = t; i < U * kUsWords; i += kPlanThreads) a.sv.ustate[i] = 0xFFFFFFFFu;
+  for (uint32_t i = t; i < B; i += kPlanThreads) {
+    a.sv.sst[i] = 0;
+    a.sv.sflags[i] = 0;
+  }
+  if (t == 0) {
+    *q.counter = 0;
+    *a.sv.queue = 0;
     bad = 0;
     sum = 0;
   }
   __syncthreads();
+  // the batch against the workspace's promise (rpp_decode_workspace_bytes):
+  // broken, every stream is decoded one wave each (one unit, no sub-blocks)
   unsigned long long part = 0;
-  for (uint32_t i = threadIdx.x; i < nblocks; i += kGuardThreads) {
-    const uint64_t n = n_samples[i];
-    if (n % cs != 0 || n >= RPP_MAX_STREAM_SAMPLES) continue;  // (not decodable: reported by the kernels)
+  for (uint32_t i = t; i < B; i += kPlanThreads) {
+    const uint64_t n = a.n_samples[i];
+    if (n % a.cs != 0 || n >= RPP_MAX_STREAM_SAMPLES) continue;  // (not decodable: reported by the kernels)
     part += n;
-    if (n > max_stream_samples) bad = 1;
+    if (n > q.max_stream_samples) bad = 1;
   }
   atomicAdd(&sum, part);
   __syncthreads();
-  if (threadIdx.x == 0) *guard = (bad || sum > total_samples) ? 1u : 0u;
+  const bool guard = bad || sum > q.total_samples;
+  if (t == 0) *q.guard = guard ? 1u : 0u;
+  // units (one per 2^L bits of a stream's header range, 1 for short or
+  // undecodable streams), sub-blocks + 1 and tiles of the split streams
+  for (uint32_t i = t; i <= B; i += kPlanThreads) {
+    uint64_t c = 0, nsb = 0;
+    if (i < B) {
+      const uint64_t n = a.n_samples[i], nb = a.in_bytes[i];
+      c = 1;
+      if (!guard && seg_stream_ok(n, nb, a.cs))
+        c = (seg_last_bit((uint32_t)(a.in_off[i] & 3u), nb, n, a.bs, a.cs) >> a.sv.seg_log2) + 1;
+      if (!guard && c > 1) nsb = (n + q.chunk_len - 1) / q.chunk_len * a.cs;
+    }
+    q.ucnt[i] = c;
+    q.sb_cnt[i] = i < B ? nsb + 1 : 0;
+    q.tile_cnt[i] = (nsb + kTile - 1) / kTile;
+  }
+  // histogram of the tile counts (into lvl_base) for the levels
+  for (uint32_t l = t; l <= q.levels; l += kPlanThreads) q.lvl_base[l] = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < B; i += kPlanThreads)
+    atomicAdd(reinterpret_cast<unsigned long long*>(&q.lvl_base[(size_t)std::min<uint64_t>(q.tile_cnt[i], q.levels)]),
+              1ull);
+  __syncthreads();
+  plan_exscan(q.ucnt, (uint64_t)B + 1, const_cast<uint64_t*>(a.sv.unit_base), sh);
+  plan_exscan(q.sb_cnt, (uint64_t)B + 1, const_cast<uint64_t*>(a.sb_base), sh);
+  plan_exscan(q.tile_cnt, (uint64_t)B + 1, q.tile_base, sh);
+  plan_exscan(q.lvl_base, (uint64_t)q.levels + 1, q.lvl_cnt, sh);  // streams with <= l - 1 tiles
+  // streams with more than l tiles = B - (streams with <= l tiles)
+  for (uint32_t l = t; l <= q.levels; l += kPlanThreads)
+    q.lvl_cnt[l] = l < q.levels ? (uint64_t)B - (q.lvl_cnt[l] + q.lvl_base[l]) : 0u;
+  __syncthreads();
+  plan_exscan(q.lvl_cnt, (uint64_t)q.levels + 1, q.lvl_base, sh);
 }
 
 }  // namespace
@@ -1237,22 +1301,11 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
   a.nblocks = nblocks;
   a.bs = cfg->block_size;
   a.cs = cfg->component_stream_count;
-  hipLaunchKernelGGL(rpp_dec_guard_kernel, dim3(1), dim3(kGuardThreads), 0, s, d_n_samples, nblocks,
-                     cfg->component_stream_count, total_samples, max_stream_samples, w.guard);
-  hipLaunchKernelGGL(rpp_seg_units_kernel, dim3(g256), dim3(256), 0, s, a, w.ucnt);
-  if ((st = rpp_exclusive_scan_u64(w.ucnt, (uint64_t)nblocks + 1, w.unit_base, s)) != RPP_OK) return st;
-  hipLaunchKernelGGL(rpp_dec_count_kernel, dim3(g256), dim3(256), 0, s, d_n_samples, nblocks, chunk_len,
-                     cfg->component_stream_count, w.sb_cnt, w.tile_cnt, (const uint64_t*)w.ucnt,
-                     (const uint32_t*)w.guard);
-  if ((st = rpp_exclusive_scan_u64(w.sb_cnt, (uint64_t)nblocks + 1, w.sb_base, s)) != RPP_OK) return st;
-  if ((st = rpp_exclusive_scan_u64(w.tile_cnt, (uint64_t)nblocks + 1, w.tile_base, s)) != RPP_OK) return st;
-  hipLaunchKernelGGL(rpp_dec_level_count_kernel, dim3(w.levels + 1), dim3(kLvlThreads), 0, s, w.tile_cnt, nblocks,
-                     w.levels, w.lvl_cnt);
-  if ((st = rpp_exclusive_scan_u64(w.lvl_cnt, (uint64_t)w.levels + 1, w.lvl_base, s)) != RPP_OK) return st;
+  PlanArgs q{a, total_samples, max_stream_samples, w.guard, w.ucnt, w.sb_cnt, w.tile_cnt, w.tile_base, w.lvl_cnt,
+             w.lvl_base, w.levels, chunk_len, w.tile_state, w.max_tiles, w.counter, w.pl_cnt, w.cnt2};
+  hipLaunchKernelGGL(rpp_seg_plan_kernel, dim3(1), dim3(kPlanThreads), 0, s, q);
   hipLaunchKernelGGL(rpp_dec_level_map_kernel, dim3(w.levels), dim3(kLvlThreads), 0, s, w.tile_cnt, nblocks,
                      w.levels, w.lvl_base, w.tile_map, w.tile_lt);
-  if (hipMemsetAsync(w.tile_state, 0, w.max_tiles * 8, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (hipMemsetAsync(w.counter, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
   // the streams that fit one unit (all of them when the guard tripped): one
   // wave each, parse and values fused, on the side stream while the units are
   // parsed
@@ -1263,15 +1316,9 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
                                          fused_waves ? fused_waves : kDecSideWaves);
   if (st != RPP_OK) return st;
   const uint64_t U = w.units_max;
-  if (hipMemsetAsync(w.pl_cnt, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (hipMemsetAsync(w.cnt2, 0, (U + 1) * 8, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (hipMemsetAsync(w.sst, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (hipMemsetAsync(w.sflags, 0, (size_t)nblocks * 4, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (hipMemsetAsync(w.queue, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
   const uint32_t gu = (uint32_t)((U + 255) / 256);
   hipLaunchKernelGGL(rpp_seg_map_kernel, dim3(gu), dim3(256), 0, s, a, w.unit_map, w.pl_cnt);
   if ((st = rpp_exclusive_scan_u64(w.pl_cnt, U + 1, w.pl_base, s)) != RPP_OK) return st;
-  if (hipMemsetAsync(w.ustate, 0xFF, U * rpp_internal::kUsWords * 4, s) != hipSuccess) return RPP_HIP_ERROR;
   // few units: their first guesses by several waves each, before pass 0
   if ((st = rpp_internal::launch_seg_guess(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_n_samples, a.sv, s)) !=
       RPP_OK)
