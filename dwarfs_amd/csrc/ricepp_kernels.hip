@@ -2158,20 +2158,23 @@ __device__ __forceinline__ uint32_t seg_sb_end_wave(const uint32_t* st, const ui
 // in the staged words: a chain that reaches their end after kGuessMinSteps
 // sub-blocks is finished (a survivor that is checked no further here).
 // A wrong guess costs time, never a wrong result.
-constexpr uint32_t kSlotsPerGuess = 4;  // candidates per lane of a 256-candidate chunk
+constexpr uint32_t kSlotsPerGuess = 4;  // candidates per lane of a chunk (one wave: 256-candidate chunks)
 constexpr uint32_t kGuessWaveMax = 12;  // survivors below which seg_guess parses wave-parallel
 constexpr uint32_t kGuessMinSteps = 4;  // sub-blocks a chain must pass before the staged words may end it
 constexpr uint32_t kGuessFin = 1u << 31;  // (list word 2: the chain is finished)
-// (chunk0, chunk_step: this wave's share of the 256-candidate chunks when
+// (chunk0, chunk_step: this wave's share of the chunks when
 // several waves search one unit -- rpp_seg_guess_kernel -- with `best`, the
 // lowest survivor any of them found so far, in LDS: a wave stops at chunks
 // beyond it)
+// (kSlots: candidates per lane of a chunk; the multi-wave search takes
+// smaller chunks, so that its waves cover the candidates in more, shorter
+// lane-serial passes)
+template <uint32_t kSlots = kSlotsPerGuess>
 __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list, uint32_t end_rel, uint32_t bs,
                                               uint32_t lane, uint32_t c_first, uint32_t range, const uint4* tab,
                                               uint32_t chunk0 = 0, uint32_t chunk_step = 1, uint32_t* best = nullptr,
                                               uint32_t steps = rpp_internal::kSpecSteps) {
   using rpp_internal::kSegNone;
-  constexpr uint32_t kSlots = kSlotsPerGuess;
   const uint32_t maxsb = 4u + 16u * bs;
   auto peek = [&](uint32_t r) {
     const uint32_t* w = st + (r >> 5);
@@ -2257,13 +2260,17 @@ __device__ __forceinline__ uint32_t seg_guess(const uint32_t* st, uint32_t* list
         fin[i] = fin[i] || (bad && may_finish);
         rice[i] = r && !bad && ncode[i] < bs;
       };
+      static_assert(kSlots == 2 || kSlots == 4, "seg_guess: 2 or 4 candidates per lane");
       for (;;) {
-        const bool more = rice[0] || rice[1] || rice[2] || rice[3];
+        bool more = rice[0] || rice[1];
+        if constexpr (kSlots == 4) more = more || rice[2] || rice[3];
         if (__ballot(more) == 0) break;
         codes(0);
         if (nslots > 1) codes(1);
-        if (nslots > 2) codes(2);
-        if (nslots > 3) codes(3);
+        if constexpr (kSlots == 4) {
+          if (nslots > 2) codes(2);
+          if (nslots > 3) codes(3);
+        }
       }
       // compact the survivors (in candidate order) into the first slots
       uint32_t cnt = 0;
@@ -2953,14 +2960,15 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
 
 // The first guess of every unit j >= 1 of a split stream, searched by
 // kGuessWaves waves at once (one workgroup per unit): wave w takes the
-// 256-candidate chunks w, w + kGuessWaves, ... of seg_guess's search and
+// 128-candidate chunks w, w + kGuessWaves, ... of seg_guess's search and
 // stops at chunks beyond the lowest survivor any wave has found (LDS); the
 // unit's guess is that lowest survivor, the candidate the one-wave search
 // returns.  For batches of few units (single long streams), where
 // the parse's work queue would run one wave per CU and the lane-serial guess
 // is most of a unit's time.
 constexpr uint32_t kGuessWaves = 8;
-constexpr uint32_t kGuessListWords = 2 * kSlotsPerGuess * kWave;  // a wave's survivors: (position, origin | range)
+constexpr uint32_t kGuessSlots = 2;  // candidates per lane of a chunk (128-candidate chunks)
+constexpr uint32_t kGuessListWords = 2 * kGuessSlots * kWave;  // a wave's survivors: (position, origin | range)
 __host__ __device__ constexpr size_t guess_lds_bytes(uint32_t bs) {
   // (the staged words of parse_wave_words, once per workgroup: 76 KiB at bs <= 128, two workgroups per CU)
   return kTabBytes + 4 * ((size_t)parse_wave_words(bs) - (kListLead + kListWords) + kGuessWaves * kGuessListWords);
@@ -3012,7 +3020,7 @@ __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(Parse
       if (threadIdx.x == 0) best = kSegNone;
       __syncthreads();
     }
-    (void)seg_guess(ring, list, end_rel, p.bs, lane, 0, k & 1 ? 5u : 3u, tab, wv, kGuessWaves, &best,
+    (void)seg_guess<kGuessSlots>(ring, list, end_rel, p.bs, lane, 0, k & 1 ? 5u : 3u, tab, wv, kGuessWaves, &best,
                     k < 2 ? kSpecVerify : kSpecSteps);
     __syncthreads();
     g = best;
