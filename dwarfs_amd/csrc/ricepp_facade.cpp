@@ -16,6 +16,7 @@
 #include <atomic>
 #include <cctype>
 #include <charconv>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -57,6 +58,12 @@ size_t align16(size_t v) { return (v + 15) & ~size_t{15}; }
 
 std::atomic<uint64_t> g_enc_launches{0}, g_enc_blocks{0}, g_dec_launches{0}, g_dec_blocks{0}, g_ctx_created{0};
 std::atomic<uint32_t> g_ctx_faults{0};  // inject_context_failures
+std::atomic<uint64_t> g_stage_ns{0}, g_device_ns{0}, g_finish_ns{0};
+inline uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 int current_device() {
   int d = 0;
@@ -331,12 +338,14 @@ class batch_queue {
       device_guard g{dev_};
       if (encode_) launch_encode(lk, b, self, *ctx);
       else launch_decode(lk, b, self, *ctx);
+      const uint64_t tf = now_ns();
       lk.lock();
       // the leader copies its own result out, then waits for the others
       // before the pinned buffers go back to the pool (with the lease)
       if (self.state == RESULT && self.counts == &counts) copy_out(lk, self);
       counts.cv.wait(lk, [&] { return counts.to_finish == 0; });
       lk.unlock();
+      g_finish_ns.fetch_add(now_ns() - tf, std::memory_order_relaxed);
     } catch (std::exception const& e) {
       // thrown before stage_in handed out slots or after every request was
       // STAGED (launch_* only throws outside stage_in): no caller is copying
@@ -422,7 +431,9 @@ class batch_queue {
     const uint64_t ws_bytes = rpp_encode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
     uint8_t* pout_dev = ctx.device_view(pout);
+    const uint64_t t0 = now_ns();
     stage_in(lk, b, self, pin, in_off);
+    const uint64_t t1 = now_ns();
     auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
     auto* dst = reinterpret_cast<int32_t*>(d + in_total + (6 * nb + 1) * 8);
     uint8_t* dslots = d + in_total + arr;
@@ -439,6 +450,8 @@ class batch_queue {
     g_enc_launches.fetch_add(1, std::memory_order_relaxed);
     g_enc_blocks.fetch_add(nb, std::memory_order_relaxed);
     ctx.sync();
+    g_stage_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
+    g_device_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);
     auto const* r64 = reinterpret_cast<uint64_t const*>(pout + out_total);  // out_bytes | dst_off | total
     auto const* hst = reinterpret_cast<int32_t const*>(pout + out_total + (3 * nb + 1) * 8);
     for (size_t i = 0; i < nb; ++i) {
@@ -483,7 +496,9 @@ class batch_queue {
     // long blocks (16 MiB DwarFS blocks) are parsed in segments by several waves
     const uint64_t ws_bytes = rpp_decode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
+    const uint64_t t0 = now_ns();
     stage_in(lk, b, self, pin, in_off);
+    const uint64_t t1 = now_ns();
     auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
     auto* dst = reinterpret_cast<int32_t*>(d + in_total + 4 * nb * 8);
     uint8_t* dout = d + in_total + 4 * nb * 8 + st_bytes;
@@ -496,6 +511,8 @@ class batch_queue {
     g_dec_launches.fetch_add(1, std::memory_order_relaxed);
     g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);
     ctx.sync();
+    g_stage_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
+    g_device_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);
     auto const* hst = reinterpret_cast<int32_t const*>(pout);
     for (size_t i = 0; i < nb; ++i) {
       b[i]->status = hst[i];
@@ -662,7 +679,7 @@ void inject_context_failures(uint32_t n) { g_ctx_faults.store(n); }
 
 facade_stats get_facade_stats() {
   return facade_stats{g_enc_launches.load(), g_enc_blocks.load(), g_dec_launches.load(), g_dec_blocks.load(),
-                      g_ctx_created.load()};
+                      g_ctx_created.load(),     g_stage_ns.load(),   g_device_ns.load(),     g_finish_ns.load()};
 }
 
 // ---- block_compressor (src/compression/ricepp.cpp:57-182, 272-296) ----

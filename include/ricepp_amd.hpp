@@ -180,6 +180,10 @@ class pcm_sample_transformer {
 struct facade_stats {
   uint64_t encode_launches, encode_blocks, decode_launches, decode_blocks;
   uint64_t contexts_created;
+  // summed over batches (ns): callers copying their inputs into the pinned
+  // staging, the device part (copies and kernels, one synchronisation), and
+  // callers copying their results out
+  uint64_t stage_ns, device_ns, finish_ns;
 };
 facade_stats get_facade_stats();
 

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <span>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -336,7 +337,11 @@ int bench(int argc, char** argv) {
     v.resize(n);
     for (auto& x : v) x = bswap((uint16_t)pois(rng));
   }
-  std::vector<std::vector<uint8_t>> enc(blocks);
+  // (encoded into preallocated worst-case buffers through the span form, as
+  // the plugin does: src/compression/ricepp.cpp:134-137)
+  size_t const wc = ricepp_amd::create_encoder<uint16_t>(c)->worst_case_encoded_bytes(n);
+  std::vector<std::vector<uint8_t>> encbuf(blocks, std::vector<uint8_t>(wc));
+  std::vector<std::span<uint8_t>> enc(blocks);
   std::vector<std::vector<uint16_t>> out(blocks, std::vector<uint16_t>(n));
   for (int T : threads) {
     auto run = [&](bool encode) {
@@ -347,7 +352,7 @@ int bench(int argc, char** argv) {
           auto e = ricepp_amd::create_encoder<uint16_t>(c);
           auto d = ricepp_amd::create_decoder<uint16_t>(c);
           for (size_t b = t; b < blocks; b += T) {
-            if (encode) enc[b] = e->encode(in[b]);
+            if (encode) enc[b] = e->encode(std::span<uint8_t>{encbuf[b]}, in[b]);
             else d->decode(out[b], enc[b]);
           }
         });
@@ -365,11 +370,15 @@ int bench(int argc, char** argv) {
     bool ok = true;
     for (size_t b = 0; b < blocks; ++b) ok = ok && out[b] == in[b];
     double gib = double(blocks) * n * 2 / double(1ull << 30);
+    const double ne = double(s1.encode_launches - s0.encode_launches), nd = double(s2.decode_launches - s1.decode_launches);
     std::printf("{\"facade_bench\": true, \"threads\": %d, \"blocks\": %zu, \"block_bytes\": %zu, "
-                "\"encode_GiBps\": %.3f, \"decode_GiBps\": %.3f, \"encode_launches\": %llu, "
-                "\"decode_launches\": %llu, \"roundtrip_ok\": %s}\n",
-                T, blocks, n * 2, gib / te, gib / td, (unsigned long long)(s1.encode_launches - s0.encode_launches),
-                (unsigned long long)(s2.decode_launches - s1.decode_launches), ok ? "true" : "false");
+                "\"encode_GiBps\": %.3f, \"decode_GiBps\": %.3f, \"encode_launches\": %.0f, "
+                "\"decode_launches\": %.0f, \"encode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, \"finish\": %.1f}, "
+                "\"decode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, \"finish\": %.1f}, \"roundtrip_ok\": %s}\n",
+                T, blocks, n * 2, gib / te, gib / td, ne, nd, (s1.stage_ns - s0.stage_ns) / 1e3 / ne,
+                (s1.device_ns - s0.device_ns) / 1e3 / ne, (s1.finish_ns - s0.finish_ns) / 1e3 / ne,
+                (s2.stage_ns - s1.stage_ns) / 1e3 / nd, (s2.device_ns - s1.device_ns) / 1e3 / nd,
+                (s2.finish_ns - s1.finish_ns) / 1e3 / nd, ok ? "true" : "false");
     std::fflush(stdout);
     if (!ok) return 1;
   }
