@@ -23,6 +23,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 
 namespace ricepp_amd {
@@ -105,6 +106,11 @@ class device_ctx {
       if (g_ctx_faults.compare_exchange_weak(n, n - 1)) throw std::runtime_error("hipStreamCreate: injected failure");
     device_guard g{dev_};
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    // the batch's end (polled by the batch_queue)
+    if (hipEventCreateWithFlags(&event_, hipEventDisableTiming) != hipSuccess) {
+      (void)hipStreamDestroy(stream_);
+      throw std::runtime_error("ricepp_amd: hipEventCreateWithFlags failed");
+    }
     g_ctx_created.fetch_add(1, std::memory_order_relaxed);
   }
   device_ctx(device_ctx const&) = delete;
@@ -112,6 +118,7 @@ class device_ctx {
 
   int device() const { return dev_; }
   hipStream_t stream() const { return stream_; }
+  hipEvent_t event() const { return event_; }
   uint8_t* dev(size_t bytes) { return grow_dev(dbuf_, dcap_, bytes); }
   uint8_t* workspace(size_t bytes) { return grow_dev(wbuf_, wcap_, bytes); }
   uint8_t* pin_in(size_t bytes) { return grow_pinned(hin_, hin_cap_, bytes); }
@@ -166,6 +173,7 @@ class device_ctx {
 
   int dev_;
   hipStream_t stream_ = nullptr;
+  hipEvent_t event_ = nullptr;
   uint8_t* dbuf_ = nullptr;
   size_t dcap_ = 0;
   uint8_t* wbuf_ = nullptr;
@@ -220,24 +228,27 @@ class ctx_lease {
   device_ctx* c_;
 };
 
-// ---- combining batch queue ----
+// ---- pipelined batch queue ----
 //
-// A request moves QUEUED -> TAKEN (in a batch) -> ASSIGNED (its pinned input
-// slot is known: the caller copies its input in) -> STAGED -> RESULT (its
-// pinned output slot is filled: the caller copies its output out) -> DONE.
-// The first waiting caller that finds a free launch slot takes everything
-// queued (up to the batch caps) and drives the launch; every caller does its
-// own host copies, in parallel.  The leader only touches a request through
-// the batch's counters once the request may have returned.  Up to kMaxActive
-// batches of one queue are in flight at once, each on its own pooled context
-// (stream), and each costs one host synchronisation.
-enum req_state { QUEUED, TAKEN, ASSIGNED, STAGED, RESULT, DONE };
-
-struct batch_counts {
-  size_t to_stage = 0;   // requests not yet STAGED
-  size_t to_finish = 0;  // requests not yet DONE
-  std::condition_variable cv;  // the leader waits here
-};
+// DwarFS calls the codec synchronously from a pool of worker threads, one
+// block per call (filesystem_writer.cpp:255-287, block_cache.cpp:628-706).
+// Concurrent calls of one (device, configuration, direction) are gathered
+// into batches, each batch one launch on a pooled context:
+//   * a caller reserves its slot in the open batch's pinned staging and
+//     copies its input in -- in parallel with the other callers, no waiting;
+//   * the open batch is closed as soon as fewer than g_max_active batches are
+//     on the device (an idle queue launches a lone call at once, a busy one
+//     gathers everything that arrives meanwhile), or when it is full;
+//   * the queue's driver thread launches a closed batch once every caller has
+//     copied in (copies and kernels enqueued, an event recorded), polls the
+//     events of the batches in flight, and publishes each batch's results
+//     with one wake-up of all its callers;
+//   * every caller copies its own result out; the last one returns the
+//     context to the pool.
+// So a call costs one reservation, two copies and one futex wait; no caller
+// ever makes a HIP call or waits on the device, and the device keeps up to
+// g_max_active batches in flight.
+struct batch;
 
 struct request {
   // encode: in = samples, out = caller's output; decode: in = stream bytes,
@@ -247,24 +258,40 @@ struct request {
   uint8_t* out;
   size_t out_cap;  // encode: output span size; decode: exact sample bytes
   uint64_t n_samples;
-  // set by the leader
+  // set by the queue (the results before the batch's `done` is raised)
   uint8_t* pin_in = nullptr;
   uint8_t const* pin_out = nullptr;
+  size_t in_off = 0, out_off = 0;
   size_t result_bytes = 0;
   int status = RPP_OK;
   std::string error;  // HIP failure text
-  req_state state = QUEUED;
-  batch_counts* counts = nullptr;
-  std::condition_variable cv;  // its caller waits here (woken individually: no notify_all storms)
+};
+
+struct batch {
+  device_ctx* ctx = nullptr;
+  std::vector<request*> reqs;
+  uint8_t* pin_in = nullptr;   // [inputs][parameter arrays]
+  uint8_t* pin_out = nullptr;  // [outputs][sizes / statuses]
+  size_t in_cap = 0, out_cap = 0;
+  size_t in_fill = 0, out_fill = 0;  // reserved bytes (16-aligned slots)
+  uint64_t total_samples = 0, max_samples = 0;
+  size_t staged = 0;  // (mutex)
+  bool closed = false;
+  std::atomic<uint32_t> done{0};      // results published (callers wait on it)
+  std::atomic<size_t> finished{0};    // callers that have copied out
+  uint64_t t_close = 0, t_launch = 0, t_done = 0;
 };
 
 constexpr size_t kMaxBatchBlocks = 8192;
-constexpr size_t kMaxBatchBytes = size_t{512} << 20;  // input + output bytes per launch
-// launches in flight per queue: HIP maps a process's streams onto
-// GPU_MAX_HW_QUEUES hardware queues (4 by default), so more concurrent launches
-// only queue behind each other on the device (measured: 16 in flight took the
-// 64-thread decode from 4.5 to 1.4 GiB/s); fewer, bigger batches win
-constexpr int kMaxActive = 4;
+// pinned staging per batch (a larger single request gets a batch of its own size)
+constexpr size_t kBatchIn = size_t{8} << 20;
+constexpr size_t kBatchOut = size_t{16} << 20;
+// batches of one queue on the device at once (set_facade_pipeline_depth
+// changes it for benchmarks)
+std::atomic<int> g_max_active{2};
+// batches alive per queue beyond those on the device (open + being copied
+// out); a caller that finds none with room waits for one to be released
+constexpr int kSpareBatches = 2;
 
 class batch_queue {
  public:
@@ -272,262 +299,315 @@ class batch_queue {
 
   void run(request& r) {
     std::unique_lock<std::mutex> lk(mu_);
-    pending_.push_back(&r);
-    for (;;) {
-      switch (r.state) {
-        case DONE: return;
-        case ASSIGNED: copy_in(lk, r); continue;
-        case RESULT: copy_out(lk, r); return;
-        case QUEUED:
-          if (active_ < kMaxActive) {
-            lead(lk, r);
-            continue;
-          }
-          break;
-        default: break;
-      }
-      r.cv.wait(lk);
+    if (!driver_started_) {
+      std::thread([this] { drive(); }).detach();  // (lives as long as the queue: forever)
+      driver_started_ = true;
+    }
+    batch* b = reserve(lk, r);  // (may throw: nothing holds r yet)
+    lk.unlock();
+    if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
+    lk.lock();
+    ++b->staged;
+    if (!b->closed && inflight_ < g_max_active.load(std::memory_order_relaxed)) close(b);
+    else if (b->closed && b->staged == b->reqs.size()) make_ready(b);
+    lk.unlock();
+    while (!b->done.load(std::memory_order_acquire)) b->done.wait(0, std::memory_order_acquire);
+    if (r.status == RPP_OK && r.result_bytes) std::memcpy(r.out, r.pin_out, r.result_bytes);
+    if (b->finished.fetch_add(1, std::memory_order_acq_rel) + 1 == b->reqs.size()) {
+      lk.lock();
+      release(b);
     }
   }
 
  private:
-  // bytes a request moves through a launch (input, and output capacity)
-  size_t footprint(request const* q) const {
-    return q->in_bytes + (encode_ ? rpp_worst_case_bytes(&cfg_, q->n_samples) : q->out_cap);
+  static size_t arrays_in(size_t nb) { return 4 * nb * 8 + 64; }
+  static size_t arrays_out(size_t nb) { return (6 * nb + 1) * 8 + align16(nb * 4) + 64; }
+  size_t need_in(request const& r) const { return align16(r.in_bytes); }
+  size_t need_out(request const& r) const {
+    return encode_ ? align16(rpp_worst_case_bytes(&cfg_, r.n_samples)) + 16 : align16(r.out_cap);
   }
-  void copy_in(std::unique_lock<std::mutex>& lk, request& r) {
-    lk.unlock();
-    if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
-    lk.lock();
-    r.state = STAGED;
-    if (--r.counts->to_stage == 0) r.counts->cv.notify_one();
-  }
-  void copy_out(std::unique_lock<std::mutex>& lk, request& r) {
-    lk.unlock();
-    if (r.status == RPP_OK && r.result_bytes) std::memcpy(r.out, r.pin_out, r.result_bytes);
-    lk.lock();
-    r.state = DONE;
-    batch_counts* c = r.counts;  // (r may be gone once DONE is seen)
-    if (--c->to_finish == 0) c->cv.notify_one();
+  bool fits(batch const* b, request const& r) const {
+    const size_t nb = b->reqs.size() + 1;
+    return nb <= kMaxBatchBlocks && b->in_fill + need_in(r) + arrays_in(nb) <= b->in_cap &&
+           b->out_fill + need_out(r) + arrays_out(nb) <= b->out_cap;
   }
 
-  // Takes a batch from the queue and drives it (lk held on entry and exit).
-  // `self` is the leader's own request, which may or may not be in the batch.
-  // Every exit path publishes a result to every request of the batch, waits
-  // until all of them are DONE, and gives the launch slot back.
-  void lead(std::unique_lock<std::mutex>& lk, request& self) {
-    std::vector<request*> b;
-    size_t bytes = 0;
-    while (!pending_.empty() && b.size() < kMaxBatchBlocks &&
-           (b.empty() || bytes + footprint(pending_.front()) <= kMaxBatchBytes)) {
-      request* q = pending_.front();
-      pending_.pop_front();
-      bytes += footprint(q);
-      q->state = TAKEN;
-      b.push_back(q);
-    }
-    batch_counts counts;
-    counts.to_stage = counts.to_finish = b.size();
-    for (request* q : b) q->counts = &counts;
-    ++active_;
-    // another caller may lead the next batch meanwhile
-    if (!pending_.empty() && active_ < kMaxActive) pending_.front()->cv.notify_one();
-    lk.unlock();
-    try {
-      ctx_lease ctx{dev_};  // (may throw: no request has a slot yet)
-      device_guard g{dev_};
-      if (encode_) launch_encode(lk, b, self, *ctx);
-      else launch_decode(lk, b, self, *ctx);
-      const uint64_t tf = now_ns();
-      lk.lock();
-      // the leader copies its own result out, then waits for the others
-      // before the pinned buffers go back to the pool (with the lease)
-      if (self.state == RESULT && self.counts == &counts) copy_out(lk, self);
-      counts.cv.wait(lk, [&] { return counts.to_finish == 0; });
-      lk.unlock();
-      g_finish_ns.fetch_add(now_ns() - tf, std::memory_order_relaxed);
-    } catch (std::exception const& e) {
-      // thrown before stage_in handed out slots or after every request was
-      // STAGED (launch_* only throws outside stage_in): no caller is copying
-      lk.lock();
-      for (request* q : b)
-        if (q->state == TAKEN) {
-          q->state = STAGED;
-          --counts.to_stage;
-        }
-      for (request* q : b) {
-        if (q->state == RESULT || q->state == DONE) continue;
-        q->status = RPP_HIP_ERROR;
-        q->error = e.what();
-        q->result_bytes = 0;
-        q->state = RESULT;
-        if (q != &self) q->cv.notify_one();
+  // A slot in the open batch for r (lk held); opens a batch when there is
+  // none with room, waiting while g_max_active + kSpareBatches are alive.
+  batch* reserve(std::unique_lock<std::mutex>& lk, request& r) {
+    for (;;) {
+      batch* b = open_;
+      if (b && fits(b, r)) break;
+      if (b && b->reqs.empty()) discard(b);  // (a spare sized for another request)
+      else if (b) close(b);                  // full: it goes out as it is
+      if (alive_ < g_max_active.load(std::memory_order_relaxed) + kSpareBatches) {
+        open_batch(lk, r);
+        continue;
       }
-      if (self.state == RESULT && self.counts == &counts) copy_out(lk, self);
-      counts.cv.wait(lk, [&] { return counts.to_finish == 0; });
+      res_cv_.wait(lk);
+    }
+    batch* b = open_;
+    r.in_off = b->in_fill;
+    r.out_off = b->out_fill;
+    r.pin_in = b->pin_in + r.in_off;
+    b->in_fill += need_in(r);
+    b->out_fill += need_out(r);
+    b->total_samples += r.n_samples;
+    b->max_samples = std::max<uint64_t>(b->max_samples, r.n_samples);
+    b->reqs.push_back(&r);
+    return b;
+  }
+
+  void open_batch(std::unique_lock<std::mutex>& lk, request const& r) {
+    ++alive_;  // (counted while the context comes up unlocked)
+    lk.unlock();
+    device_ctx* c = nullptr;
+    auto* b = new batch;
+    try {
+      c = ctx_pool::get().acquire(dev_);
+      b->in_cap = std::max(kBatchIn, need_in(r) + arrays_in(1));
+      b->out_cap = std::max(kBatchOut, need_out(r) + arrays_out(1));
+      device_guard g{dev_};
+      b->pin_in = c->pin_in(b->in_cap);
+      b->pin_out = c->pin_out(b->out_cap);
+      b->ctx = c;
+    } catch (...) {
+      if (c) ctx_pool::get().release(c);
+      delete b;
+      lk.lock();
+      --alive_;
+      res_cv_.notify_all();
+      throw;
+    }
+    lk.lock();
+    if (open_) spare_.push_back(b);  // another caller opened one meanwhile: keep ours for later
+    else open_ = b;
+  }
+
+  // (lk held) an open batch that nobody joined and that is too small for the
+  // request at hand
+  void discard(batch* b) {
+    if (open_ == b) open_ = nullptr;
+    device_ctx* c = b->ctx;
+    delete b;
+    --alive_;
+    ctx_pool::get().release(c);
+  }
+
+  // (lk held) no more requests join b
+  void close(batch* b) {
+    b->closed = true;
+    b->t_close = now_ns();
+    ++inflight_;
+    if (open_ == b) {
+      open_ = nullptr;
+      if (!spare_.empty()) {
+        open_ = spare_.back();
+        spare_.pop_back();
+      }
+    }
+    if (b->staged == b->reqs.size()) make_ready(b);
+  }
+
+  // (lk held) closed and every input copied in: the driver launches it
+  void make_ready(batch* b) {
+    ready_.push_back(b);
+    if (driver_idle_) drv_cv_.notify_one();
+  }
+
+  // The driver thread: launches ready batches, polls the oldest batch in
+  // flight, publishes results.
+  void drive() {
+    (void)hipSetDevice(dev_);
+    std::unique_lock<std::mutex> lk(mu_);
+    uint32_t polls = 0;
+    for (;;) {
+      while (!ready_.empty()) {
+        batch* b = ready_.front();
+        ready_.pop_front();
+        b->t_launch = now_ns();
+        lk.unlock();
+        std::string err;
+        try {
+          if (encode_) launch_encode(*b);
+          else launch_decode(*b);
+          hip_check(hipEventRecord(b->ctx->event(), b->ctx->stream()), "hipEventRecord");
+        } catch (std::exception const& e) {
+          err = e.what();
+        }
+        lk.lock();
+        if (err.empty()) {
+          flight_.push_back(b);
+        } else {
+          fail(b, err);
+        }
+      }
+      if (flight_.empty()) {
+        driver_idle_ = true;
+        drv_cv_.wait(lk);
+        driver_idle_ = false;
+        continue;
+      }
+      batch* b = flight_.front();
       lk.unlock();
+      const hipError_t e = hipEventQuery(b->ctx->event());
+      if (e == hipErrorNotReady) {
+        // (yielding the core; after a few ms of one batch the poll backs off)
+        if (++polls < 4096) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        lk.lock();
+        continue;
+      }
+      polls = 0;
+      lk.lock();
+      flight_.pop_front();
+      if (e != hipSuccess) {
+        fail(b, std::string("ricepp_amd: hipEventQuery: ") + hipGetErrorString(e));
+        continue;
+      }
+      if (encode_) results_encode(*b);
+      else results_decode(*b);
+      complete(b);
     }
-    lk.lock();
-    --active_;
-    if (!pending_.empty()) pending_.front()->cv.notify_one();  // the next leader
   }
 
-  // Hands out the pinned input slots and waits until every caller copied in
-  // (lk not held on entry or exit).
-  void stage_in(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self, uint8_t* pin,
-                std::vector<size_t> const& off) {
-    lk.lock();
-    for (size_t i = 0; i < b.size(); ++i) {
-      b[i]->pin_in = pin + off[i];
-      b[i]->state = ASSIGNED;
-      if (b[i] != &self) b[i]->cv.notify_one();
+  void fail(batch* b, std::string const& what) {
+    for (request* q : b->reqs) {
+      q->status = RPP_HIP_ERROR;
+      q->error = what;
+      q->result_bytes = 0;
     }
-    batch_counts* c = b.front()->counts;
-    if (self.state == ASSIGNED && self.counts == c) copy_in(lk, self);
-    c->cv.wait(lk, [&] { return c->to_stage == 0; });
-    lk.unlock();
+    complete(b);
   }
 
-  // Publishes the results (lk not held on entry or exit).
-  void publish(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self) {
-    lk.lock();
-    for (request* q : b) {
-      q->state = RESULT;
-      if (q != &self) q->cv.notify_one();
-    }
-    lk.unlock();
+  // (lk held) every caller of b gets its result; a batch waiting for a free
+  // device slot may close now
+  void complete(batch* b) {
+    b->t_done = now_ns();
+    --inflight_;
+    g_stage_ns.fetch_add(b->t_launch - b->t_close, std::memory_order_relaxed);
+    g_device_ns.fetch_add(b->t_done - b->t_launch, std::memory_order_relaxed);
+    b->done.store(1, std::memory_order_release);
+    b->done.notify_all();
+    if (open_ && !open_->reqs.empty() && inflight_ < g_max_active.load(std::memory_order_relaxed)) close(open_);
   }
 
-  // One synchronisation per batch: the packed encoded bytes go straight from
-  // the pack kernel into mapped pinned memory, the sizes and statuses follow
-  // in one small copy.
-  void launch_encode(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self,
-                     device_ctx& ctx) {
-    const size_t nb = b.size();
-    std::vector<size_t> in_off(nb), out_off(nb);
-    size_t in_total = 0, out_total = 0;
-    uint64_t total_samples = 0, max_samples = 0;
-    for (size_t i = 0; i < nb; ++i) {
-      in_off[i] = in_total;
-      in_total += align16(b[i]->in_bytes);
-      out_off[i] = out_total;
-      out_total += align16(rpp_worst_case_bytes(&cfg_, b[i]->n_samples)) + 16;
-      total_samples += b[i]->n_samples;
-      max_samples = std::max<uint64_t>(max_samples, b[i]->n_samples);
-    }
-    // device: [in][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status][out slots]
-    // pinned in: [in][u64 in_off | n | out_off]   (one H2D copy)
-    // pinned out: [packed bytes][u64 out_bytes | dst_off | total][i32 status]
+  // (lk held) the last caller has copied its result out
+  void release(batch* b) {
+    g_finish_ns.fetch_add(now_ns() - b->t_done, std::memory_order_relaxed);
+    device_ctx* c = b->ctx;
+    delete b;
+    --alive_;
+    res_cv_.notify_all();
+    ctx_pool::get().release(c);  // (the stream is idle: the event covered its last work)
+  }
+
+  // device: [in][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status][out slots]
+  // pinned in: [in][u64 in_off | n | out_off]   (one H2D copy)
+  // pinned out: [packed bytes][u64 out_bytes | dst_off | total][i32 status]
+  // The pack kernel writes the encoded bytes straight into the mapped pinned
+  // output; the sizes and statuses follow in one small copy.
+  void launch_encode(batch& b) {
+    device_ctx& ctx = *b.ctx;
+    const size_t nb = b.reqs.size();
+    const size_t in_total = b.in_fill, out_total = b.out_fill;
     const size_t arr = (6 * nb + 1) * 8 + align16(nb * 4);
-    uint8_t* d = ctx.dev(in_total + arr + out_total + 64);
-    uint8_t* pin = ctx.pin_in(in_total + 3 * nb * 8 + 64);
-    uint8_t* pout = ctx.pin_out(out_total + arr + 64);
-    auto* h64 = reinterpret_cast<uint64_t*>(pin + in_total);
+    auto* h64 = reinterpret_cast<uint64_t*>(b.pin_in + in_total);
     for (size_t i = 0; i < nb; ++i) {
-      h64[i] = in_off[i] / 2;
-      h64[nb + i] = b[i]->n_samples;
-      h64[2 * nb + i] = out_off[i];
+      h64[i] = b.reqs[i]->in_off / 2;
+      h64[nb + i] = b.reqs[i]->n_samples;
+      h64[2 * nb + i] = b.reqs[i]->out_off;
     }
-    const uint64_t ws_bytes = rpp_encode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
+    uint8_t* d = ctx.dev(in_total + arr + out_total + 64);
+    const uint64_t ws_bytes =
+        rpp_encode_workspace_bytes(&cfg_, b.total_samples, b.max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
-    uint8_t* pout_dev = ctx.device_view(pout);
-    const uint64_t t0 = now_ns();
-    stage_in(lk, b, self, pin, in_off);
-    const uint64_t t1 = now_ns();
+    uint8_t* pout_dev = ctx.device_view(b.pin_out);
     auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
     auto* dst = reinterpret_cast<int32_t*>(d + in_total + (6 * nb + 1) * 8);
     uint8_t* dslots = d + in_total + arr;
     hipStream_t s = ctx.stream();
-    hip_check(hipMemcpyAsync(d, pin, in_total + 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode input");
+    hip_check(hipMemcpyAsync(d, b.pin_in, in_total + 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode input");
     int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
-                                 dslots, d64 + 2 * nb, d64 + 3 * nb, dst, total_samples, max_samples, ws, ws_bytes, s);
+                                 dslots, d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes,
+                                 s);
     if (st != RPP_OK) throw_status(st);
     st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
                         d64 + 5 * nb, s);
     if (st != RPP_OK) throw_status(st);
-    hip_check(hipMemcpyAsync(pout + out_total, d64 + 3 * nb, arr - 3 * nb * 8, hipMemcpyDeviceToHost, s),
+    hip_check(hipMemcpyAsync(b.pin_out + out_total, d64 + 3 * nb, arr - 3 * nb * 8, hipMemcpyDeviceToHost, s),
               "D2H encode sizes");
     g_enc_launches.fetch_add(1, std::memory_order_relaxed);
     g_enc_blocks.fetch_add(nb, std::memory_order_relaxed);
-    ctx.sync();
-    g_stage_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
-    g_device_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);
-    auto const* r64 = reinterpret_cast<uint64_t const*>(pout + out_total);  // out_bytes | dst_off | total
-    auto const* hst = reinterpret_cast<int32_t const*>(pout + out_total + (3 * nb + 1) * 8);
+  }
+  void results_encode(batch& b) {
+    const size_t nb = b.reqs.size();
+    auto const* r64 = reinterpret_cast<uint64_t const*>(b.pin_out + b.out_fill);  // out_bytes | dst_off | total
+    auto const* hst = reinterpret_cast<int32_t const*>(b.pin_out + b.out_fill + (3 * nb + 1) * 8);
     for (size_t i = 0; i < nb; ++i) {
-      b[i]->status = hst[i];
-      b[i]->result_bytes = hst[i] == RPP_OK ? r64[i] : 0;
-      b[i]->pin_out = pout + r64[nb + i];
-      if (b[i]->status == RPP_OK && b[i]->result_bytes > b[i]->out_cap) b[i]->status = RPP_OUTPUT_TOO_SMALL;
+      request* q = b.reqs[i];
+      q->status = hst[i];
+      q->result_bytes = hst[i] == RPP_OK ? r64[i] : 0;
+      q->pin_out = b.pin_out + r64[nb + i];
+      if (q->status == RPP_OK && q->result_bytes > q->out_cap) q->status = RPP_OUTPUT_TOO_SMALL;
     }
-    publish(lk, b, self);
   }
 
-  // One synchronisation per batch: one H2D copy (streams and parameters),
-  // one D2H copy (statuses and samples).
-  void launch_decode(std::unique_lock<std::mutex>& lk, std::vector<request*> const& b, request& self,
-                     device_ctx& ctx) {
-    const size_t nb = b.size();
-    std::vector<size_t> in_off(nb), out_off(nb);
-    size_t in_total = 0, out_total = 0;
-    uint64_t total_samples = 0, max_samples = 0;
+  // device: [in][u64 in_off | in_bytes | out_off | n][out samples][i32 status]
+  // pinned in: [in][u64 in_off | in_bytes | out_off | n]   (one H2D copy)
+  // pinned out: [out samples][i32 status]                  (one D2H copy)
+  void launch_decode(batch& b) {
+    device_ctx& ctx = *b.ctx;
+    const size_t nb = b.reqs.size();
+    const size_t in_total = b.in_fill, out_total = b.out_fill;
+    auto* h64 = reinterpret_cast<uint64_t*>(b.pin_in + in_total);
     for (size_t i = 0; i < nb; ++i) {
-      in_off[i] = in_total;
-      in_total += align16(b[i]->in_bytes);
-      out_off[i] = out_total;
-      out_total += align16(b[i]->out_cap);
-      total_samples += b[i]->n_samples;
-      max_samples = std::max<uint64_t>(max_samples, b[i]->n_samples);
+      h64[i] = b.reqs[i]->in_off;
+      h64[nb + i] = b.reqs[i]->in_bytes;
+      h64[2 * nb + i] = b.reqs[i]->out_off / 2;
+      h64[3 * nb + i] = b.reqs[i]->n_samples;
     }
-    // device: [in][u64 in_off | in_bytes | out_off | n][i32 status][out samples]
-    // pinned in: [in][u64 in_off | in_bytes | out_off | n]   (one H2D copy)
-    // pinned out: [i32 status][out samples]                  (one D2H copy)
     const size_t st_bytes = align16(nb * 4);
-    uint8_t* d = ctx.dev(in_total + 4 * nb * 8 + st_bytes + out_total + 64);
-    uint8_t* pin = ctx.pin_in(in_total + 4 * nb * 8 + 64);
-    uint8_t* pout = ctx.pin_out(st_bytes + out_total + 64);
-    auto* h64 = reinterpret_cast<uint64_t*>(pin + in_total);
-    for (size_t i = 0; i < nb; ++i) {
-      h64[i] = in_off[i];
-      h64[nb + i] = b[i]->in_bytes;
-      h64[2 * nb + i] = out_off[i] / 2;
-      h64[3 * nb + i] = b[i]->n_samples;
-    }
+    uint8_t* d = ctx.dev(in_total + 4 * nb * 8 + out_total + st_bytes + 64);
     // long blocks (16 MiB DwarFS blocks) are parsed in segments by several waves
-    const uint64_t ws_bytes = rpp_decode_workspace_bytes(&cfg_, total_samples, max_samples, static_cast<uint32_t>(nb));
+    const uint64_t ws_bytes =
+        rpp_decode_workspace_bytes(&cfg_, b.total_samples, b.max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
-    const uint64_t t0 = now_ns();
-    stage_in(lk, b, self, pin, in_off);
-    const uint64_t t1 = now_ns();
     auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
-    auto* dst = reinterpret_cast<int32_t*>(d + in_total + 4 * nb * 8);
-    uint8_t* dout = d + in_total + 4 * nb * 8 + st_bytes;
+    uint8_t* dout = d + in_total + 4 * nb * 8;
+    auto* dst = reinterpret_cast<int32_t*>(dout + out_total);
     hipStream_t s = ctx.stream();
-    hip_check(hipMemcpyAsync(d, pin, in_total + 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode input");
+    hip_check(hipMemcpyAsync(d, b.pin_in, in_total + 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode input");
     int st = rpp_decode_batch_ws(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb), reinterpret_cast<uint16_t*>(dout),
-                                 d64 + 2 * nb, d64 + 3 * nb, dst, total_samples, max_samples, ws, ws_bytes, s);
+                                 d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes, s);
     if (st != RPP_OK) throw_status(st);
-    hip_check(hipMemcpyAsync(pout, dst, st_bytes + out_total, hipMemcpyDeviceToHost, s), "D2H decoded");
+    hip_check(hipMemcpyAsync(b.pin_out, dout, out_total + st_bytes, hipMemcpyDeviceToHost, s), "D2H decoded");
     g_dec_launches.fetch_add(1, std::memory_order_relaxed);
     g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);
-    ctx.sync();
-    g_stage_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
-    g_device_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);
-    auto const* hst = reinterpret_cast<int32_t const*>(pout);
-    for (size_t i = 0; i < nb; ++i) {
-      b[i]->status = hst[i];
-      b[i]->result_bytes = hst[i] == RPP_OK ? b[i]->out_cap : 0;
-      b[i]->pin_out = pout + st_bytes + out_off[i];
+  }
+  void results_decode(batch& b) {
+    auto const* hst = reinterpret_cast<int32_t const*>(b.pin_out + b.out_fill);
+    for (size_t i = 0; i < b.reqs.size(); ++i) {
+      request* q = b.reqs[i];
+      q->status = hst[i];
+      q->result_bytes = hst[i] == RPP_OK ? q->out_cap : 0;
+      q->pin_out = b.pin_out + q->out_off;
     }
-    publish(lk, b, self);
   }
 
   int dev_;
   rpp_config cfg_;
   bool encode_;
   std::mutex mu_;
-  std::deque<request*> pending_;
-  int active_ = 0;
+  std::condition_variable res_cv_;  // callers waiting for a batch with room
+  std::condition_variable drv_cv_;  // the driver, when it has nothing in flight
+  batch* open_ = nullptr;           // the batch taking new requests
+  std::vector<batch*> spare_;       // opened concurrently, not yet taking requests
+  std::deque<batch*> ready_;        // closed and staged, to be launched
+  std::deque<batch*> flight_;       // launched, in launch order
+  int inflight_ = 0;                // closed, not yet completed
+  int alive_ = 0;
+  bool driver_started_ = false, driver_idle_ = false;
 };
 
 batch_queue& queue_for(int dev, rpp_config const& c, bool encode) {
@@ -676,6 +756,8 @@ std::unique_ptr<decoder_interface<uint16_t>> create_decoder<uint16_t>(codec_conf
 }
 
 void inject_context_failures(uint32_t n) { g_ctx_faults.store(n); }
+
+void set_facade_pipeline_depth(int batches) { g_max_active.store(std::max(1, std::min(batches, 16))); }
 
 facade_stats get_facade_stats() {
   return facade_stats{g_enc_launches.load(), g_enc_blocks.load(), g_dec_launches.load(), g_dec_blocks.load(),

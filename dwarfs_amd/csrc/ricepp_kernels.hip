@@ -182,22 +182,26 @@ struct EncParams {
   // units the workspace holds: a batch with more (its samples exceed the
   // caller's total_samples) is encoded one wave per stream, nothing split
   uint64_t max_units;
+  uint32_t seg_chunks;  // chunks per unit (enc_seg_chunks)
 };
 // segment mode and the batch fits the workspace
 __device__ __forceinline__ bool enc_split_ok(const EncParams& p) {
   return p.seg_map && p.seg_base[p.nblocks] <= p.max_units;
 }
 
-// Segment mode: a stream of more than kEncSegChunks chunks is encoded by
-// several waves, one per run of kEncSegChunks chunks.  Every sub-block's codes
+// Segment mode: a stream of more than seg_chunks chunks is encoded by
+// several waves, one per run of seg_chunks chunks.  Every sub-block's codes
 // depend only on its samples and the sample before it (encode.h:92-157), so a
 // segment starts from the real preceding sample, at bit 0 of its own scratch
 // slot (segment 0: after the initial values, in the stream's output), and
 // rpp_enc_concat_kernel then places each segment at its bit offset.
-#ifndef RPP_ENC_SEG_CHUNKS
-#define RPP_ENC_SEG_CHUNKS 256
-#endif
-constexpr uint32_t kEncSegChunks = RPP_ENC_SEG_CHUNKS;
+// seg_chunks is kEncSegChunks when the batch fills the GPU with units of that
+// size, smaller (down to kEncSegChunksMin, so that a unit that is not its
+// stream's last holds at least 64 bits) for batches of few blocks, whose
+// latency is one wave's pass over a whole block otherwise (enc_seg_chunks)
+constexpr uint32_t kEncSegChunks = 256;
+constexpr uint32_t kEncSegChunksMin = 16;
+constexpr uint64_t kEncTargetUnits = 2048;
 #ifndef RPP_EPRIO
 #define RPP_EPRIO 1  // wave priority in the pipelined encode (1: plans over emission, 2: the reverse, 0: off)
 #endif
@@ -616,10 +620,11 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint16_t* in = p.in + p.in_off[b];
   const uint32_t chunk_len = CS * bs;
   const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
-  const bool multi = split && nchunks > kEncSegChunks;
+  const uint32_t segc = p.seg_chunks;
+  const bool multi = split && nchunks > segc;
   // this unit's chunks [c_lo, c_hi)
-  const uint32_t c_lo = multi ? seg * kEncSegChunks : 0u;
-  const uint32_t c_hi = multi ? min(nchunks, c_lo + kEncSegChunks) : nchunks;
+  const uint32_t c_lo = multi ? seg * segc : 0u;
+  const uint32_t c_hi = multi ? min(nchunks, c_lo + segc) : nchunks;
   uint8_t* out8 = seg == 0 ? p.out + ooff : p.scratch + (size_t)(blockIdx.x - b - 1) * p.slot_bytes;
 #ifdef RPP_STATS
   uint32_t stat_acc[16] = {0};
@@ -746,17 +751,18 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
 #endif
 }
 
-// Units of each stream (nseg: one per kEncSegChunks chunks for a stream of
-// more than kEncSegChunks chunks, else 1); entry nblocks is 0 so the
-// exclusive scan ends in the total.
-__global__ void rpp_enc_units_kernel(const uint64_t* n_samples, uint32_t nblocks, uint32_t chunk_len, uint64_t* units) {
+// Units of each stream (nseg: one per seg_chunks chunks for a stream of
+// more than seg_chunks chunks, else 1); entry nblocks is 0 so the exclusive
+// scan ends in the total.
+__global__ void rpp_enc_units_kernel(const uint64_t* n_samples, uint32_t nblocks, uint32_t chunk_len,
+                                     uint32_t seg_chunks, uint64_t* units) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nblocks) return;
   uint64_t u = 0;
   if (i < nblocks) {
     const uint64_t n = n_samples[i];
     const uint64_t nch = (n + chunk_len - 1) / chunk_len;
-    u = nch > kEncSegChunks && n < RPP_MAX_STREAM_SAMPLES ? (nch + kEncSegChunks - 1) / kEncSegChunks : 1;
+    u = nch > seg_chunks && n < RPP_MAX_STREAM_SAMPLES ? (nch + seg_chunks - 1) / seg_chunks : 1;
   }
   units[i] = u;
 }
@@ -854,9 +860,20 @@ EncKernel enc_kernel_for(uint32_t bs) {
   return rpp_encode_kernel<8, 8, CS, SH>;
 }
 
-// streams of more than kEncSegChunks chunks are split
-bool enc_segmented(const rpp_config* cfg, uint64_t max_stream_samples) {
-  return max_stream_samples > (uint64_t)kEncSegChunks * cfg->block_size * cfg->component_stream_count;
+// chunks per unit for a batch of total_samples: kEncSegChunks when that gives
+// kEncTargetUnits units, else the power of two that comes closest from below
+// (a batch of 16 x 64 KiB blocks: 16-chunk units, 16 waves per block)
+uint32_t enc_seg_chunks(const rpp_config* cfg, uint64_t total_samples) {
+  const uint64_t chunks = total_samples / ((uint64_t)cfg->block_size * cfg->component_stream_count);
+  uint32_t c = kEncSegChunks;
+  while (c > kEncSegChunksMin && chunks / c < kEncTargetUnits) c >>= 1;
+  return c;
+}
+
+// streams of more than seg_chunks chunks are split
+bool enc_segmented(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples) {
+  return max_stream_samples >
+         (uint64_t)enc_seg_chunks(cfg, total_samples) * cfg->block_size * cfg->component_stream_count;
 }
 
 EncKernel enc_kernel(const rpp_config* cfg) {
@@ -877,12 +894,14 @@ struct EncWorkspace {
   uint64_t* seg_off;   // [max_units]
   uint8_t* scratch;    // [(max_units - B) * slot_bytes]
   uint64_t slot_bytes, max_units, bytes;
+  uint32_t seg_chunks;
 };
 
 EncWorkspace enc_layout(const rpp_config* cfg, uint64_t total_samples, uint32_t nblocks, uint8_t* base) {
   const uint64_t B = nblocks;
-  const uint64_t seg_samples = (uint64_t)kEncSegChunks * cfg->block_size * cfg->component_stream_count;
   EncWorkspace w{};
+  w.seg_chunks = enc_seg_chunks(cfg, total_samples);
+  const uint64_t seg_samples = (uint64_t)w.seg_chunks * cfg->block_size * cfg->component_stream_count;
   w.max_units = B + total_samples / seg_samples;
   w.slot_bytes = (rpp_worst_case_bytes(cfg, seg_samples) + 16 + 15) & ~uint64_t{15};
   uint64_t off = 0;
@@ -1075,12 +1094,20 @@ RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", "0xa")
 RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc")
 // the persistent destination registers of the six steps and of the final
 // shift, initialised to the identity map (opaque to the compiler)
+#ifndef RPP_SPEC
+#define RPP_SPEC 0  // entry states from 2^RPP_SPEC-segment compositions when constant (0: the full scan)
+#endif
 struct ScanRegs {
   Map8 r1, r2, r4, r8, b15, b31, w1;
   // entry-state rounds (jacobi8, fs >= 8 loop): lane 0 holds the window's
   // entry state (skip the 4-bit header) in replicated form and is never
   // written
   uint32_t ja, jb;
+#if RPP_SPEC
+  // short compositions (spec_sel): lane 0 keeps the constant map "-> 4" (the
+  // window's entry: skip the header), lanes 1.. are rewritten every time
+  Map8 c1, c2, c3, c4;
+#endif
   __device__ ScanRegs() {
     Map8* all[7] = {&r1, &r2, &r4, &r8, &b15, &b31, &w1};
     for (Map8* x : all) {
@@ -1090,6 +1117,13 @@ struct ScanRegs {
     }
     ja = jb = 0x04040404u;
     asm volatile("" : "+v"(ja), "+v"(jb));
+#if RPP_SPEC
+    Map8* cs[4] = {&c1, &c2, &c3, &c4};
+    for (Map8* x : cs) {
+      x->lo = x->hi = 0x04040404u;
+      asm volatile("" : "+v"(x->lo), "+v"(x->hi));
+    }
+#endif
   }
 };
 // the value of lane l-1 into `keep` (lane 0 keeps its value)
@@ -1577,7 +1611,26 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
             const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
             return __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
           };
-#if RPP_JACOBI > 0
+#if RPP_SPEC
+          // Lane l's entry state is E_l = X_l(E_(l-1)) with X_l = M_(l-1)
+          // (X_0 = the constant map to 4).  Parses of a Rice stream from
+          // different states merge within a few codes, so the composition of
+          // the 2 (RPP_SPEC 1) or 4 (RPP_SPEC 2) segments before a lane is
+          // almost always a constant map, which then is E_l whatever came
+          // before.  Lanes where it is not are flagged; the exact scan runs
+          // only when one of them lies before the sub-block's end (if none
+          // does, every lane up to the end is exact: induction from lane 0).
+          auto spec_sel = [&](uint64_t& nonconst) {
+            const Map8 X = shift8_wave(M, sreg.c1);
+            Map8 C = comp8(X, shift8_wave(X, sreg.c2));
+            if constexpr (RPP_SPEC >= 2) C = comp8(C, shift8_wave(shift8_wave(C, sreg.c3), sreg.c4));
+            const uint32_t r = __builtin_amdgcn_perm(C.hi, C.lo, 0u);  // entry 0, in all four bytes
+            nonconst = __ballot((C.lo != r) | (C.hi != r));
+            return r;
+          };
+          uint64_t unsettled;
+          tm = term_mask(spec_sel(unsettled));
+#elif RPP_JACOBI > 0
           uint64_t unsettled;
           tm = term_mask(jacobi8<RPP_JACOBI>(M, sreg, unsettled));
 #else
@@ -1599,7 +1652,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           __builtin_amdgcn_s_setprio(RPP_PRIO);
 #endif
           finm = __ballot(incl >= n);
-#if RPP_JACOBI > 0
+#if RPP_JACOBI > 0 || RPP_SPEC
           if (unsettled & upto_end(finm)) {
             RPP_STAT(9, 1);
             tm = term_mask(scan_sel());
@@ -3088,7 +3141,7 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
     return RPP_INVALID_ARGUMENT;
   EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count, nullptr, nullptr, nullptr, nullptr, 0, 0};
+              cfg->unused_lsb_count, nullptr, nullptr, nullptr, nullptr, 0, 0, kEncSegChunks};
   hipLaunchKernelGGL(enc_kernel(cfg), dim3(nblocks), dim3(kWave), 0, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
@@ -3096,7 +3149,7 @@ int rpp_encode_batch(const rpp_config* cfg, const uint16_t* d_in, const uint64_t
 uint64_t rpp_encode_workspace_bytes(const rpp_config* cfg, uint64_t total_samples, uint64_t max_stream_samples,
                                     uint32_t nblocks) {
   if (rpp_check_config(cfg) != RPP_OK) return 0;
-  if (!enc_segmented(cfg, max_stream_samples)) return 0;
+  if (!enc_segmented(cfg, total_samples, max_stream_samples)) return 0;
   return enc_layout(cfg, total_samples, nblocks, nullptr).bytes;
 }
 
@@ -3109,7 +3162,7 @@ int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint6
   if (nblocks == 0) return RPP_OK;
   if (!d_in || !d_in_offsets || !d_n_samples || !d_out || !d_out_offsets || !d_out_bytes || !d_status)
     return RPP_INVALID_ARGUMENT;
-  if (!enc_segmented(cfg, max_stream_samples))  // no stream to split: one wave per stream
+  if (!enc_segmented(cfg, total_samples, max_stream_samples))  // no stream to split: one wave per stream
     return rpp_encode_batch(cfg, d_in, d_in_offsets, d_n_samples, nblocks, d_out, d_out_offsets, d_out_bytes,
                             d_status, stream);
   const EncWorkspace w = enc_layout(cfg, total_samples, nblocks, static_cast<uint8_t*>(d_workspace));
@@ -3117,13 +3170,14 @@ int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint6
   hipStream_t s = (hipStream_t)stream;
   const uint32_t chunk_len = cfg->block_size * cfg->component_stream_count;
   hipLaunchKernelGGL(rpp_enc_units_kernel, dim3((nblocks + 256) / 256), dim3(256), 0, s, d_n_samples, nblocks,
-                     chunk_len, w.units);
+                     chunk_len, w.seg_chunks, w.units);
   if ((st = rpp_exclusive_scan_u64(w.units, (uint64_t)nblocks + 1, w.seg_base, s)) != RPP_OK) return st;
   hipLaunchKernelGGL(rpp_enc_unit_map_kernel, dim3((nblocks + 255) / 256), dim3(256), 0, s, w.seg_base, nblocks,
                      w.max_units, w.seg_map);
   EncParams p{d_in, d_in_offsets, d_n_samples, d_out, d_out_offsets, d_out_bytes, d_status, nblocks,
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
-              cfg->unused_lsb_count, w.seg_map, w.seg_base, w.seg_bits, w.scratch, w.slot_bytes, w.max_units};
+              cfg->unused_lsb_count, w.seg_map, w.seg_base, w.seg_bits, w.scratch, w.slot_bytes, w.max_units,
+              w.seg_chunks};
   hipLaunchKernelGGL(enc_kernel(cfg), dim3((uint32_t)w.max_units), dim3(kWave), 0, s, p);
   if (w.max_units > nblocks) {  // streams long enough to be split: place the segments
     if ((st = rpp_exclusive_scan_u64(w.seg_bits, w.max_units, w.seg_off, s)) != RPP_OK) return st;

@@ -191,4 +191,8 @@ facade_stats get_facade_stats();
 // hipStreamCreate would), to exercise the error paths of the batch queue.
 void inject_context_failures(uint32_t n);
 
+// Benchmarks only: batches of one queue on the device at once (default 4, the
+// process's hardware queues; clamped to 1..16).
+void set_facade_pipeline_depth(int batches);
+
 }  // namespace ricepp_amd

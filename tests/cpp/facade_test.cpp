@@ -323,11 +323,14 @@ int bench(int argc, char** argv) {
   size_t const blocks = argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 4096;
   std::vector<int> threads;
   size_t kib = 64;
+  int depth = 4;
   for (int i = 3; i < argc; ++i) {
     if (std::string(argv[i]).rfind("--kib=", 0) == 0) kib = std::strtoul(argv[i] + 6, nullptr, 10);
+    else if (std::string(argv[i]).rfind("--depth=", 0) == 0) depth = std::atoi(argv[i] + 8);
     else threads.push_back(std::atoi(argv[i]));
   }
   if (threads.empty()) threads = {1, 8, 64};
+  ricepp_amd::set_facade_pipeline_depth(depth);
   size_t const n = kib * 512;  // samples per block
   auto c = cfg(128, 1, true, 0);
   std::vector<std::vector<uint16_t>> in(blocks);
@@ -371,11 +374,11 @@ int bench(int argc, char** argv) {
     for (size_t b = 0; b < blocks; ++b) ok = ok && out[b] == in[b];
     double gib = double(blocks) * n * 2 / double(1ull << 30);
     const double ne = double(s1.encode_launches - s0.encode_launches), nd = double(s2.decode_launches - s1.decode_launches);
-    std::printf("{\"facade_bench\": true, \"threads\": %d, \"blocks\": %zu, \"block_bytes\": %zu, "
+    std::printf("{\"facade_bench\": true, \"threads\": %d, \"depth\": %d, \"blocks\": %zu, \"block_bytes\": %zu, "
                 "\"encode_GiBps\": %.3f, \"decode_GiBps\": %.3f, \"encode_launches\": %.0f, "
                 "\"decode_launches\": %.0f, \"encode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, \"finish\": %.1f}, "
                 "\"decode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, \"finish\": %.1f}, \"roundtrip_ok\": %s}\n",
-                T, blocks, n * 2, gib / te, gib / td, ne, nd, (s1.stage_ns - s0.stage_ns) / 1e3 / ne,
+                T, depth, blocks, n * 2, gib / te, gib / td, ne, nd, (s1.stage_ns - s0.stage_ns) / 1e3 / ne,
                 (s1.device_ns - s0.device_ns) / 1e3 / ne, (s1.finish_ns - s0.finish_ns) / 1e3 / ne,
                 (s2.stage_ns - s1.stage_ns) / 1e3 / nd, (s2.device_ns - s1.device_ns) / 1e3 / nd,
                 (s2.finish_ns - s1.finish_ns) / 1e3 / nd, ok ? "true" : "false");

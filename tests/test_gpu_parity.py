@@ -434,10 +434,12 @@ def test_decode_streams_at_any_byte_offset(path):
 
 @pytest.mark.parametrize("bs,cs", [(128, 1), (16, 1), (32, 2), (13, 2), (512, 1)])
 def test_segmented_encode_of_long_streams(bs, cs):
-    """rpp_encode_batch_ws splits streams of more than 256 chunks into segments encoded by separate waves
-    and then places their bits; the result must be the oracle's stream byte for byte, at every segment
-    count and tail shape: exactly 256 chunks (one segment), 257 (a one-chunk last segment), a ragged
-    last chunk, a last segment of a single sample, and data that makes raw / zero / Rice sub-blocks."""
+    """rpp_encode_batch_ws splits long streams into segments encoded by separate waves and then places
+    their bits; the result must be the oracle's stream byte for byte, at every segment count and tail
+    shape.  Units are 256 chunks when the batch fills the GPU with them, else smaller powers of two down
+    to 16 (these batches: 16), so the sizes below -- multiples of 256 chunks plus a chunk, a sample, a
+    ragged chunk -- give one-chunk and one-sample last units, and the data makes raw / zero / Rice
+    sub-blocks."""
     rng = np.random.default_rng(bs * 10 + cs)
     seg = 256 * bs * cs
     sizes = [seg, seg + bs * cs, seg + cs, 2 * seg + 5 * cs, 3 * seg - cs, 5 * seg + 7 * cs]
