@@ -502,41 +502,42 @@ class batch_queue {
     ctx_pool::get().release(c);  // (the stream is idle: the event covered its last work)
   }
 
-  // device: [in][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status][out slots]
-  // pinned in: [in][u64 in_off | n | out_off]   (one H2D copy)
+  // The encode kernel reads the samples and the parameter arrays straight from
+  // the mapped pinned input (each sample once, 16-byte loads issued three
+  // groups ahead), and the pack kernel writes the encoded bytes straight into
+  // the mapped pinned output; the sizes and statuses follow in one small copy.
+  // device: [u64 out_bytes | dst_off | total][i32 status][out slots]
+  // pinned in: [in][u64 in_off | n | out_off]
   // pinned out: [packed bytes][u64 out_bytes | dst_off | total][i32 status]
-  // The pack kernel writes the encoded bytes straight into the mapped pinned
-  // output; the sizes and statuses follow in one small copy.
   void launch_encode(batch& b) {
     device_ctx& ctx = *b.ctx;
     const size_t nb = b.reqs.size();
     const size_t in_total = b.in_fill, out_total = b.out_fill;
-    const size_t arr = (6 * nb + 1) * 8 + align16(nb * 4);
+    const size_t arr = (3 * nb + 1) * 8 + align16(nb * 4);
     auto* h64 = reinterpret_cast<uint64_t*>(b.pin_in + in_total);
     for (size_t i = 0; i < nb; ++i) {
       h64[i] = b.reqs[i]->in_off / 2;
       h64[nb + i] = b.reqs[i]->n_samples;
       h64[2 * nb + i] = b.reqs[i]->out_off;
     }
-    uint8_t* d = ctx.dev(in_total + arr + out_total + 64);
+    uint8_t* d = ctx.dev(arr + out_total + 64);
     const uint64_t ws_bytes =
         rpp_encode_workspace_bytes(&cfg_, b.total_samples, b.max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
+    uint8_t* pin_dev = ctx.device_view(b.pin_in);
     uint8_t* pout_dev = ctx.device_view(b.pin_out);
-    auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
-    auto* dst = reinterpret_cast<int32_t*>(d + in_total + (6 * nb + 1) * 8);
-    uint8_t* dslots = d + in_total + arr;
+    auto* p64 = reinterpret_cast<uint64_t*>(pin_dev + in_total);  // in_off | n | out_off
+    auto* d64 = reinterpret_cast<uint64_t*>(d);                   // out_bytes | dst_off | total
+    auto* dst = reinterpret_cast<int32_t*>(d + (3 * nb + 1) * 8);
+    uint8_t* dslots = d + arr;
     hipStream_t s = ctx.stream();
-    hip_check(hipMemcpyAsync(d, b.pin_in, in_total + 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode input");
-    int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
-                                 dslots, d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes,
-                                 s);
+    int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(pin_dev), p64, p64 + nb,
+                                 static_cast<uint32_t>(nb), dslots, p64 + 2 * nb, d64, dst, b.total_samples,
+                                 b.max_samples, ws, ws_bytes, s);
     if (st != RPP_OK) throw_status(st);
-    st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
-                        d64 + 5 * nb, s);
+    st = rpp_pack_batch(dslots, p64 + 2 * nb, d64, static_cast<uint32_t>(nb), pout_dev, d64 + nb, d64 + 2 * nb, s);
     if (st != RPP_OK) throw_status(st);
-    hip_check(hipMemcpyAsync(b.pin_out + out_total, d64 + 3 * nb, arr - 3 * nb * 8, hipMemcpyDeviceToHost, s),
-              "D2H encode sizes");
+    hip_check(hipMemcpyAsync(b.pin_out + out_total, d, arr, hipMemcpyDeviceToHost, s), "D2H encode sizes");
     g_enc_launches.fetch_add(1, std::memory_order_relaxed);
     g_enc_blocks.fetch_add(nb, std::memory_order_relaxed);
   }
@@ -556,6 +557,8 @@ class batch_queue {
   // device: [in][u64 in_off | in_bytes | out_off | n][out samples][i32 status]
   // pinned in: [in][u64 in_off | in_bytes | out_off | n]   (one H2D copy)
   // pinned out: [out samples][i32 status]                  (one D2H copy)
+  // (batches of short streams only: no device buffers, the kernel works on
+  // the pinned buffers themselves)
   void launch_decode(batch& b) {
     device_ctx& ctx = *b.ctx;
     const size_t nb = b.reqs.size();
@@ -568,15 +571,33 @@ class batch_queue {
       h64[3 * nb + i] = b.reqs[i]->n_samples;
     }
     const size_t st_bytes = align16(nb * 4);
-    uint8_t* d = ctx.dev(in_total + 4 * nb * 8 + out_total + st_bytes + 64);
     // long blocks (16 MiB DwarFS blocks) are parsed in segments by several waves
     const uint64_t ws_bytes =
         rpp_decode_workspace_bytes(&cfg_, b.total_samples, b.max_samples, static_cast<uint32_t>(nb));
-    uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
+    hipStream_t s = ctx.stream();
+    if (ws_bytes == 0) {
+      // every stream is decoded by one wave, which reads its compressed bytes
+      // once (through its LDS ring, prefetched far ahead) and writes each
+      // sample once: straight from and to the mapped pinned buffers, no
+      // copies (a batch of short streams is latency-bound, and copies on two
+      // streams at once do not overlap with the kernels)
+      uint8_t* din = ctx.device_view(b.pin_in);
+      uint8_t* dout = ctx.device_view(b.pin_out);
+      auto* d64 = reinterpret_cast<uint64_t*>(din + in_total);
+      int st = rpp_decode_batch_ws(&cfg_, din, d64, d64 + nb, static_cast<uint32_t>(nb),
+                                   reinterpret_cast<uint16_t*>(dout), d64 + 2 * nb, d64 + 3 * nb,
+                                   reinterpret_cast<int32_t*>(dout + out_total), b.total_samples, b.max_samples,
+                                   nullptr, 0, s);
+      if (st != RPP_OK) throw_status(st);
+      g_dec_launches.fetch_add(1, std::memory_order_relaxed);
+      g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);
+      return;
+    }
+    uint8_t* d = ctx.dev(in_total + 4 * nb * 8 + out_total + st_bytes + 64);
+    uint8_t* ws = ctx.workspace(ws_bytes);
     auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
     uint8_t* dout = d + in_total + 4 * nb * 8;
     auto* dst = reinterpret_cast<int32_t*>(dout + out_total);
-    hipStream_t s = ctx.stream();
     hip_check(hipMemcpyAsync(d, b.pin_in, in_total + 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode input");
     int st = rpp_decode_batch_ws(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb), reinterpret_cast<uint16_t*>(dout),
                                  d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes, s);

@@ -1011,6 +1011,23 @@ constexpr MapTable make_map_table() {
 
 __device__ const MapTable g_map_table = make_map_table();
 
+// The transfer tables into LDS, eight 16-byte loads in flight per lane (a
+// one-wave workgroup -- small batches -- copies the 56 KiB in 7 round trips
+// instead of 56).  The caller synchronises.
+__device__ __forceinline__ void copy_tables(uint4* dsm) {
+  const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
+  const uint32_t bd = blockDim.x;
+  uint32_t i = threadIdx.x;
+  for (; i + 7 * bd < kMapEntries; i += 8 * bd) {
+    uint4 v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) v[k] = gt[i + k * bd];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) dsm[i + k * bd] = v[k];
+  }
+  for (; i < kMapEntries; i += bd) dsm[i] = gt[i];
+}
+
 constexpr uint32_t kSegBits = 24;                // bits per lane segment (3 table bytes)
 constexpr uint32_t kWinBits = kWave * kSegBits;  // bits per window
 constexpr uint32_t kRingWords = 1024;            // per-stream LDS ring of the compressed stream (4 KiB)
@@ -1351,10 +1368,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   if (mine && p.units && p.units[b] > 1) mine = false;
   if (!__syncthreads_or(mine)) return;
   // ---- the transfer tables, one copy per workgroup ----
-  {
-    const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
-    for (uint32_t i = threadIdx.x; i < kMapEntries; i += blockDim.x) dsm[i] = gt[i];
-  }
+  copy_tables(dsm);
   __syncthreads();
   const uint4* tab = dsm;
   const uint32_t lane = lane_id();
@@ -2443,8 +2457,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     }
   }
   {
-    const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
-    for (uint32_t i = threadIdx.x; i < kMapEntries; i += blockDim.x) dsm[i] = gt[i];
+    copy_tables(dsm);
   }
   __syncthreads();
   const uint4* tab = dsm;
@@ -3040,8 +3053,7 @@ __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(Parse
   const uint64_t n64 = p.n_samples[b], ioff = p.in_off[b], nb64 = p.in_bytes[b];
   if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) return;
   {
-    const uint4* gt = reinterpret_cast<const uint4*>(g_map_table.w);
-    for (uint32_t i = threadIdx.x; i < kMapEntries; i += blockDim.x) dsm[i] = gt[i];
+    copy_tables(dsm);
   }
   if (threadIdx.x == 0) best = kSegNone;
   __syncthreads();

@@ -11,3 +11,8 @@ done
 timeout -k 10 150 tests/cpp/build/facade_test --bench 256 16 64 --kib=1024 >> gpurun_out/facade_bench.log 2>&1 || { echo "facade_bench1m failed"; exit 1; }
 timeout -k 10 150 tests/cpp/build/facade_test --bench 64 16 64 --kib=4096 >> gpurun_out/facade_bench.log 2>&1 || { echo "facade_bench4m failed"; exit 1; }
 cat gpurun_out/facade_bench.log
+export TMPDIR=/tmp
+rm -rf gpurun_out/segtrace
+timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/segtrace -o gen16 -- python3 tools/seg_bench.py "16 x 1 MiB generator" > gpurun_out/segtrace_gen16.log 2>&1; echo "gen16=$?"
+cat gpurun_out/segtrace_gen16.log | tail -2
+f=$(find gpurun_out/segtrace -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cut -c1-160 "$f" | head -25
