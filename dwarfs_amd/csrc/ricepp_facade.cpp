@@ -2,9 +2,9 @@
 //
 // The DwarFS plugin semantics follow src/compression/ricepp.cpp (file:line
 // cited at each method).  Encode / decode calls go through a per-(device,
-// config) combining queue: concurrent calls are coalesced into one
-// rpp_encode_batch_ws / rpp_decode_batch_ws launch on a pooled device context
-// (stream + grow-only device arena + grow-only pinned staging), so the
+// config, direction) pipelined batch queue: concurrent calls are coalesced
+// into one rpp_encode_batch_ws / rpp_decode_batch_ws launch on a pooled device
+// context (stream + event + device buffers + mapped pinned staging), so the
 // worker_group threads of the DwarFS writer (src/writer/filesystem_writer.cpp:
 // 255-287) and block cache (src/reader/internal/block_cache.cpp:628-706) feed
 // the GPU in batches without any per-call stream creation or allocation.
@@ -502,42 +502,44 @@ class batch_queue {
     ctx_pool::get().release(c);  // (the stream is idle: the event covered its last work)
   }
 
-  // The encode kernel reads the samples and the parameter arrays straight from
-  // the mapped pinned input (each sample once, 16-byte loads issued three
-  // groups ahead), and the pack kernel writes the encoded bytes straight into
-  // the mapped pinned output; the sizes and statuses follow in one small copy.
-  // device: [u64 out_bytes | dst_off | total][i32 status][out slots]
-  // pinned in: [in][u64 in_off | n | out_off]
+  // device: [in][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status][out slots]
+  // pinned in: [in][u64 in_off | n | out_off]   (one H2D copy)
   // pinned out: [packed bytes][u64 out_bytes | dst_off | total][i32 status]
+  // The pack kernel writes the encoded bytes straight into the mapped pinned
+  // output; the sizes and statuses follow in one small copy.  (The samples
+  // are copied in rather than read over PCIe by the encode kernel: reading
+  // them in place measured 1.6x slower for 1 MiB blocks and no faster for
+  // 64 KiB ones, profiles/r03_facade_bench.jsonl.)
   void launch_encode(batch& b) {
     device_ctx& ctx = *b.ctx;
     const size_t nb = b.reqs.size();
     const size_t in_total = b.in_fill, out_total = b.out_fill;
-    const size_t arr = (3 * nb + 1) * 8 + align16(nb * 4);
+    const size_t arr = (6 * nb + 1) * 8 + align16(nb * 4);
     auto* h64 = reinterpret_cast<uint64_t*>(b.pin_in + in_total);
     for (size_t i = 0; i < nb; ++i) {
       h64[i] = b.reqs[i]->in_off / 2;
       h64[nb + i] = b.reqs[i]->n_samples;
       h64[2 * nb + i] = b.reqs[i]->out_off;
     }
-    uint8_t* d = ctx.dev(arr + out_total + 64);
+    uint8_t* d = ctx.dev(in_total + arr + out_total + 64);
     const uint64_t ws_bytes =
         rpp_encode_workspace_bytes(&cfg_, b.total_samples, b.max_samples, static_cast<uint32_t>(nb));
     uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
-    uint8_t* pin_dev = ctx.device_view(b.pin_in);
     uint8_t* pout_dev = ctx.device_view(b.pin_out);
-    auto* p64 = reinterpret_cast<uint64_t*>(pin_dev + in_total);  // in_off | n | out_off
-    auto* d64 = reinterpret_cast<uint64_t*>(d);                   // out_bytes | dst_off | total
-    auto* dst = reinterpret_cast<int32_t*>(d + (3 * nb + 1) * 8);
-    uint8_t* dslots = d + arr;
+    auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
+    auto* dst = reinterpret_cast<int32_t*>(d + in_total + (6 * nb + 1) * 8);
+    uint8_t* dslots = d + in_total + arr;
     hipStream_t s = ctx.stream();
-    int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(pin_dev), p64, p64 + nb,
-                                 static_cast<uint32_t>(nb), dslots, p64 + 2 * nb, d64, dst, b.total_samples,
-                                 b.max_samples, ws, ws_bytes, s);
+    hip_check(hipMemcpyAsync(d, b.pin_in, in_total + 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode input");
+    int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
+                                 dslots, d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes,
+                                 s);
     if (st != RPP_OK) throw_status(st);
-    st = rpp_pack_batch(dslots, p64 + 2 * nb, d64, static_cast<uint32_t>(nb), pout_dev, d64 + nb, d64 + 2 * nb, s);
+    st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
+                        d64 + 5 * nb, s);
     if (st != RPP_OK) throw_status(st);
-    hip_check(hipMemcpyAsync(b.pin_out + out_total, d, arr, hipMemcpyDeviceToHost, s), "D2H encode sizes");
+    hip_check(hipMemcpyAsync(b.pin_out + out_total, d64 + 3 * nb, arr - 3 * nb * 8, hipMemcpyDeviceToHost, s),
+              "D2H encode sizes");
     g_enc_launches.fetch_add(1, std::memory_order_relaxed);
     g_enc_blocks.fetch_add(nb, std::memory_order_relaxed);
   }

@@ -30,12 +30,14 @@
 // (src/writer/filesystem_writer.cpp:255-287) and decompress blocks
 // concurrently (src/reader/internal/block_cache.cpp:628-706).  Concurrent
 // encode / decode calls with the same configuration on the same device are
-// coalesced into one rpp_encode_batch_ws / rpp_decode_batch_ws launch (a combining
-// queue: the first waiting caller launches everything queued, the other
-// callers copy their own data in and out of pinned staging in parallel).
-// Device contexts (stream, device and pinned staging) come from a per-device
-// pool and are reused, so no call creates a stream or allocates once the pool
-// is warm.  An object runs on the device that was current when it was created.
+// coalesced into one rpp_encode_batch_ws / rpp_decode_batch_ws launch (a
+// pipelined batch queue: callers copy their own data into and out of pinned
+// staging in parallel, a driver thread per queue launches the batches and
+// publishes their results; up to two batches per queue on the device).
+// Device contexts (stream, event, device and pinned staging) come from a
+// per-device pool and are reused, so no call creates a stream or allocates
+// once the pool is warm.  An object runs on the device that was current when
+// it was created.
 #pragma once
 
 #include <bit>
@@ -191,8 +193,9 @@ facade_stats get_facade_stats();
 // hipStreamCreate would), to exercise the error paths of the batch queue.
 void inject_context_failures(uint32_t n);
 
-// Benchmarks only: batches of one queue on the device at once (default 4, the
-// process's hardware queues; clamped to 1..16).
+// Benchmarks only: batches of one queue on the device at once (default 2: two
+// launches on different streams overlap on the device, more do not; clamped
+// to 1..16).
 void set_facade_pipeline_depth(int batches);
 
 }  // namespace ricepp_amd
