@@ -206,6 +206,9 @@ def main() -> None:
     ap.add_argument("--block-bytes", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step as a captured HIP graph (measured no faster than eager launches: "
+                         "profiles/r03_graph_ab.jsonl)")
     ap.add_argument("--workload", choices=("blocks", "mix"), default="blocks",
                     help="blocks: configs[1] (default, weak scaling); mix: configs[3] (strong scaling)")
     ap.add_argument("--mix-gib", type=int, default=32, help="total size of the configs[3] mix")
@@ -247,6 +250,19 @@ def main() -> None:
     for _ in range(args.warmup):
         pipe.step()
     torch.cuda.synchronize()
+    # the step's kernel chain as a HIP graph (one per rank; with several ranks
+    # the size all-gather stays eager between two graphs): removes the host
+    # launch path and part of the inter-kernel gaps; checked once more below
+    graphed = args.graph and args.workload == "blocks"
+    if graphed:
+        try:
+            pipe.capture()
+        except RuntimeError as e:  # (a runtime that cannot capture: the eager step, said in the line)
+            print(f"bench: graph capture failed, eager steps: {e}", file=sys.stderr)
+            graphed = False
+        for _ in range(max(1, args.warmup)):
+            pipe.step()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -258,6 +274,8 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if graphed:
+        pipe.check(x)  # (the replayed steps are exact too)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -347,6 +365,8 @@ def main() -> None:
             "block_bytes": args.block_bytes,
             "compression_ratio": round(comp_bytes / raw_bytes, 5),
             "parallelism": f"shard{world} (blocks sharded, RCCL all-gather of encoded sizes)",
+            "step_launch": ("HIP graph replay" + (" (encode | eager all-gather | scan + decode)" if world > 1 else "")
+                            if graphed else "eager"),
             "encode_kernel_us": round(k_enc * 1e6, 2),
             "decode_kernel_us": round(k_dec * 1e6, 2),
             "encode_GiBps": round(raw_bytes / k_enc / 2**30, 2),

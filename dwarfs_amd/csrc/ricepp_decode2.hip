@@ -1274,9 +1274,10 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
   hipStream_t s = (hipStream_t)stream;
   const uint32_t fused_waves = opt ? opt->fused_waves : 0u;
   const uint32_t L = seg_log2_for(cfg, total_samples, max_stream_samples, opt);
-  if (!L)
+  if (!L)  // (the rows kernel for bs 16 / 32 unless the one-wave path is asked for)
     return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                             d_n_samples, d_status, s, false, nullptr, fused_waves);
+                                             d_n_samples, d_status, s, false, nullptr, fused_waves,
+                                             path_of(opt) != RPP_DECODE_FUSED);
   const Workspace w = layout(cfg, total_samples, max_stream_samples, nblocks, L, static_cast<uint8_t*>(d_workspace));
   if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
   SideStream* side = side_stream_for(s);
@@ -1373,7 +1374,7 @@ int rpp_decode_batch(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
                      const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                      const uint64_t* d_n_samples, int32_t* d_status, void* stream) {
   return rpp_internal::launch_decode_fused(cfg, d_in, d_in_offsets, d_in_bytes, nblocks, d_out, d_out_offsets,
-                                           d_n_samples, d_status, (hipStream_t)stream);
+                                           d_n_samples, d_status, (hipStream_t)stream, false, nullptr, 0, true);
 }
 
 }  // extern "C"

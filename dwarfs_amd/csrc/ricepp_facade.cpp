@@ -95,9 +95,11 @@ class device_guard {
 // hipFreeAsync on the context's stream), so growing one never synchronises the
 // device.  Pinned buffers are mapped into the device's address space (the
 // encoder packs its output straight into them) and grow geometrically; a
-// context going back to the pool drops pinned buffers above kPinnedKeep, so a
-// burst of huge batches does not keep GiBs of host memory pinned.
+// context going back to the pool drops pinned buffers above kPinnedKeep and
+// device buffers above kDeviceKeep, so a burst of huge batches does not keep
+// GiBs of host memory pinned or of device memory reserved.
 constexpr size_t kPinnedKeep = size_t{64} << 20;
+constexpr size_t kDeviceKeep = size_t{256} << 20;
 
 class device_ctx {
  public:
@@ -130,12 +132,20 @@ class device_ctx {
     return static_cast<uint8_t*>(d);
   }
   void sync() { hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
-  // on release (the stream is idle: every batch ends with a sync)
+  // on release (the stream is idle: every batch ends with its event)
   void trim() {
     for (auto* q : {&hin_, &hout_}) {
       size_t& cap = q == &hin_ ? hin_cap_ : hout_cap_;
       if (cap > kPinnedKeep) {
         (void)hipHostFree(*q);
+        *q = nullptr;
+        cap = 0;
+      }
+    }
+    for (auto* q : {&dbuf_, &wbuf_}) {
+      size_t& cap = q == &dbuf_ ? dcap_ : wcap_;
+      if (cap > kDeviceKeep) {
+        (void)hipFreeAsync(*q, stream_);
         *q = nullptr;
         cap = 0;
       }

@@ -72,11 +72,13 @@ __host__ __device__ inline uint32_t seg_last_bit(uint32_t mis, uint64_t in_bytes
 // rpp_decode_kernel: one wave per stream, parse and values fused (any bs).
 // only_fallback: decode only the streams whose status is kSegFallback;
 // d_units (the segmented decode's units per stream): skip split streams.
-// waves: streams per workgroup (0: by batch size).
+// waves: streams per workgroup (0: by batch size).  rows (bs 16 / 32, a
+// whole-batch launch): rpp_decode_rows_kernel first, four streams per wave,
+// then the fused kernel for the streams it leaves.
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                         const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback = false,
-                        const uint64_t* d_units = nullptr, uint32_t waves = 0);
+                        const uint64_t* d_units = nullptr, uint32_t waves = 0, bool rows = false);
 
 // rpp_parse_kernel over units (SegView): the units of split streams, into
 // their position and overshoot lists (single-unit streams are left to the

@@ -2110,6 +2110,280 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
 
 
 // ===========================================================================
+// DECODE, FOUR STREAMS PER WAVE (bs 16 / 32)
+// ===========================================================================
+// The fast loop of rpp_decode_kernel issues ~100 VALU per sub-block whatever
+// its size: its window, scans and list are sized for 64 lanes, so a 16-sample
+// sub-block (~130 bits) pays what a 128-sample one (~1000 bits) pays, and
+// bs 16 / 32 decode is bound by that issue count.  Here a wave decodes four
+// streams, one per 16-lane row: a 384-bit window per row (16 lanes x 24-bit
+// segments), the same table-driven exact parse with row-local scans
+// (row_shr 1/2/4/8: no row_bcast levels), so one pass over the wave's
+// instructions advances four streams by one sub-block each.  Per-row state is
+// row-uniform VGPRs; each row has its own LDS ring (refilled for all rows at
+// once from per-lane prefetch registers), list and output.  Everything this
+// path does not take -- raw or fs >= 8 sub-blocks, a sub-block that does
+// not end in its 384-bit window, a read
+// past the input, invalid arguments -- marks the stream kSegFallback, and the
+// fused kernel's only_fallback launch that follows decodes it from the start
+// (with the exact error contract).
+constexpr uint32_t kRowsWaves = 4;                   // waves (16 streams) per workgroup
+constexpr uint32_t kRowRing = 512;                   // ring words per row (power of two)
+constexpr uint32_t kRowPad = 16;                     // ring words 0..15 mirrored after its end
+constexpr uint32_t kRowChunk = 64;                   // refill unit: 16 lanes x 16 bytes
+constexpr uint32_t kRowDump = 40;                    // first list pair of lanes past the sub-block
+constexpr uint32_t kRowMT = 24;                      // terminators per 24-bit segment at most (fs 0: 1-bit codes)
+constexpr uint32_t kRowListWords = 4 + 2 * (kRowDump + kRowMT);
+constexpr uint32_t kRowWords = kRowRing + kRowPad + kRowListWords;
+constexpr uint32_t kRowsLdsBytes = kTabBytes + kRowsWaves * 4 * kRowWords * 4;
+#ifndef RPP_ROWS
+#define RPP_ROWS 0  // (off until measured on the GPU)
+#endif
+constexpr bool kRowsDecode = RPP_ROWS != 0;
+
+// exclusive form of a row-local map scan: the map of row lanes 0..i-1
+// (identity on each row's lane 0)
+__device__ __forceinline__ Map8 shift8_row(Map8 m, Map8& keep) {
+  asm("s_nop 1\n\t"
+      "v_mov_b32_dpp %0, %2 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %1, %3 row_shr:1 row_mask:0xf bank_mask:0xf"
+      : "+v"(keep.lo), "+v"(keep.hi)
+      : "v"(m.lo), "v"(m.hi));
+  return keep;
+}
+__device__ __forceinline__ uint32_t row_incl_sum(uint32_t v) {
+  v += dpp<kDppRowShr1>(v);
+  v += dpp<kDppRowShr2>(v);
+  v += dpp<kDppRowShr4>(v);
+  v += dpp<kDppRowShr8>(v);
+  return v;
+}
+
+// TWO: bs 32 (two codes per lane), else bs 16 (one code per lane)
+template <uint32_t CS, bool SH, bool TWO>
+__global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
+  constexpr uint32_t BS = TWO ? 32 : 16;
+  const uint32_t lane = lane_id(), ri = lane & 15u, row = lane >> 4;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t b = (blockIdx.x * kRowsWaves + wv) * 4 + row;  // this row's stream
+  copy_tables(dsm);
+  __syncthreads();
+  const uint4* tab = dsm;
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + kTabBytes / 4 + (wv * 4 + row) * kRowWords;
+  uint32_t* list = ring + kRowRing + kRowPad + 4;
+  if (ri < 4) list[(int)ri - 4] = 0u;  // pair -1 = (0, 0): a_(-1) of the deltas
+  const uint32_t be = p.be, ulsb = p.ulsb;
+  const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
+  const uint32_t selpack = be ? 0x04050001u : 0x05040100u;
+  const uint32_t lane24 = kSegBits * ri;
+
+  // ---- the row's stream (row-uniform values in every lane of the row) ----
+  bool active = b < p.nblocks;
+  int32_t status = rpp_internal::kSegFallback;
+  uint32_t N = 0, nbytes = 0, mis = 0;
+  const uint8_t* in = p.in;
+  uint16_t* out = p.out;
+  if (active) {
+    const uint64_t n64 = p.n_samples[b], ioff = p.in_off[b], nb64 = p.in_bytes[b];
+    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
+      active = false;  // (the fused kernel reports it)
+    } else {
+      mis = (uint32_t)(ioff & 3u);
+      N = (uint32_t)n64;
+      nbytes = (uint32_t)nb64 + mis;
+      in = p.in + (ioff - mis);
+      out = p.out + p.out_off[b];
+    }
+  }
+  const bool aligned16 = ((uintptr_t)in & 15u) == 0;
+  const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
+  constexpr uint32_t chunk_len = CS * BS;
+  const uint32_t nsb = active ? (N + chunk_len - 1) / chunk_len * CS : 0u;
+  // this lane's 16 bytes of the row's chunk at word w (zero past the input)
+  auto chunk_part = [&](uint32_t w) -> uint4 {
+    const uint32_t x = w + 4 * ri;
+    if (aligned16 && 4 * x + 16 <= nbytes) return *reinterpret_cast<const uint4*>(in + 4 * x);
+    return make_uint4(stream_word(in, nbytes, x), stream_word(in, nbytes, x + 1), stream_word(in, nbytes, x + 2),
+                      stream_word(in, nbytes, x + 3));
+  };
+  auto put_chunk = [&](uint32_t w, uint4 v) {  // (w: a multiple of kRowChunk)
+    const uint32_t slot = (w + 4 * ri) & (kRowRing - 1);
+    *reinterpret_cast<uint4*>(&ring[slot]) = v;
+    if (slot < kRowPad) *reinterpret_cast<uint4*>(&ring[kRowRing + slot]) = v;
+  };
+  uint32_t fill_w = 0;
+  put_chunk(0, chunk_part(0));
+  put_chunk(kRowChunk, chunk_part(kRowChunk));
+  fill_w = 2 * kRowChunk;
+  uint4 pf = chunk_part(fill_w);  // the next chunk, in flight
+  lds_fence();
+  auto word_at = [&](uint32_t w) -> const uint32_t* { return ring + (w & (kRowRing - 1)); };
+
+  uint32_t P = 8 * mis + 16 * CS;
+  uint32_t last0 = 0, last1 = 0;
+  if (active) {
+    if (P > lim) active = false;
+    const uint32_t* q = word_at((8 * mis) >> 5);
+    const uint32_t first = __builtin_amdgcn_alignbit(q[1], q[0], (8 * mis) & 31u);
+    last0 = first & 0xFFFFu;
+    last1 = first >> 16;
+  }
+  if (active && nsb == 0) {
+    active = false;
+    status = RPP_OK;
+  }
+  uint32_t s = 0;  // the row's sub-block
+  ScanRegs sreg;
+  uint2* const list2 = reinterpret_cast<uint2*>(list);
+  const uint4* const list4 = reinterpret_cast<const uint4*>(list);
+
+  // one sub-block of every active row; MT: terminators a segment can hold
+  auto step = [&]<uint32_t MT>() {
+    const uint32_t q = P;
+    const uint32_t* w = word_at(q >> 5);
+    const uint32_t h = __builtin_amdgcn_alignbit(w[1], w[0], q & 31u) & 15u;
+    const uint32_t o = lane24 + (q & 31u);
+    const uint32_t oi = o >> 5;
+    const uint32_t xl = __builtin_amdgcn_alignbit(w[oi + 1], w[oi], o);  // (shift o mod 32)
+    const bool zero = h == 0;
+    const bool rice = h - 1u <= 7u;  // fs 0..7
+    const uint32_t fs = rice ? h - 1 : 1u;
+    const uint32_t k = fs + 1;
+    const uint32_t comp = s % CS, cbase = (s / CS) * chunk_len;
+    const uint32_t n = active ? min(N - cbase, chunk_len) / CS : BS;
+    // ---- parse: maps, row scan, entry states, terminators, counts ----
+    const uint4* tb = tab + 256u * fs;
+    const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)], e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
+    const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});
+    const Map8 M = comp8(Map8{e2.x, e2.y}, M01);
+    Map8 S = scan8_shr1(M, sreg.r1);
+    S = scan8_shr2(S, sreg.r2);
+    S = scan8_shr4(S, sreg.r4);
+    S = scan8_shr8(S, sreg.r8);
+    const Map8 X = shift8_row(S, sreg.w1);
+    const uint32_t sel = __builtin_amdgcn_perm(X.hi, X.lo, 0xFFFFFF04u);  // state 4: skip the header
+    const uint32_t a0 = __builtin_amdgcn_perm(e0.w, e0.z, sel);
+    const uint32_t a1 = __builtin_amdgcn_perm(e1.w, e1.z, __builtin_amdgcn_perm(e0.y, e0.x, sel));
+    const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
+    uint32_t tm = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
+    if (zero) tm = 0;
+    const uint32_t cnt = __builtin_popcount(tm);
+    const uint32_t incl = row_incl_sum(cnt);
+    const uint32_t excl = incl - cnt;
+    const uint64_t fin = __ballot(incl >= n);
+    const uint32_t mrow = (uint32_t)(fin >> (16 * row)) & 0xFFFFu;
+    const uint32_t lz = ffbl(mrow);  // the lane holding code n-1 (0xFFFFFFFF: not in the window)
+    uint32_t t[MT];
+#pragma unroll
+    for (uint32_t j = 0; j < MT; ++j) {
+      t[j] = ffbl(tm);
+      tm &= tm - 1;
+    }
+    const uint32_t r = n - 1 - excl;  // (at lane lz: code n-1 is its terminator r)
+    uint32_t tsel;
+    if constexpr (MT <= 12) {
+      uint32_t tp = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
+      if constexpr (MT > 4) {
+        const uint32_t tp1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
+        const uint32_t tp2 = t[8] | (t[9] << 8) | ((t[10] | (t[11] << 8)) << 16);
+        tp = r < 4 ? tp : (r < 8 ? tp1 : tp2);
+      }
+      tsel = __builtin_amdgcn_ubfe(tp, 8 * (r & 3u), 8);
+    } else {
+      tsel = t[0];
+#pragma unroll
+      for (uint32_t j = 1; j < MT; ++j) tsel = r == j ? t[j] : tsel;
+    }
+    const uint32_t tend = (uint32_t)__shfl((int)tsel, (int)((lane & 48u) | (lz & 15u)));
+    const uint32_t Pe = zero ? q + 4 : q + kSegBits * lz + tend + k;
+    const bool ok = active && (zero || (rice && mrow != 0)) && Pe <= lim;
+    // ---- terminators -> (a_i, remainder) list pairs (as the fused loop) ----
+    const uint32_t base = ok && !zero && cnt != 0 && excl < n ? excl : kRowDump;
+    const uint32_t abase = lane24 - 4u - base * k;
+    const uint32_t xr = xl >> 1;
+#pragma unroll
+    for (int j = (int)MT - 1; j >= 0; --j) {
+      list2[base + j] = make_uint2(abase + t[j] - (uint32_t)j * k, __builtin_amdgcn_ubfe(xr, t[j], fs));
+      lds_fence();
+    }
+    // ---- codes -> zig-zag deltas -> values -> stores ----
+    uint32_t d0 = 0, d1 = 0, dsum = 0;
+    if constexpr (TWO) {
+      const uint4 tt = list4[ri];
+      const uint32_t aprev = list[4 * ri - 2];
+      const uint32_t df0 = lshl_or(tt.x - aprev, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
+      d0 = (df0 >> 1) ^ neg_lsb(df0);
+      d1 = (df1 >> 1) ^ neg_lsb(df1);
+      if (zero || 2 * ri >= n) d0 = 0;
+      if (zero || 2 * ri + 1 >= n) d1 = 0;
+      dsum = d0 + d1;
+    } else {
+      const uint2 tt = list2[ri];
+      const uint32_t aprev = list[2 * ri - 2];
+      const uint32_t df = lshl_or(tt.x - aprev, fs, tt.y);
+      d1 = (df >> 1) ^ neg_lsb(df);
+      if (zero || ri >= n) d1 = 0;
+      dsum = d1;
+    }
+    const uint32_t inc = row_incl_sum(dsum);
+    const uint32_t lastc = comp ? last1 : last0;
+    const uint32_t v1 = lastc + inc;  // value of the lane's last code (mod 2^16)
+    uint16_t* dst = out + cbase + comp;
+    if (ok) {
+      if constexpr (TWO) {
+        const uint32_t v0 = v1 - d1;
+        if (CS == 1 && 2 * ri + 1 < n && ((((uintptr_t)dst) & 3u) == 0)) {
+          const uint32_t o2 = SH ? px_write2(__builtin_amdgcn_perm(v1, v0, 0x05040100u), selbe, ulsb)
+                                 : __builtin_amdgcn_perm(v1, v0, selpack);
+          *reinterpret_cast<uint32_t*>(dst + 2 * ri) = o2;
+        } else {
+          if (2 * ri < n) dst[CS * 2 * ri] = (uint16_t)px_write(v0 & 0xFFFFu, be, ulsb);
+          if (2 * ri + 1 < n) dst[CS * (2 * ri + 1)] = (uint16_t)px_write(v1 & 0xFFFFu, be, ulsb);
+        }
+      } else {
+        if (ri < n) dst[CS * ri] = (uint16_t)px_write(v1 & 0xFFFFu, be, ulsb);
+      }
+    }
+    const uint32_t tot = (uint32_t)__shfl((int)inc, (int)(lane | 15u));
+    if (ok) {
+      const uint32_t lnew = (lastc + tot) & 0xFFFFu;
+      if (comp) last1 = lnew;
+      else last0 = lnew;
+      P = Pe;
+      if (++s == nsb) {
+        active = false;
+        status = RPP_OK;
+      }
+    } else if (active) {
+      active = false;  // kSegFallback: the fused kernel takes the whole stream
+    }
+    lds_fence();
+  };
+
+  while (__any(active)) {
+    // list slots per segment: 24 for 1-bit codes (fs 0), 12 for fs 1..4, else 4
+    const uint32_t* w = word_at(P >> 5);
+    const uint32_t h = __builtin_amdgcn_alignbit(w[1], w[0], P & 31u) & 15u;
+    if (__any(active && h == 1u)) step.template operator()<kRowMT>();
+    else if (__any(active && h - 2u <= 3u)) step.template operator()<12>();
+    else step.template operator()<4>();
+    // ---- ring: once a row's look-ahead drops below 40 words, every row with
+    //      room takes its prefetched chunk and prefetches the next ----
+    if (__any(active && fill_w < (P >> 5) + 40u)) {
+      const bool room = fill_w + kRowChunk <= (P >> 5) + kRowRing - 1u;
+      if (room) {
+        put_chunk(fill_w, pf);
+        fill_w += kRowChunk;
+        pf = chunk_part(fill_w);
+      }
+      lds_fence();
+    }
+  }
+  if (ri == 0 && b < p.nblocks) p.status[b] = status;
+}
+
+// ===========================================================================
 // DECODE, PARSE PASS (rpp_decode_batch stage 1 of 2)
 // ===========================================================================
 // The serial part of decoding a stream is finding where each sub-block
@@ -3206,7 +3480,7 @@ namespace rpp_internal {
 int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                         const uint64_t* d_in_bytes, uint32_t nblocks, uint16_t* d_out, const uint64_t* d_out_offsets,
                         const uint64_t* d_n_samples, int32_t* d_status, hipStream_t stream, bool only_fallback,
-                        const uint64_t* d_units, uint32_t waves) {
+                        const uint64_t* d_units, uint32_t waves, bool rows) {
   int st = rpp_check_config(cfg);
   if (st != RPP_OK) return st;
   if (nblocks == 0) return RPP_OK;
@@ -3232,6 +3506,30 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count, W, only_fallback ? 1u : 0u, d_units};
   const auto k = kernels[2 * (cfg->component_stream_count - 1) + (cfg->unused_lsb_count ? 1 : 0)];
+  if (kRowsDecode && rows && !only_fallback && !d_units && !waves &&
+      (cfg->block_size == 16 || cfg->block_size == 32)) {
+    // bs 16 / 32: four streams per wave, then the fused kernel for the
+    // streams it left (status kSegFallback)
+    static void (*const rk[8])(DecParams) = {
+        rpp_decode_rows_kernel<1, false, false>, rpp_decode_rows_kernel<1, true, false>,
+        rpp_decode_rows_kernel<2, false, false>, rpp_decode_rows_kernel<2, true, false>,
+        rpp_decode_rows_kernel<1, false, true>,  rpp_decode_rows_kernel<1, true, true>,
+        rpp_decode_rows_kernel<2, false, true>,  rpp_decode_rows_kernel<2, true, true>};
+    static std::once_flag rows_once;
+    static hipError_t rows_err = hipSuccess;
+    std::call_once(rows_once, [] {
+      for (auto f : rk)
+        if (rows_err == hipSuccess)
+          rows_err = hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)kRowsLdsBytes);
+    });
+    if (rows_err != hipSuccess) return RPP_HIP_ERROR;
+    const auto r = rk[4 * (cfg->block_size == 32 ? 1 : 0) + 2 * (cfg->component_stream_count - 1) +
+                      (cfg->unused_lsb_count ? 1 : 0)];
+    const uint32_t per_wg = 4 * kRowsWaves;
+    hipLaunchKernelGGL(r, dim3((nblocks + per_wg - 1) / per_wg), dim3(kWave * kRowsWaves), kRowsLdsBytes, stream, p);
+    p.only_fallback = 1;
+  }
   hipLaunchKernelGGL(k, dim3((nblocks + W - 1) / W), dim3(kWave * W), lds, stream, p);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }

@@ -163,6 +163,7 @@ class ShardPipeline:
         self.all_sizes: Optional[torch.Tensor] = None
         self.image_offsets: Optional[torch.Tensor] = None
         self.size_gather = SizeGather(self.nblocks, dev, group)
+        self._graphs = None  # (capture)
 
         class _Enc:
             pass
@@ -199,9 +200,52 @@ class ShardPipeline:
         order.  (A side stream overlapping the gather/scan with the decode
         measured slower at N=1: the cross-stream dependency opened a ~7 us
         gap before the decode, more than the 5 us scan it hid.)"""
+        if self._graphs is not None:
+            self._replay()
+            return
         self.encode()
         self.gather()
         self.decode()
+
+    def capture(self) -> None:
+        """Records the step's kernel chains as HIP graphs (every buffer is
+        preallocated and every launch is asynchronous, so a step replays
+        exactly): one graph for the whole step on one rank; with several ranks
+        the encode and the scan + decode, the size all-gather between them
+        issued eagerly (a collective is not captured).  Call after one eager
+        step (it sizes the gather's buffers)."""
+        if self.all_sizes is None:
+            raise RuntimeError("ShardPipeline.capture: run one step first")
+        world = self.size_gather.world
+        graphs = []
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            parts = [(self.encode, self.gather, self.decode)] if world == 1 else [(self.encode,),
+                                                                                   (self._scan, self.decode)]
+            for fns in parts:
+                g = torch.cuda.CUDAGraph()
+                # (thread-local: RCCL's proxy threads keep making HIP calls
+                # while this thread captures)
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                    for f in fns:
+                        f()
+                graphs.append(g)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self._graphs = graphs
+
+    def _scan(self) -> None:
+        self.image_offsets = global_offsets(self.all_sizes, self.image_offsets)
+
+    def _replay(self) -> None:
+        if len(self._graphs) == 1:
+            self._graphs[0].replay()
+        else:
+            self._graphs[0].replay()
+            self.all_sizes = self.size_gather(self.sizes)
+            self._graphs[1].replay()
 
     def check(self, reference: torch.Tensor) -> None:
         if int(self.enc_status.abs().sum().item()) or int(self.dec_status.abs().sum().item()):

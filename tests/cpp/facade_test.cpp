@@ -323,14 +323,14 @@ int bench(int argc, char** argv) {
   size_t const blocks = argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 4096;
   std::vector<int> threads;
   size_t kib = 64;
-  int depth = 4;
+  int depth = 0;  // 0: the library's default
   for (int i = 3; i < argc; ++i) {
     if (std::string(argv[i]).rfind("--kib=", 0) == 0) kib = std::strtoul(argv[i] + 6, nullptr, 10);
     else if (std::string(argv[i]).rfind("--depth=", 0) == 0) depth = std::atoi(argv[i] + 8);
     else threads.push_back(std::atoi(argv[i]));
   }
   if (threads.empty()) threads = {1, 8, 64};
-  ricepp_amd::set_facade_pipeline_depth(depth);
+  if (depth) ricepp_amd::set_facade_pipeline_depth(depth);
   size_t const n = kib * 512;  // samples per block
   auto c = cfg(128, 1, true, 0);
   std::vector<std::vector<uint16_t>> in(blocks);

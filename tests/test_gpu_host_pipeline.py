@@ -88,3 +88,34 @@ def test_pack_batch_empty_and_scan_total():
                                 C.c_void_p(torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     assert st == 0 and int(tot.item()) == 0
+
+
+@pytest.mark.parametrize("kind", ["blocks", "long"])
+def test_shard_pipeline_graph_replay_exact(kind):
+    """parallel.ShardPipeline.capture (the bench's HIP-graph step): after an eager step, replayed steps give
+    the same encoded streams (oracle-exact) and decode every block exactly, for short blocks (one wave each)
+    and for a batch with long streams (segmented encode and decode, side-stream fork/join inside the graph)."""
+    from dwarfs_amd import parallel
+
+    rng = np.random.default_rng(17 if kind == "blocks" else 18)
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    oc = O.cfg(128, 1, True, 0)
+    lens = [32768] * 48 if kind == "blocks" else [1 << 19, 3000, 1 << 18, 40000]
+    blocks = [datagen.poisson_data(rng, n) for n in lens]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    x = torch.from_numpy(np.concatenate(blocks).view(np.int16)).to("cuda:0")
+    pipe = parallel.ShardPipeline(cfg, x, offs, np.asarray(lens, np.int64))
+    pipe.step()
+    torch.cuda.synchronize()
+    pipe.check(x)
+    pipe.capture()
+    pipe.data.zero_()
+    pipe.decoded.zero_()
+    for _ in range(3):
+        pipe.step()
+    torch.cuda.synchronize()
+    pipe.check(x)
+    data, sizes = pipe.data.cpu().numpy(), pipe.sizes.cpu().numpy()
+    for i, b in enumerate(blocks):
+        o = int(pipe.out_offsets[i])
+        assert data[o:o + int(sizes[i])].tobytes() == O.encode(oc, b), i

@@ -574,3 +574,57 @@ def test_segmented_decode_default_16mib_bs512_block():
     run_batch(codec.CodecConfig(512, 1, "big", 0), blocks)
     st = codec.segmented_decode_stats(reset=True)
     assert st["met"] > 0 and st["fallback"] == 0, st
+
+
+# ---- bs 16 / 32: four streams per wave (rpp_decode_rows_kernel), the rest by the fused kernel ----
+
+@pytest.mark.parametrize("bs", [16, 32])
+@pytest.mark.parametrize("cs", [1, 2])
+@pytest.mark.parametrize("be,ulsb", [(True, 0), (False, 3), (True, 6)])
+def test_rows_decode_matches_oracle(bs, cs, be, ulsb):
+    """The default (auto) decode of bs 16 / 32 batches runs the four-streams-per-wave kernel and hands every
+    stream it cannot take (raw, fs 0 or >= 8, a sub-block past its 384-bit window, odd arguments) to the
+    fused kernel: every stream must decode to the oracle's samples whichever kernel took it, and mixing
+    both kinds in one wave (rows of one wave: consecutive streams) must not disturb either.  Sizes: ragged
+    last chunks, zero- and one-chunk streams, more than 16 streams (several workgroups), byte offsets."""
+    rng = np.random.default_rng(3000 + 10 * bs + cs + ulsb)
+    sizes = [0, cs, bs * cs, bs * cs + cs, 3 * bs * cs - cs] + [int(x) * cs for x in rng.integers(1, 6000, 27)]
+    cfg = codec.CodecConfig(bs, cs, "big" if be else "little", ulsb)
+    blocks = _kind_blocks(rng, sizes, cs, ulsb, be)
+    run_batch(cfg, blocks)
+    _decode_oracle_streams(cfg, blocks, ragged=True)
+    # a wave of four Poisson streams at every bit depth the configs[4] sweep uses (fs 1..7: the rows path)
+    for lam in (4.0, 60.0, 250.0, 1000.0):
+        run_batch(cfg, [datagen.poisson_data(rng, 32768 // cs * cs, lam=lam, ulsb=ulsb, big_endian=be)
+                        for _ in range(20)])
+
+
+def test_rows_decode_truncated_and_corrupt_streams():
+    """Truncated and corrupt bs 16 / 32 streams through the default decode: the status and the samples must be
+    the oracle's (the rows kernel hands such streams to the fused kernel, which owns the error contract)."""
+    rng = np.random.default_rng(77)
+    for bs in (16, 32):
+        cfg = codec.CodecConfig(bs, 1, "big", 0)
+        oc = ocfg(cfg)
+        blocks = [datagen.poisson_data(rng, 5000) for _ in range(12)]
+        streams = [O.encode(oc, b) for b in blocks]
+        streams = [s[: len(s) * (i % 4 + 1) // 5] if i % 3 == 0 else s for i, s in enumerate(streams)]
+        streams[4] = rng.integers(0, 256, len(streams[4]), dtype=np.uint8).tobytes()
+        offs, pos = [], 0
+        for s in streams:
+            offs.append(pos)
+            pos += (len(s) + 15) // 16 * 16
+        buf = np.zeros(pos + 16, np.uint8)
+        for o, s in zip(offs, streams):
+            buf[o:o + len(s)] = np.frombuffer(s, np.uint8)
+        ns = [len(b) for b in blocks]
+        out, st = codec.decode_batch(cfg, torch.from_numpy(buf).to(DEV), offs, [len(s) for s in streams], ns)
+        torch.cuda.synchronize()
+        st, outn = st.cpu().numpy(), out.cpu().numpy().view(np.uint16)
+        p = 0
+        for i, s in enumerate(streams):
+            want_st, want = _oracle_status(oc, s, ns[i])
+            assert int(st[i]) == want_st, (bs, i, st[i], want_st)
+            if want_st == 0:
+                assert np.array_equal(outn[p:p + ns[i]], want), (bs, i)
+            p += ns[i]
