@@ -2137,7 +2137,7 @@ constexpr uint32_t kRowListWords = 4 + 2 * (kRowDump + kRowMT);
 constexpr uint32_t kRowWords = kRowRing + kRowPad + kRowListWords;
 constexpr uint32_t kRowsLdsBytes = kTabBytes + kRowsWaves * 4 * kRowWords * 4;
 #ifndef RPP_ROWS
-#define RPP_ROWS 0  // (off until measured on the GPU)
+#define RPP_ROWS 1  // 0: bs 16 / 32 one wave per stream too (profiles/r03_rows_sweep.jsonl)
 #endif
 constexpr bool kRowsDecode = RPP_ROWS != 0;
 

@@ -141,7 +141,9 @@ int rpp_encode_batch_ws(const rpp_config* cfg, const uint16_t* d_in, const uint6
  *   d_status      [nblocks] RPP_OK, RPP_TRUNCATED_INPUT (the reference's
  *                 std::out_of_range) or RPP_INVALID_ARGUMENT
  * This workspace-free form ALWAYS decodes one stream per wavefront (parse
- * and values fused), fully asynchronously on `stream`.  That is the fast
+ * and values fused; bs 16 / 32: four streams per wavefront, one per 16-lane
+ * row, any stream that path leaves then one per wavefront), fully
+ * asynchronously on `stream`.  That is the fast
  * path for batches of many short streams (thousands of 64 KiB blocks), but a
  * long stream then decodes at one wave's speed (a 16 MiB block: ~30 ms).
  * Batches with long streams should use rpp_decode_batch_ws, which splits
