@@ -200,8 +200,8 @@ def profiled_traffic(kernel: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=4096)
     ap.add_argument("--block-bytes", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
