@@ -78,9 +78,16 @@ def pipe_for(cfg, x, block_samples):
     return p
 
 
-def timed(fn, iters=5):
+def timed(fn, iters=5, warm_s=0.05):
+    # warm-up of at least warm_s seconds of GPU work: the clocks reach their
+    # steady state only after a few milliseconds (bench.py measures 662-677 GiB/s
+    # after 3 warm-up steps and 736-740 after 20)
+    t0 = time.perf_counter()
     fn()
     torch.cuda.synchronize()
+    while time.perf_counter() - t0 < warm_s:
+        fn()
+        torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best = float("inf")
