@@ -37,6 +37,7 @@ from dwarfs_amd import codec  # noqa: E402
 from dwarfs_amd import parallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+WARMUP_FLOOR_S = 0.5  # minimum warm-up time, whatever --warmup says
 
 
 def make_poisson_blocks(nblocks: int, n: int, lam: float, seed: int, device) -> torch.Tensor:
@@ -247,9 +248,18 @@ def main() -> None:
     torch.cuda.synchronize()
     pipe.check(x)
 
-    for _ in range(args.warmup):
+    # warm-up: the requested steps, then more until the GPU has run for at
+    # least WARMUP_FLOOR_S (its clocks settle only after a few ms of load: a
+    # count of steps alone made the driver's short command read ~8 % low)
+    tw = time.perf_counter()
+    warm_steps = 0
+    while warm_steps < args.warmup or time.perf_counter() - tw < WARMUP_FLOOR_S:
         pipe.step()
+        warm_steps += 1
+        if warm_steps % 8 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
+    warm_s = time.perf_counter() - tw
     # the step's kernel chain as a HIP graph (one per rank; with several ranks
     # the size all-gather stays eager between two graphs): removes the host
     # launch path and part of the inter-kernel gaps; checked once more below
@@ -304,6 +314,8 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_steps_run": warm_steps,
+            "warmup_s": round(warm_s, 3),
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
@@ -352,6 +364,8 @@ def main() -> None:
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_steps_run": warm_steps,
+        "warmup_s": round(warm_s, 3),
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",

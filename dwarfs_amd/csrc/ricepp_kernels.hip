@@ -28,24 +28,12 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <stdlib.h>
 
 #include "ricepp_amd.h"
 #include "ricepp_internal.h"
-
-// Diagnostic builds only: -DRPP_ABLATE=<mask> changes the decode to time
-// its parts (outputs are then wrong): 4 no async ring refill, 64 no output
-// stores in the fast loop; in the fast loop, per sub-block, 1024 / 4096 /
-// 32768 add 20 independent v_nop / v_add / v_perm, 2048 20 s_nop, 8192 /
-// 16384 an extra random / linear table read.
-#ifndef RPP_ABLATE
-#define RPP_ABLATE 0
-#endif
-// Encode ablations (diagnostic builds, outputs wrong): 1 code emission, 2 split walk.
-#ifndef RPP_EABLATE
-#define RPP_EABLATE 0
-#endif
 
 #ifdef RPP_STATS
 // Diagnostic build only (-DRPP_STATS): loop trip counters, summed over waves.
@@ -462,9 +450,9 @@ __device__ __forceinline__ void enc_plan_b(EncPlan<SPL>& P, EncState& st, uint32
       P.walking = false;
     }
   };
-  walk_step(P.walking && P.cand > 0 && P.cand < 14 && !(RPP_EABLATE & 2));
+  walk_step(P.walking && P.cand > 0 && P.cand < 14);
   for (;;) {
-    const bool act = P.walking && P.cand > 0 && P.cand < 14 && !(RPP_EABLATE & 2);
+    const bool act = P.walking && P.cand > 0 && P.cand < 14;
     if (!__any(act)) break;
     walk_step(act);
   }
@@ -493,7 +481,7 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
     emit_bits(st.win, pos, mode == 0 ? 0u : (mode == 1 ? fs + 1 : 15u));
     pos += 4;
   }
-  if (mode == 1 && !mask_tail && !(RPP_EABLATE & 1)) {
+  if (mode == 1 && !mask_tail) {
     // every lane owns SPL samples: two codes per packed step.  The '1' of
     // code i sits at e_i = e_(i-1) + k + q_i; the code value (1 | r << 1,
     // <= 15 bits) is OR-ed in by one 64-bit shift and two ds_or_b32.
@@ -510,7 +498,7 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
     // the pair (2h, 2h+1) spans k + q_(2h+1) + k bits from code 2h's '1':
     // when that fits 32 bits for every pair of the wave (fs <= 13 and unary
     // runs short: Poisson data), one 64-bit shift and two ds_or_b32 per pair
-    if (!__any(2u * k + (as_u32(qmax) >> 16) > 32u) && !(RPP_EABLATE & 4)) {
+    if (!__any(2u * k + (as_u32(qmax) >> 16) > 32u)) {
 #pragma unroll
       for (uint32_t h = 0; h < SPL / 2; ++h) {
         const uint32_t qq = as_u32(qv[h]);
@@ -531,7 +519,7 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
         emit_bits64(st.win, e, cc >> 16);
       }
     }
-  } else if (mode == 1 && !(RPP_EABLATE & 1)) {
+  } else if (mode == 1) {
     const uint32_t lowmask = (1u << fs) - 1u;
 #pragma unroll
     for (uint32_t i = 0; i < SPL; ++i) {
@@ -651,7 +639,7 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint32_t nsb_full = vec_ok ? min(N / chunk_len, c_hi) * CS : 0u;
   const uint32_t nfull = nsb_full > s_lo ? (nsb_full - s_lo) / spw : 0u;
   const bool empty_lanes = G * SPL != bs;
-  const bool dpp_prev = CS == 1 && !empty_lanes && !(RPP_EABLATE & 4);
+  const bool dpp_prev = CS == 1 && !empty_lanes;
 
   // ---- full iterations, software-pipelined: group it+1 is planned
   //      (deltas, split, positions) around the emission of group it, so the
@@ -1111,20 +1099,12 @@ RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", "0xa")
 RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc")
 // the persistent destination registers of the six steps and of the final
 // shift, initialised to the identity map (opaque to the compiler)
-#ifndef RPP_SPEC
-#define RPP_SPEC 0  // entry states from 2^RPP_SPEC-segment compositions when constant (0: the full scan)
-#endif
 struct ScanRegs {
   Map8 r1, r2, r4, r8, b15, b31, w1;
-  // entry-state rounds (jacobi8, fs >= 8 loop): lane 0 holds the window's
+  // entry-state rounds (w32_count, fs >= 8 loop): lane 0 holds the window's
   // entry state (skip the 4-bit header) in replicated form and is never
   // written
   uint32_t ja, jb;
-#if RPP_SPEC
-  // short compositions (spec_sel): lane 0 keeps the constant map "-> 4" (the
-  // window's entry: skip the header), lanes 1.. are rewritten every time
-  Map8 c1, c2, c3, c4;
-#endif
   __device__ ScanRegs() {
     Map8* all[7] = {&r1, &r2, &r4, &r8, &b15, &b31, &w1};
     for (Map8* x : all) {
@@ -1134,13 +1114,6 @@ struct ScanRegs {
     }
     ja = jb = 0x04040404u;
     asm volatile("" : "+v"(ja), "+v"(jb));
-#if RPP_SPEC
-    Map8* cs[4] = {&c1, &c2, &c3, &c4};
-    for (Map8* x : cs) {
-      x->lo = x->hi = 0x04040404u;
-      asm volatile("" : "+v"(x->lo), "+v"(x->hi));
-    }
-#endif
   }
 };
 // the value of lane l-1 into `keep` (lane 0 keeps its value)
@@ -1148,43 +1121,8 @@ __device__ __forceinline__ uint32_t jshift(uint32_t x, uint32_t& keep) {
   asm("s_nop 1\n\tv_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(keep) : "v"(x));
   return keep;
 }
-// Entry states of the lanes' segments by fixed-point rounds instead of the
-// map scan.  With E_0 = 4 (skip the header), E_l = M_(l-1)(E_(l-1)) defines
-// the exact entry states; a round sets E_l <- M_(l-1)(E_l-1) for all lanes at
-// once (one v_perm + one DPP move), starting from "state 0 before every
-// lane".  Parses from different states of a Rice stream merge within a few
-// codes, so after R rounds E is exact for every lane whose R preceding
-// segments merge all entry states.  Returns E after R + 1 rounds in selector
-// form (the state replicated in all four bytes) and in `unsettled` the lanes where
-// the last round still changed E.  If no lane up to l changed, E is exact up
-// to lane l (induction from lane 0), so the caller needs the map scan only
-// when an unsettled lane lies before the sub-block's end (rare).
-#ifndef RPP_PRIO
-#define RPP_PRIO 1  // wave priority over the fast loop's parse chain (0: off)
-#endif
-#ifndef RPP_PRIO_TOP
-#define RPP_PRIO_TOP 0  // diagnostics: raise it from the ring read before the parse
-#endif
-#ifndef RPP_PRIO_MID
-#define RPP_PRIO_MID 0  // diagnostics: drop it for the previous sub-block's stores inside the parse
-#endif
-#ifndef RPP_END_SCALAR
-#define RPP_END_SCALAR 0  // 1: fs 5-7 loop end by one packed readlane + scalar bit clearing (measured 245 vs 239 us, profiles/r03_decode_ab.jsonl)
-#endif
-#ifndef RPP_JACOBI
-#define RPP_JACOBI 0  // measured: rounds 4 / 6 / 8 = 286 / 267 / 265 us vs 262 us with the scan (bench decode)
-#endif
-template <int R>
-__device__ __forceinline__ uint32_t jacobi8(Map8 M, ScanRegs& sr, uint64_t& unsettled) {
-  uint32_t ea = jshift(__builtin_amdgcn_perm(M.hi, M.lo, 0u), sr.ja), eb = 0;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (r & 1) ea = jshift(__builtin_amdgcn_perm(M.hi, M.lo, eb), sr.ja);
-    else eb = jshift(__builtin_amdgcn_perm(M.hi, M.lo, ea), sr.jb);
-  }
-  unsettled = __ballot(ea != eb);
-  return (R & 1) ? eb : ea;
-}
+// wave priority over the fast loop's parse chain (profiles/r02_prio_ab.jsonl)
+constexpr int kParsePrio = 1;
 
 // fs >= 8: states 0..13 (13 remainder bits still to skip at most).  A state
 // is kept replicated in all four bytes of a dword (a v_perm selector that
@@ -1508,7 +1446,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   // next bit to be read)
   auto ring_keep = [&](uint32_t q) {
     if (pend && fill_w < (q >> 5) + kAhead + 128) retire();
-    if (!(RPP_ABLATE & 4) && !pend && fill_w <= (q >> 5) + 766) request();
+    if (!pend && fill_w <= (q >> 5) + 766) request();
   };
   const uint32_t nsb = nchunks * CS;
   // sub-blocks the fast loop may take: those of full 128-sample chunks
@@ -1589,17 +1527,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // halves), so that sub-block's value prefix costs no scan of its own.
       auto parse = [&](uint32_t q, uint32_t xl, uint32_t xh, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint4 e3,
                        uint32_t& Pe, uint32_t rider, uint32_t& rider_incl, auto&& mid) -> bool {
-#if RPP_PRIO
-        __builtin_amdgcn_s_setprio(RPP_PRIO);
-#endif
+        __builtin_amdgcn_s_setprio(kParsePrio);
         const uint32_t k = fs + 1;
         uint32_t tm, cnt, incl;
         uint64_t finm;
-        // lanes up to the first one that ends the sub-block (all when none
-        // does)
-        auto upto_end = [](uint64_t fm) {
-          return (2ull << (uint32_t)__builtin_ctzll(fm | (1ull << 63))) - 1ull;
-        };
         if constexpr (!W32) {
           const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});  // (also gives byte 2's entry state)
           const Map8 M = comp8(Map8{e2.x, e2.y}, M01);
@@ -1625,31 +1556,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
             const uint32_t a2 = __builtin_amdgcn_perm(e2.w, e2.z, __builtin_amdgcn_perm(M01.hi, M01.lo, sel));
             return __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x0C0C0400u), 0x0C040100u);
           };
-#if RPP_SPEC
-          // Lane l's entry state is E_l = X_l(E_(l-1)) with X_l = M_(l-1)
-          // (X_0 = the constant map to 4).  Parses of a Rice stream from
-          // different states merge within a few codes, so the composition of
-          // the 2 (RPP_SPEC 1) or 4 (RPP_SPEC 2) segments before a lane is
-          // almost always a constant map, which then is E_l whatever came
-          // before.  Lanes where it is not are flagged; the exact scan runs
-          // only when one of them lies before the sub-block's end (if none
-          // does, every lane up to the end is exact: induction from lane 0).
-          auto spec_sel = [&](uint64_t& nonconst) {
-            const Map8 X = shift8_wave(M, sreg.c1);
-            Map8 C = comp8(X, shift8_wave(X, sreg.c2));
-            if constexpr (RPP_SPEC >= 2) C = comp8(C, shift8_wave(shift8_wave(C, sreg.c3), sreg.c4));
-            const uint32_t r = __builtin_amdgcn_perm(C.hi, C.lo, 0u);  // entry 0, in all four bytes
-            nonconst = __ballot((C.lo != r) | (C.hi != r));
-            return r;
-          };
-          uint64_t unsettled;
-          tm = term_mask(spec_sel(unsettled));
-#elif RPP_JACOBI > 0
-          uint64_t unsettled;
-          tm = term_mask(jacobi8<RPP_JACOBI>(M, sreg, unsettled));
-#else
           tm = term_mask(scan_sel());
-#endif
           cnt = __builtin_popcount(tm);
           const uint32_t incl2 = wave_incl_sum(cnt | (rider << 16));
           incl = incl2 & 0xFFFFu;
@@ -1658,23 +1565,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           rider_incl = incl2 >> 16;
           // (the previous sub-block's stores, issued before the settle
           // branch so that they overlap this parse)
-#if RPP_PRIO && RPP_PRIO_MID
-          __builtin_amdgcn_s_setprio(0);
-#endif
           mid(rider_incl);
-#if RPP_PRIO && RPP_PRIO_MID
-          __builtin_amdgcn_s_setprio(RPP_PRIO);
-#endif
           finm = __ballot(incl >= n);
-#if RPP_JACOBI > 0 || RPP_SPEC
-          if (unsettled & upto_end(finm)) {
-            RPP_STAT(9, 1);
-            tm = term_mask(scan_sel());
-            cnt = __builtin_popcount(tm);
-            incl = wave_incl_sum(cnt);
-            finm = __ballot(incl >= n);
-          }
-#endif
         } else {
           w32_count(e0, e1, e2, e3, n, rider, sreg, tm, cnt, incl, finm, rider_incl);
           mid(rider_incl);
@@ -1686,16 +1578,6 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // (bit 63 set: a defined lane when no lane ends the sub-block; Pe is
         // then unused)
         const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
-        constexpr bool kEndScalar = RPP_END_SCALAR && !W32 && MT == 4;
-        if constexpr (kEndScalar) {
-          // that lane's mask and exclusive count in one readlane (24 + 8 bits:
-          // excl < n <= 128 there), its r-th set bit found by the scalar unit
-          const uint32_t x = readlane(tm | (excl << 24), (int)lz);
-          const uint32_t r = n - 1 - (x >> 24);
-          const uint32_t m0 = x & 0xFFFFFFu, m1 = m0 & (m0 - 1u), m2 = m1 & (m1 - 1u), m3 = m2 & (m2 - 1u);
-          const uint32_t m = r == 0 ? m0 : r == 1 ? m1 : r == 2 ? m2 : m3;
-          Pe = q + SB * lz + (uint32_t)__builtin_ctz(m | 0x80000000u) + k;
-        }
         // terminator positions t0 < t1 < ... in the segment (garbage past
         // cnt)
         uint32_t t[MT];
@@ -1704,7 +1586,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           t[j] = ffbl(tm);
           tm &= tm - 1;
         }
-        if constexpr (!kEndScalar) {
+        {
           // (positions <= 23 packed in bytes and picked by one bit-field
           // extract: a few vector ops rather than a chain of scalar ones)
           const uint32_t r = n - 1 - excl;
@@ -1720,9 +1602,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
           Pe = q + SB * lz + readlane(tend, (int)lz) + k;
         }
-#if RPP_PRIO
         __builtin_amdgcn_s_setprio(0);
-#endif
         RPP_TSTAMP(8);
         // pair excl + j for j = MT-1 .. 0, one instruction each (kept apart:
         // a merged ds_write2 would put two j in one instruction): a slot past
@@ -1770,11 +1650,9 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (TWO) or c (mod 2^16)
         if constexpr (!TWO) {
           const uint32_t o = SH ? px_write2(v1, selbe, ulsb) : __builtin_amdgcn_perm(v1, v1, selbe);
-          if (!(RPP_ABLATE & 64)) {
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, lane_off1,
-                                                  (int)(2 * ((sx / CS) * chunk_len + comp)), 0);
-            vm_after += 1;
-          }
+          __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, lane_off1,
+                                                (int)(2 * ((sx / CS) * chunk_len + comp)), 0);
+          vm_after += 1;
           const uint32_t lnew = lastc + wave_last(inc);
           if (comp) last1 = lnew;
           else last0 = lnew;
@@ -1784,17 +1662,15 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // in one v_perm when there is no shift
         const uint32_t o = SH ? px_write2(__builtin_amdgcn_perm(v1, v1 - d1, 0x05040100u), selbe, ulsb)
                               : __builtin_amdgcn_perm(v1, v1 - d1, selpack);
-        if (!(RPP_ABLATE & 64)) {
-          // buffer stores: scalar base + 32-bit lane offset
-          if constexpr (CS == 1) {
-            __builtin_amdgcn_raw_buffer_store_b32(o, orsrc, 4 * lane, (int)(sx * (2 * n)), 0);
-            vm_after += 1;
-          } else {
-            const int sbase = (int)(2 * ((sx / CS) * chunk_len + comp));
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, 4 * CS * lane, sbase, 0);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(o >> 16), orsrc, 4 * CS * lane + 2 * CS, sbase, 0);
-            vm_after += 2;
-          }
+        // buffer stores: scalar base + 32-bit lane offset
+        if constexpr (CS == 1) {
+          __builtin_amdgcn_raw_buffer_store_b32(o, orsrc, 4 * lane, (int)(sx * (2 * n)), 0);
+          vm_after += 1;
+        } else {
+          const int sbase = (int)(2 * ((sx / CS) * chunk_len + comp));
+          __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, 4 * CS * lane, sbase, 0);
+          __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(o >> 16), orsrc, 4 * CS * lane + 2 * CS, sbase, 0);
+          vm_after += 2;
         }
         // (kept mod 2^32 here, only the low 16 bits count; masked when the
         // loop is left)
@@ -1845,9 +1721,6 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           aprev = list[2 * lane - 2];
         }
         uint32_t xhB;
-#if RPP_PRIO && RPP_PRIO_TOP
-        __builtin_amdgcn_s_setprio(RPP_PRIO);  // (the chain: ring read, lookups, parse)
-#endif
         const uint32_t xlB = seg_bits(Pn, xhB);
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
         RPP_TSTAMP(1);
@@ -1856,26 +1729,6 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         lookups(xlB, fsB, e0, e1, e2, e3);
         uint32_t d1A, sumA, incA;
         deltas(tt, aprev, fs, d1A, sumA);
-        if (RPP_ABLATE & 1024) asm volatile(".rept 20\n\tv_nop\n\t.endr" ::: "memory");
-        if (RPP_ABLATE & 2048) asm volatile(".rept 20\n\ts_nop 0\n\t.endr" ::: "memory");
-        if (RPP_ABLATE & 4096) {  // 20 independent integer VALU ops
-          uint32_t d0 = lane, d1 = lane + 1, d2 = lane + 2, d3 = lane + 3;
-          asm volatile(".rept 5\n\tv_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1\n\t.endr"
-                       : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
-        }
-        if (RPP_ABLATE & 32768) {  // 20 independent v_perm
-          uint32_t d0 = lane, d1 = lane + 1, d2 = lane + 2, d3 = lane + 3;
-          asm volatile(".rept 5\n\tv_perm_b32 %0, %0, %1, %2\n\tv_perm_b32 %1, %1, %2, %3\n\tv_perm_b32 %2, %2, %3, %0\n\tv_perm_b32 %3, %3, %0, %1\n\t.endr"
-                       : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
-        }
-        if (RPP_ABLATE & 8192) {  // one extra random table read
-          const uint4 x = tab[256u * fsB + ((xlB >> 4) & 0xFFu)];
-          asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w));
-        }
-        if (RPP_ABLATE & 16384) {  // one extra conflict-free read
-          const uint4 x = tab[256u * fsB + lane];
-          asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w));
-        }
         RPP_TSTAMP(2);
         uint32_t PnB;
         ok = parse(Pn, xlB, xhB, fsB, e0, e1, e2, e3, PnB, sumA, incA,
@@ -3560,6 +3413,19 @@ int launch_seg_guess(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
+// CUs of the current device, queried once per device (callers on any thread:
+// the facade's driver threads run segmented decodes concurrently)
+int device_cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
 int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples,
                      const uint64_t* d_sb_base, uint32_t* d_sb_pos, int32_t* d_status, const SegView& sv,
@@ -3567,13 +3433,7 @@ int launch_parse_seg(const rpp_config* cfg, const uint8_t* d_in, const uint64_t*
   if (nblocks == 0 || sv.units_max == 0) return RPP_OK;
   // pass 0: a work queue, one workgroup per CU; rerun passes have a few units
   // to do: one wave per workgroup, one unit each
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      cus = n;
-    if (cus <= 0) cus = 256;
-  }
+  const int cus = device_cu_count();
   // (pass 0: as many waves per workgroup as the unit bound needs to give every
   // CU some, at most 16, so that a batch of few units still spreads over all CUs)
   const uint32_t wave_words = parse_wave_words(cfg->block_size);

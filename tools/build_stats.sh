@@ -1,1 +1,2 @@
-hipcc -O3 -std=c++20 --offload-arch=gfx950 -fPIC -shared -DRPP_STATS -Iinclude -o dwarfs_amd/lib/libricepp_amd_stats.so dwarfs_amd/csrc/ricepp_kernels.hip dwarfs_amd/csrc/fits_lsb.hip dwarfs_amd/csrc/batch_image.hip dwarfs_amd/csrc/ricepp_frame.cpp dwarfs_amd/csrc/ricepp_facade.cpp
+# Diagnostic build with per-phase s_memtime stamps (-DRPP_STATS) -> dwarfs_amd/lib/libricepp_amd_stats.so
+bash "$(dirname "$0")/variant.sh" stats -DRPP_STATS
