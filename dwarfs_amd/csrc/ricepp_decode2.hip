@@ -1280,6 +1280,13 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
                                              path_of(opt) != RPP_DECODE_FUSED);
   const Workspace w = layout(cfg, total_samples, max_stream_samples, nblocks, L, static_cast<uint8_t*>(d_workspace));
   if (!d_workspace || workspace_bytes < w.bytes) return RPP_INVALID_ARGUMENT;
+  // the side stream is created on the current device: the caller's stream
+  // must belong to it (include/ricepp_amd.h, rpp_decode_batch_ws)
+  {
+    int cur = 0, sdev = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(s, &sdev) != hipSuccess) return RPP_HIP_ERROR;
+    if (cur != sdev) return RPP_INVALID_ARGUMENT;
+  }
   SideStream* side = side_stream_for(s);
   if (!side) return RPP_HIP_ERROR;
   const uint32_t chunk_len = cfg->block_size * cfg->component_stream_count;

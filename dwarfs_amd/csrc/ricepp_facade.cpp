@@ -58,7 +58,13 @@ rpp_config to_rpp(codec_config const& c) {
 size_t align16(size_t v) { return (v + 15) & ~size_t{15}; }
 
 std::atomic<uint64_t> g_enc_launches{0}, g_enc_blocks{0}, g_dec_launches{0}, g_dec_blocks{0}, g_ctx_created{0};
-std::atomic<uint32_t> g_ctx_faults{0};  // inject_context_failures
+std::atomic<uint32_t> g_ctx_faults{0};     // inject_context_failures
+std::atomic<uint32_t> g_launch_faults{0};  // inject_launch_failures
+// a test hook: throws once per injected launch failure
+void maybe_fail_launch() {
+  for (uint32_t n = g_launch_faults.load(); n;)
+    if (g_launch_faults.compare_exchange_weak(n, n - 1)) throw std::runtime_error("ricepp_amd: injected launch failure");
+}
 std::atomic<uint64_t> g_stage_ns{0}, g_device_ns{0}, g_finish_ns{0};
 inline uint64_t now_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -132,7 +138,22 @@ class device_ctx {
     return static_cast<uint8_t*>(d);
   }
   void sync() { hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
-  // on release (the stream is idle: every batch ends with its event)
+  // Waits for everything enqueued on the stream (a failed launch may have
+  // left copies or kernels on it that still use the buffers); false if the
+  // stream is in error, and the context must not be used again.
+  bool drain() { return hipStreamSynchronize(stream_) == hipSuccess; }
+  // frees everything (a context whose stream failed; errors ignored)
+  void destroy() {
+    for (uint8_t* q : {hin_, hout_})
+      if (q) (void)hipHostFree(q);
+    for (uint8_t* q : {dbuf_, wbuf_})
+      if (q) (void)hipFree(q);
+    (void)hipEventDestroy(event_);
+    (void)hipStreamDestroy(stream_);
+    hin_ = hout_ = dbuf_ = wbuf_ = nullptr;
+    hin_cap_ = hout_cap_ = dcap_ = wcap_ = 0;
+  }
+  // on release, after drain()
   void trim() {
     for (auto* q : {&hin_, &hout_}) {
       size_t& cap = q == &hin_ ? hin_cap_ : hout_cap_;
@@ -214,8 +235,22 @@ class ctx_pool {
     }
     return new device_ctx(dev);
   }
+  // Drains the context's stream (idle in the normal case: a batch ends with
+  // its event; after a failed launch it may still hold work) and pools it,
+  // or destroys it when its stream is in error.  Never called with a queue
+  // lock held: the drain and the trim may synchronise.
   void release(device_ctx* c) {
-    c->trim();
+    try {
+      device_guard g{c->device()};
+      if (!c->drain()) {
+        c->destroy();
+        delete c;
+        return;
+      }
+      c->trim();
+    } catch (...) {  // (hipSetDevice failed: keep the context out of the pool)
+      return;
+    }
     std::lock_guard<std::mutex> lk(mu_);
     free_[c->device()].push_back(c);
   }
@@ -255,9 +290,11 @@ class ctx_lease {
 //     with one wake-up of all its callers;
 //   * every caller copies its own result out; the last one returns the
 //     context to the pool.
-// So a call costs one reservation, two copies and one futex wait; no caller
-// ever makes a HIP call or waits on the device, and the device keeps up to
-// g_max_active batches in flight.
+// So a call costs one reservation, two copies and one futex wait, and the
+// device keeps up to g_max_active batches in flight.  Callers make HIP calls
+// only to bring up a batch (a pooled context, pinned staging) and to return
+// its context to the pool, never with the queue's lock held; they never wait
+// on the device.
 struct batch;
 
 struct request {
@@ -314,7 +351,10 @@ class batch_queue {
       driver_started_ = true;
     }
     batch* b = reserve(lk, r);  // (may throw: nothing holds r yet)
+    std::vector<device_ctx*> unused;
+    unused.swap(discarded_);
     lk.unlock();
+    for (device_ctx* c : unused) ctx_pool::get().release(c);
     if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
     lk.lock();
     ++b->staged;
@@ -325,7 +365,9 @@ class batch_queue {
     if (r.status == RPP_OK && r.result_bytes) std::memcpy(r.out, r.pin_out, r.result_bytes);
     if (b->finished.fetch_add(1, std::memory_order_acq_rel) + 1 == b->reqs.size()) {
       lk.lock();
-      release(b);
+      device_ctx* c = release(b);
+      lk.unlock();
+      ctx_pool::get().release(c);
     }
   }
 
@@ -398,10 +440,9 @@ class batch_queue {
   // request at hand
   void discard(batch* b) {
     if (open_ == b) open_ = nullptr;
-    device_ctx* c = b->ctx;
+    discarded_.push_back(b->ctx);  // (returned to the pool once the lock is dropped)
     delete b;
     --alive_;
-    ctx_pool::get().release(c);
   }
 
   // (lk held) no more requests join b
@@ -444,6 +485,11 @@ class batch_queue {
           hip_check(hipEventRecord(b->ctx->event(), b->ctx->stream()), "hipEventRecord");
         } catch (std::exception const& e) {
           err = e.what();
+          // part of the batch may be on the stream already (copies, kernels
+          // writing the mapped pinned output): let it finish before the
+          // callers are released and the buffers reused (a stream in error
+          // makes release() destroy the context instead of pooling it)
+          (void)b->ctx->drain();
         }
         lk.lock();
         if (err.empty()) {
@@ -469,6 +515,7 @@ class batch_queue {
         continue;
       }
       polls = 0;
+      if (e != hipSuccess) (void)b->ctx->drain();
       lk.lock();
       flight_.pop_front();
       if (e != hipSuccess) {
@@ -502,14 +549,15 @@ class batch_queue {
     if (open_ && !open_->reqs.empty() && inflight_ < g_max_active.load(std::memory_order_relaxed)) close(open_);
   }
 
-  // (lk held) the last caller has copied its result out
-  void release(batch* b) {
+  // (lk held) the last caller has copied its result out; returns the
+  // context, for the caller to pool once it has dropped the lock
+  device_ctx* release(batch* b) {
     g_finish_ns.fetch_add(now_ns() - b->t_done, std::memory_order_relaxed);
     device_ctx* c = b->ctx;
     delete b;
     --alive_;
     res_cv_.notify_all();
-    ctx_pool::get().release(c);  // (the stream is idle: the event covered its last work)
+    return c;
   }
 
   // device: [in][u64 in_off | n | out_off | out_bytes | dst_off | total][i32 status][out slots]
@@ -541,6 +589,7 @@ class batch_queue {
     uint8_t* dslots = d + in_total + arr;
     hipStream_t s = ctx.stream();
     hip_check(hipMemcpyAsync(d, b.pin_in, in_total + 3 * nb * 8, hipMemcpyHostToDevice, s), "H2D encode input");
+    maybe_fail_launch();
     int st = rpp_encode_batch_ws(&cfg_, reinterpret_cast<uint16_t const*>(d), d64, d64 + nb, static_cast<uint32_t>(nb),
                                  dslots, d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes,
                                  s);
@@ -601,6 +650,7 @@ class batch_queue {
                                    reinterpret_cast<int32_t*>(dout + out_total), b.total_samples, b.max_samples,
                                    nullptr, 0, s);
       if (st != RPP_OK) throw_status(st);
+      maybe_fail_launch();
       g_dec_launches.fetch_add(1, std::memory_order_relaxed);
       g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);
       return;
@@ -611,6 +661,7 @@ class batch_queue {
     uint8_t* dout = d + in_total + 4 * nb * 8;
     auto* dst = reinterpret_cast<int32_t*>(dout + out_total);
     hip_check(hipMemcpyAsync(d, b.pin_in, in_total + 4 * nb * 8, hipMemcpyHostToDevice, s), "H2D decode input");
+    maybe_fail_launch();
     int st = rpp_decode_batch_ws(&cfg_, d, d64, d64 + nb, static_cast<uint32_t>(nb), reinterpret_cast<uint16_t*>(dout),
                                  d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes, s);
     if (st != RPP_OK) throw_status(st);
@@ -638,6 +689,7 @@ class batch_queue {
   std::vector<batch*> spare_;       // opened concurrently, not yet taking requests
   std::deque<batch*> ready_;        // closed and staged, to be launched
   std::deque<batch*> flight_;       // launched, in launch order
+  std::vector<device_ctx*> discarded_;  // contexts of discarded batches, to pool unlocked
   int inflight_ = 0;                // closed, not yet completed
   int alive_ = 0;
   bool driver_started_ = false, driver_idle_ = false;
@@ -789,6 +841,8 @@ std::unique_ptr<decoder_interface<uint16_t>> create_decoder<uint16_t>(codec_conf
 }
 
 void inject_context_failures(uint32_t n) { g_ctx_faults.store(n); }
+
+void inject_launch_failures(uint32_t n) { g_launch_faults.store(n); }
 
 void set_facade_pipeline_depth(int batches) { g_max_active.store(std::max(1, std::min(batches, 16))); }
 

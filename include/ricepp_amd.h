@@ -42,8 +42,10 @@
  *
  * Memory: every pointer passed to the *_batch calls is DEVICE memory owned by
  * the caller (hipMalloc'd).  Calls are asynchronous on `stream` (a
- * hipStream_t; NULL = default stream).  Per-block status / sizes are written
- * to device arrays and are valid once the stream has been synchronised.
+ * hipStream_t; NULL = default stream), which must belong to the current
+ * device (rpp_decode_batch_ws / _ex return RPP_INVALID_ARGUMENT otherwise).
+ * Per-block status / sizes are written to device arrays and are valid once
+ * the stream has been synchronised.
  */
 #ifndef RICEPP_AMD_H
 #define RICEPP_AMD_H

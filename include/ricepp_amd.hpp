@@ -193,6 +193,11 @@ facade_stats get_facade_stats();
 // hipStreamCreate would), to exercise the error paths of the batch queue.
 void inject_context_failures(uint32_t n);
 
+// Test only: the next `n` batch launches fail after their first operation is
+// on the device's stream (as a failed kernel launch after the input copy
+// would), to exercise the drain of a failed batch before its buffers are reused.
+void inject_launch_failures(uint32_t n);
+
 // Benchmarks only: batches of one queue on the device at once (default 2: two
 // launches on different streams overlap on the device, more do not; clamped
 // to 1..16).
