@@ -182,9 +182,10 @@ def kernel_source_sha256() -> str:
     return h.hexdigest()
 
 
-def profiled_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from profiles/pmc_latest.json (rocprofv3 FETCH_SIZE / WRITE_SIZE
-    passes, gfx950 corrections of MI355X_MICROARCH.md), only if it was taken of the current sources."""
+def profiled_counters(kernel: str):
+    """PMC figures of `kernel` per launch from profiles/pmc_latest.json (rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes with the gfx950 corrections of MI355X_MICROARCH.md, GRBM_GUI_ACTIVE), only if they were taken
+    of the current kernel sources: (dict or None, provenance)."""
     pmc = ROOT / "profiles" / "pmc_latest.json"
     if not pmc.exists():
         return None, "no PMC profile"
@@ -194,8 +195,8 @@ def profiled_traffic(kernel: str):
         return None, "unreadable PMC profile"
     if j.get("kernel_source_sha256") != kernel_source_sha256():
         return None, "PMC profile of other kernel sources (stale); not reported"
-    v = j.get(kernel, {}).get("hbm_bytes_per_launch")
-    return v, f"{j.get('source', 'profiles')} (rocprofv3 PMC, kernel sources sha256 {j['kernel_source_sha256'][:12]})"
+    return j.get(kernel), f"{j.get('source', 'profiles')} (rocprofv3 PMC, kernel sources sha256 " \
+                         f"{j['kernel_source_sha256'][:12]})"
 
 
 def main() -> None:
@@ -353,7 +354,10 @@ def main() -> None:
             dist.destroy_process_group()
         return
 
-    traffic, traffic_src = profiled_traffic(f"rpp_{dominant}_kernel")
+    counters, traffic_src = profiled_counters(f"rpp_{dominant}_kernel")
+    traffic = counters.get("hbm_bytes_per_launch") if counters else None
+    # the launch's length in GPU cycles (GRBM_GUI_ACTIVE per XCD): the kernel's work, whatever the clock
+    kcycles = counters.get("cycles_per_launch") if counters else None
 
     total_bytes = raw_bytes * world * args.steps
     value = total_bytes / elapsed / 2**30
@@ -395,6 +399,8 @@ def main() -> None:
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "kernel_cycles_per_launch": kcycles,
+            "kernel_clock_GHz": round(kcycles / kt / 1e9, 3) if kcycles else None,
             "device_copy_GBps": round(device_copy_gbps(dev), 1),
         },
     }

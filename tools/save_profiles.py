@@ -27,5 +27,13 @@ for k, v in pmc.items():
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         latest[k] = {"hbm_bytes_per_launch": int((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024),
                      "fetch_kb": v["FETCH_SIZE"], "write_kb": v["WRITE_SIZE"]}
+        if "GRBM_GUI_ACTIVE" in v:
+            # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles: per XCD it is the launch's length in
+            # GPU clock cycles, independent of the clock the chip ran at
+            latest[k]["grbm_gui_active"] = v["GRBM_GUI_ACTIVE"]
+            latest[k]["cycles_per_launch"] = int(v["GRBM_GUI_ACTIVE"] / 8)
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT"):
+            if c in v:
+                latest[k][c] = v[c]
 (dst / "pmc_latest.json").write_text(json.dumps(latest, indent=1) + "\n")
 print(json.dumps(latest, indent=1))
