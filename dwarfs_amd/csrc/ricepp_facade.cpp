@@ -104,7 +104,7 @@ class device_guard {
 // context going back to the pool drops pinned buffers above kPinnedKeep and
 // device buffers above kDeviceKeep, so a burst of huge batches does not keep
 // GiBs of host memory pinned or of device memory reserved.
-constexpr size_t kPinnedKeep = size_t{64} << 20;
+constexpr size_t kPinnedKeep = size_t{320} << 20;  // (a batch of 8 x 16 MiB blocks: 128 + 64 MiB)
 constexpr size_t kDeviceKeep = size_t{256} << 20;
 
 class device_ctx {
@@ -333,6 +333,12 @@ constexpr size_t kMaxBatchBlocks = 8192;
 // pinned staging per batch (a larger single request gets a batch of its own size)
 constexpr size_t kBatchIn = size_t{8} << 20;
 constexpr size_t kBatchOut = size_t{16} << 20;
+// A batch opened by a request larger than kBatchOut / 4 (DwarFS blocks of
+// 4 MiB and up: mkdwarfs -S 22..30) has room for kLargeJoin requests of its
+// size, so that concurrent long blocks share one segmented launch and its
+// copies instead of one launch each (block_cache.cpp:628-706 issues them
+// from a worker pool).
+constexpr size_t kLargeJoin = 8;
 // batches of one queue on the device at once (set_facade_pipeline_depth
 // changes it for benchmarks)
 std::atomic<int> g_max_active{2};
@@ -417,8 +423,9 @@ class batch_queue {
     auto* b = new batch;
     try {
       c = ctx_pool::get().acquire(dev_);
-      b->in_cap = std::max(kBatchIn, need_in(r) + arrays_in(1));
-      b->out_cap = std::max(kBatchOut, need_out(r) + arrays_out(1));
+      const size_t join = need_out(r) > kBatchOut / 4 || need_in(r) > kBatchIn / 4 ? kLargeJoin : 1;
+      b->in_cap = std::max(kBatchIn, join * need_in(r) + arrays_in(join));
+      b->out_cap = std::max(kBatchOut, join * need_out(r) + arrays_out(join));
       device_guard g{dev_};
       b->pin_in = c->pin_in(b->in_cap);
       b->pin_out = c->pin_out(b->out_cap);

@@ -1082,7 +1082,11 @@ __device__ __forceinline__ Map8 scan_step8(Map8 m) {
 // bound_ctrl, so they keep the identity map the register was initialised
 // with -- no mask, no vcc.  s_nop 1: a DPP read of a VGPR written by the
 // previous VALU instruction needs two wait states.
-#define RPP_SCAN8_STEP(NAME, CTRL, RM)                                                                    \
+#ifndef RPP_ASM_DPP
+#define RPP_ASM_DPP 1
+#endif
+#if RPP_ASM_DPP
+#define RPP_SCAN8_STEP(NAME, CTRL, RM, CT, RMI)                                                           \
   __device__ __forceinline__ Map8 NAME(Map8 m, Map8& keep) {                                              \
     asm("s_nop 1\n\t"                                                                                    \
         "v_mov_b32_dpp %0, %2 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"                                \
@@ -1091,12 +1095,22 @@ __device__ __forceinline__ Map8 scan_step8(Map8 m) {
         : "v"(m.lo), "v"(m.hi));                                                                          \
     return comp8(m, keep);                                                                                \
   }
-RPP_SCAN8_STEP(scan8_shr1, "row_shr:1", "0xf")
-RPP_SCAN8_STEP(scan8_shr2, "row_shr:2", "0xf")
-RPP_SCAN8_STEP(scan8_shr4, "row_shr:4", "0xf")
-RPP_SCAN8_STEP(scan8_shr8, "row_shr:8", "0xf")
-RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", "0xa")
-RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc")
+#else
+// (the intrinsic form: `keep` is loop-carried, so the move writes the same
+// register, and the compiler schedules the moves and their wait states)
+#define RPP_SCAN8_STEP(NAME, CTRL, RM, CT, RMI)                                    \
+  __device__ __forceinline__ Map8 NAME(Map8 m, Map8& keep) {                      \
+    keep.lo = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.lo, (int)m.lo, CT, RMI, 0xF, false); \
+    keep.hi = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.hi, (int)m.hi, CT, RMI, 0xF, false); \
+    return comp8(m, keep);                                                        \
+  }
+#endif
+RPP_SCAN8_STEP(scan8_shr1, "row_shr:1", "0xf", kDppRowShr1, 0xF)
+RPP_SCAN8_STEP(scan8_shr2, "row_shr:2", "0xf", kDppRowShr2, 0xF)
+RPP_SCAN8_STEP(scan8_shr4, "row_shr:4", "0xf", kDppRowShr4, 0xF)
+RPP_SCAN8_STEP(scan8_shr8, "row_shr:8", "0xf", kDppRowShr8, 0xF)
+RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", "0xa", kDppRowBcast15, 0xA)
+RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc", kDppRowBcast31, 0xC)
 // the persistent destination registers of the six steps and of the final
 // shift, initialised to the identity map (opaque to the compiler)
 struct ScanRegs {
@@ -1147,11 +1161,16 @@ __device__ __forceinline__ uint32_t byte_term(uint32_t S, uint4 e) {
 #undef RPP_SCAN8_STEP
 // exclusive form: the map of lanes 0..l-1 (identity on lane 0)
 __device__ __forceinline__ Map8 shift8_wave(Map8 m, Map8& keep) {
+#if RPP_ASM_DPP
   asm("s_nop 1\n\t"
       "v_mov_b32_dpp %0, %2 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
       "v_mov_b32_dpp %1, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
       : "+v"(keep.lo), "+v"(keep.hi)
       : "v"(m.lo), "v"(m.hi));
+#else
+  keep.lo = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.lo, (int)m.lo, kDppWaveShr1, 0xF, 0xF, false);
+  keep.hi = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.hi, (int)m.hi, kDppWaveShr1, 0xF, 0xF, false);
+#endif
   return keep;
 }
 

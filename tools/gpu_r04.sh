@@ -1,0 +1,46 @@
+# Round-4 GPU session steps (run through gpurun; outputs under gpurun_out/r04/).
+# usage: bash tools/gpu_r04.sh step [step ...]
+#   isa      instruction-rate microbenchmark (tools/isa_rate)
+#   occ      fused-decode time vs waves per SIMD (tools/occupancy_sweep.py)
+#   bench    bench line, the driver's short command and the default one (no CPU baseline)
+#   variants bench line per library variant dwarfs_amd/lib/libricepp_amd_<v>.so (VARIANTS="a b")
+#   facade   C++ facade test, then its throughput bench (64 KiB, 1 / 16 MiB blocks)
+#   tests    the GPU test suite
+#   trace    rocprofv3 kernel trace of the bench workload
+#   pmc      PMC passes of the bench workload (tools/gpu_pmc.sh)
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r04
+mkdir -p $O
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$O/$name.out" 2> "$O/$name.err"
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -c 1500 "$O/$name.out"
+  if [ $rc -ne 0 ]; then tail -20 "$O/$name.err"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    isa) run isa 120 ./tools/isa_rate ;;
+    occ) run occ 240 python tools/occupancy_sweep.py ;;
+    bench)
+      run bench_short 240 python bench.py --no-cpu --steps 20 --warmup 5
+      run bench_def 240 python bench.py --no-cpu ;;
+    variants)
+      for v in ${VARIANTS:-}; do
+        RICEPP_AMD_LIB=$PWD/dwarfs_amd/lib/libricepp_amd_$v.so run "bench_$v" 240 python bench.py --no-cpu
+      done ;;
+    facade)
+      run facade_test 300 ./tests/cpp/build/facade_test
+      run facade_64k 300 ./tests/cpp/build/facade_test --bench 4096 16 64
+      run facade_1m 300 ./tests/cpp/build/facade_test --bench 256 --kib=1024 16 64
+      run facade_16m 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 4 16 ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    trace)
+      rm -rf $O/trace
+      run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu ;;
+    pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
