@@ -18,6 +18,8 @@
 #include <charconv>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -324,6 +326,7 @@ struct batch {
   uint64_t total_samples = 0, max_samples = 0;
   size_t staged = 0;  // (mutex)
   bool closed = false;
+  bool packed = true;  // encode: outputs packed back to back (else at their slots)
   std::atomic<uint32_t> done{0};      // results published (callers wait on it)
   std::atomic<size_t> finished{0};    // callers that have copied out
   uint64_t t_close = 0, t_launch = 0, t_done = 0;
@@ -339,6 +342,9 @@ constexpr size_t kBatchOut = size_t{16} << 20;
 // copies instead of one launch each (block_cache.cpp:628-706 issues them
 // from a worker pool).
 constexpr size_t kLargeJoin = 8;
+// encode batches whose worst-case output exceeds this go out by a DMA copy of
+// the slots instead of being packed into mapped host memory by a kernel
+constexpr size_t kPackMax = ~size_t{0};  // (no-pack path under investigation: kept off)
 // batches of one queue on the device at once (set_facade_pipeline_depth
 // changes it for benchmarks)
 std::atomic<int> g_max_active{2};
@@ -601,9 +607,17 @@ class batch_queue {
                                  dslots, d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes,
                                  s);
     if (st != RPP_OK) throw_status(st);
-    st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
-                        d64 + 5 * nb, s);
-    if (st != RPP_OK) throw_status(st);
+    b.packed = out_total <= kPackMax;
+    if (b.packed) {
+      st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
+                          d64 + 5 * nb, s);
+      if (st != RPP_OK) throw_status(st);
+    } else {
+      // long blocks: the slots as they are, by one DMA copy (kernel writes
+      // into mapped host memory ran at ~3.5 GB/s for tens of MiB, the copy
+      // engine at the PCIe rate; the slots' unused tails cross too)
+      hip_check(hipMemcpyAsync(b.pin_out, dslots, out_total, hipMemcpyDeviceToHost, s), "D2H encode slots");
+    }
     hip_check(hipMemcpyAsync(b.pin_out + out_total, d64 + 3 * nb, arr - 3 * nb * 8, hipMemcpyDeviceToHost, s),
               "D2H encode sizes");
     g_enc_launches.fetch_add(1, std::memory_order_relaxed);
@@ -617,8 +631,13 @@ class batch_queue {
       request* q = b.reqs[i];
       q->status = hst[i];
       q->result_bytes = hst[i] == RPP_OK ? r64[i] : 0;
-      q->pin_out = b.pin_out + r64[nb + i];
+      q->pin_out = b.pin_out + (b.packed ? r64[nb + i] : q->out_off);
       if (q->status == RPP_OK && q->result_bytes > q->out_cap) q->status = RPP_OUTPUT_TOO_SMALL;
+      if (q->status != RPP_OK && std::getenv("RICEPP_AMD_DEBUG_FACADE"))
+        std::fprintf(stderr, "ricepp_amd facade: encode batch nb=%zu total=%llu max=%llu in_fill=%zu out_fill=%zu "
+                     "packed=%d: block %zu n=%llu in_off=%zu out_off=%zu status=%d\n", nb,
+                     (unsigned long long)b.total_samples, (unsigned long long)b.max_samples, b.in_fill, b.out_fill,
+                     (int)b.packed, i, (unsigned long long)q->n_samples, q->in_off, q->out_off, q->status);
     }
   }
 

@@ -1137,6 +1137,18 @@ __device__ __forceinline__ uint32_t jshift(uint32_t x, uint32_t& keep) {
 }
 // wave priority over the fast loop's parse chain (profiles/r02_prio_ab.jsonl)
 constexpr int kParsePrio = 1;
+#ifndef RPP_END_LIST
+#define RPP_END_LIST 1  // the fast loop's sub-block end read back from the list (0: picked by readlane)
+#endif
+#ifndef RPP_EARLY_EXIT
+#define RPP_EARLY_EXIT 1  // the fast loop's continue tests as scalar branches before the parse (0: after it)
+#endif
+#ifndef RPP_RING_VALU
+#define RPP_RING_VALU 1  // window word addresses from q + 24 lane in vector code (0: scalar split of q)
+#endif
+#ifndef RPP_SDWA
+#define RPP_SDWA 1  // table entry offsets by SDWA byte selects (0: bit-field extract + shift-add)
+#endif
 
 // fs >= 8: states 0..13 (13 remainder bits still to skip at most).  A state
 // is kept replicated in all four bytes of a dword (a v_perm selector that
@@ -1293,6 +1305,25 @@ __device__ __forceinline__ uint32_t neg_lsb(uint32_t x) {
   uint32_t r;
   asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(r) : "v"(x));
   return r;
+}
+
+// 16 * byte B of x in one VOP2 operation (SDWA source select)
+template <int B>
+__device__ __forceinline__ uint32_t sdwa_byte16(uint32_t x) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(x));
+  else if constexpr (B == 1)
+    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(x));
+  else if constexpr (B == 2)
+    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(x));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(x));
+  return r;
+}
+// the table entry at byte offset off16 (16 * entry) from tb
+__device__ __forceinline__ uint4 tb_entry(const uint4* tb, uint32_t off16) {
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(tb) + off16);
 }
 
 // v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0
@@ -1516,26 +1547,28 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           xh = __builtin_amdgcn_alignbit(w2, w1, q & 31u);
           return __builtin_amdgcn_alignbit(w1, w0, q & 31u);
         } else {
+          // (vector addressing from q + lane24 alone: no scalar splitting of
+          // q; word wi + 1 <= kRingWords lies in the ring's mirror)
+#if RPP_RING_VALU
+          const uint32_t x = q + lane24;
+          const uint32_t* w = ring + ((x >> 5) & kRingMask);
+          xh = 0u;
+          return __builtin_amdgcn_alignbit(w[1], w[0], x);  // (shift x mod 32)
+#else
           const uint32_t o = lane24 + (q & 31u);
           uint32_t oi = o >> 5;
           asm("" : "+v"(oi));  // (else the compiler masks o >> 3: one more op)
           const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
           xh = 0u;
           return __builtin_amdgcn_alignbit(w[1], w[0], o);  // (shift o mod 32)
+#endif
         }
       };
-      // the header's fs clamped to [LO, HI] (scalar), so the lookups stay in
-      // range for any header; the loop only keeps sub-blocks whose fs is in
-      // range
-      auto fs_of = [](uint32_t h) {
-        uint32_t r;
-        asm("s_and_b32 %0, %1, 15\n\ts_max_u32 %0, %0, %2\n\ts_min_u32 %0, %0, %3\n\ts_sub_u32 %0, %0, 1"
-            : "=&s"(r)
-            : "s"(h), "n"(LO + 1), "n"(HI + 1)
-            : "scc");
-        return r;
-      };
-      auto header_ok = [](uint32_t h) { return (h & 15u) - (LO + 1) <= HI - LO; };
+      // the header's fs (scalar; not clamped: a header outside [LO+1, HI+1]
+      // -- which the loop then leaves -- makes lookups read other LDS words or
+      // out of range, which reads 0; their results are discarded)
+      auto fs_of = [](uint32_t h) { return (h & 15u) - 1u; };
+      auto header_ok = [](uint32_t h) { return (uint32_t)((h & 15u) - (LO + 1) <= HI - LO); };
       // Parse of the sub-block at bit q: entry states by the map scan,
       // terminators, (a_i, remainder) of code i into list pair i with a_i =
       // terminator position - (q + 4) - i k (the unary part of code i is then
@@ -1544,12 +1577,18 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // The count scan also carries a rider: the previous sub-block's delta
       // sums in the high halves (mod 2^16; counts <= 512 stay in the low
       // halves), so that sub-block's value prefix costs no scan of its own.
+      // The next window's bits are read from the ring as soon as Pe is known
+      // (into xln / xhn), before this sub-block's list writes, so that the
+      // read's LDS latency overlaps them instead of opening the next parse.
       auto parse = [&](uint32_t q, uint32_t xl, uint32_t xh, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint4 e3,
-                       uint32_t& Pe, uint32_t rider, uint32_t& rider_incl, auto&& mid) -> bool {
+                       uint32_t& Pe, uint32_t& xln, uint32_t& xhn, uint32_t rider, uint32_t& rider_incl,
+                       auto&& mid) -> uint32_t {
         __builtin_amdgcn_s_setprio(kParsePrio);
         const uint32_t k = fs + 1;
+        // (off the chain) the end is q + 4 + n k + a_(n-1)
+        const uint32_t pe_base = q + 4u + n * k;
         uint32_t tm, cnt, incl;
-        uint64_t finm;
+        uint32_t tot2;  // lane 63's inclusive sums: the window's code count (low), the rider's total (high)
         if constexpr (!W32) {
           const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});  // (also gives byte 2's entry state)
           const Map8 M = comp8(Map8{e2.x, e2.y}, M01);
@@ -1582,21 +1621,14 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           // (the rider in the high halves is exact whatever the counts: they
           // sum to at most 512 and never carry into it)
           rider_incl = incl2 >> 16;
-          // (the previous sub-block's stores, issued before the settle
-          // branch so that they overlap this parse)
-          mid(rider_incl);
-          finm = __ballot(incl >= n);
+          tot2 = readlane(incl2, kWave - 1);
         } else {
+          uint64_t finm;
           w32_count(e0, e1, e2, e3, n, rider, sreg, tm, cnt, incl, finm, rider_incl);
-          mid(rider_incl);
+          tot2 = readlane(incl, kWave - 1) | (readlane(rider_incl, kWave - 1) << 16);
         }
         const uint32_t excl = incl - cnt;
         RPP_TSTAMP(7);
-        // the next sub-block starts after code n-1's remainder: terminator
-        // n-1-excl (< MT) of the first lane whose inclusive count reaches n.
-        // (bit 63 set: a defined lane when no lane ends the sub-block; Pe is
-        // then unused)
-        const uint32_t lz = (uint32_t)__builtin_ctzll(finm | (1ull << 63));
         // terminator positions t0 < t1 < ... in the segment (garbage past
         // cnt)
         uint32_t t[MT];
@@ -1605,9 +1637,13 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           t[j] = ffbl(tm);
           tm &= tm - 1;
         }
+#if !RPP_END_LIST
         {
-          // (positions <= 23 packed in bytes and picked by one bit-field
-          // extract: a few vector ops rather than a chain of scalar ones)
+          // the next sub-block starts after code n-1's remainder: terminator
+          // n-1-excl (< MT) of the first lane whose inclusive count reaches
+          // n (positions <= 23 packed in bytes and picked by one bit-field
+          // extract); lane 63 when no lane ends the sub-block (Pe unused)
+          const uint32_t lz = (uint32_t)__builtin_ctzll(__ballot(incl >= n) | (1ull << 63));
           const uint32_t r = n - 1 - excl;
           uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
           if constexpr (MT > 4) {
@@ -1618,10 +1654,12 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
             const uint32_t tpk2 = t[8] | (t[9] << 8) | ((t[10] | (t[11] << 8)) << 16);
             tpk = r < 8 ? tpk : tpk2;
           }
-          const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8);
-          Pe = q + SB * lz + readlane(tend, (int)lz) + k;
+          const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8) + SB * lane;
+          Pe = q + k + readlane(tend, (int)lz);
         }
         __builtin_amdgcn_s_setprio(0);
+        xln = seg_bits(Pe, xhn);
+#endif
         RPP_TSTAMP(8);
         // pair excl + j for j = MT-1 .. 0, one instruction each (kept apart:
         // a merged ds_write2 would put two j in one instruction): a slot past
@@ -1640,8 +1678,19 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           list2[base + j] = make_uint2(abase + t[j] - j * k, rem);
           lds_fence();
         }
+#if RPP_END_LIST
+        // the next sub-block starts after code n-1's remainder: its pair,
+        // read back from the list (one broadcast LDS read after the writes,
+        // instead of picking the terminator out of the lane that holds it);
+        // unused when the sub-block does not end in the window
+        Pe = pe_base + __builtin_amdgcn_readfirstlane(list[2 * (n - 1)]);
+        __builtin_amdgcn_s_setprio(0);
+        xln = seg_bits(Pe, xhn);
+#endif
+        // (the previous sub-block's stores, off the chain)
+        mid(rider_incl, tot2 >> 16);
         RPP_TSTAMP(13);
-        return finm != 0;
+        return (uint32_t)((tot2 & 0xFFFFu) >= n);
       };
       // codes 2c, 2c+1 of a sub-block on lane c -> zig-zag deltas
       // (decode.h:66-69): d1 and the lane's sum d0 + d1
@@ -1663,7 +1712,8 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       };
       // inclusive prefix inc of the delta sums -> values -> stored samples of
       // sub-block sx
-      auto store = [&](uint32_t d1, uint32_t inc, uint32_t sx) {
+      // (inc_last: inc of lane 63, the sub-block's delta total)
+      auto store = [&](uint32_t d1, uint32_t inc, uint32_t inc_last, uint32_t sx) {
         const uint32_t comp = sx % CS;
         const uint32_t lastc = comp ? last1 : last0;
         const uint32_t v1 = lastc + inc;  // value of sample 2c + 1 (TWO) or c (mod 2^16)
@@ -1671,8 +1721,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           const uint32_t o = SH ? px_write2(v1, selbe, ulsb) : __builtin_amdgcn_perm(v1, v1, selbe);
           __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, lane_off1,
                                                 (int)(2 * ((sx / CS) * chunk_len + comp)), 0);
-          vm_after += 1;
-          const uint32_t lnew = lastc + wave_last(inc);
+          const uint32_t lnew = lastc + inc_last;
           if (comp) last1 = lnew;
           else last0 = lnew;
           return;
@@ -1684,37 +1733,51 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // buffer stores: scalar base + 32-bit lane offset
         if constexpr (CS == 1) {
           __builtin_amdgcn_raw_buffer_store_b32(o, orsrc, 4 * lane, (int)(sx * (2 * n)), 0);
-          vm_after += 1;
         } else {
           const int sbase = (int)(2 * ((sx / CS) * chunk_len + comp));
           __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o, orsrc, 4 * CS * lane, sbase, 0);
           __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(o >> 16), orsrc, 4 * CS * lane + 2 * CS, sbase, 0);
-          vm_after += 2;
         }
         // (kept mod 2^32 here, only the low 16 bits count; masked when the
         // loop is left)
-        const uint32_t lnew = lastc + wave_last(inc);
+        const uint32_t lnew = lastc + inc_last;
         if (comp) last1 = lnew;
         else last0 = lnew;
       };
+      // (entry offsets by SDWA byte selects: two VOP2 operations per byte
+      // instead of a bit-field extract and a shift-add, both VOP3)
       auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2, uint4& e3) {
         const uint4* tb = tab + 256u * fs;
+#if RPP_SDWA
+        e0 = tb_entry(tb, sdwa_byte16<0>(xl));
+        e1 = tb_entry(tb, sdwa_byte16<1>(xl));
+        e2 = tb_entry(tb, sdwa_byte16<2>(xl));
+        if constexpr (W32) e3 = tb_entry(tb, sdwa_byte16<3>(xl));
+#else
         e0 = tb[xl & 0xFFu];
         e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
         e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
         if constexpr (W32) e3 = tb[xl >> 24];
-        else e3 = make_uint4(0u, 0u, 0u, 0u);
+#endif
+        if constexpr (!W32) e3 = make_uint4(0u, 0u, 0u, 0u);
       };
 
       // Ring bounds, recomputed only when the ring changes: the next window
       // start may be at most pn_limit (resident look-ahead, the header
       // inside the input), and ring_keep has something to do once the
       // window start reaches word trig_w (lim >= P + 4 here).
-      uint32_t pn_limit, trig_w;
+      // (wave-uniform; readfirstlane keeps them in SGPRs for the loop's
+      // scalar tests)
+      uint32_t pn_limit, trig_bits;
       auto ring_bounds = [&]() {
-        pn_limit = min(lim - 4u, 32u * (fill_w - kAhead) + 31u);
-        trig_w = pend ? fill_w - (kAhead + 127u) : (fill_w > 766u ? fill_w - 766u : 0u);
+        pn_limit = __builtin_amdgcn_readfirstlane(min(lim - 4u, 32u * (fill_w - kAhead) + 31u));
+        trig_bits =
+            __builtin_amdgcn_readfirstlane(32u * (pend ? fill_w - (kAhead + 127u) : (fill_w > 766u ? fill_w - 766u : 0u)));
       };
+      // vector-memory stores per loop iteration (the previous sub-block's
+      // samples), counted into vm_after only when the ring is kept
+      constexpr uint32_t kStoresPerSub = TWO && CS == 2 ? 2u : 1u;
+      uint32_t s_keep = s;
       ring_bounds();
       // prologue: parse sub-block s
       uint32_t Pn;
@@ -1725,10 +1788,15 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       uint4 e0, e1, e2, e3;
       lookups(xl, fs, e0, e1, e2, e3);
       uint32_t unused_rider;
-      bool ok = parse(P, xl, xh, fs, e0, e1, e2, e3, Pn, 0u, unused_rider, [](uint32_t) {}) && header_ok(h);
+      uint32_t xlB, xhB;  // the window of the sub-block at Pn
+      uint32_t ok =
+          parse(P, xl, xh, fs, e0, e1, e2, e3, Pn, xlB, xhB, 0u, unused_rider, [](uint32_t, uint32_t) {}) & header_ok(h);
+      // the look-ahead bound when the window at Pn was read (ring_keep may
+      // raise pn_limit afterwards; the window read earlier stays good only
+      // below the bound of its time)
+      uint32_t pn_read_limit = pn_limit;
       while (ok) {
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
-        const bool nxt = s + 1 < nsb_fast && Pn <= pn_limit;
         uint4 tt;
         uint32_t aprev;
         if constexpr (TWO) {
@@ -1739,30 +1807,64 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           tt = make_uint4(t2.x, t2.y, 0u, 0u);
           aprev = list[2 * lane - 2];
         }
-        uint32_t xhB;
-        const uint32_t xlB = seg_bits(Pn, xhB);
         const uint32_t hB = __builtin_amdgcn_readfirstlane(xlB);
         RPP_TSTAMP(1);
         RPP_STAT(0, 1);
-        const uint32_t fsB = fs_of(hB);
-        lookups(xlB, fsB, e0, e1, e2, e3);
         uint32_t d1A, sumA, incA;
-        deltas(tt, aprev, fs, d1A, sumA);
-        RPP_TSTAMP(2);
-        uint32_t PnB;
-        ok = parse(Pn, xlB, xhB, fsB, e0, e1, e2, e3, PnB, sumA, incA,
-                   [&](uint32_t inc) { store(d1A, inc, s); }) &&
-             header_ok(hB) && nxt;
-        ++s;
-        P = Pn;
-        if (!ok) {
-          // (with ok, nxt held: P <= pn_limit < lim)
+        // Does the loop go on to the sub-block at Pn?  Tested before its
+        // parse, as scalar branches (the parse then only tells whether it
+        // ends in its window); if not, sub-block s's values are finished
+        // with a prefix scan of their own and the loop is left.
+#if RPP_EARLY_EXIT
+        if (s + 1 >= nsb_fast || Pn > pn_read_limit || !header_ok(hB)) {
+          deltas(tt, aprev, fs, d1A, sumA);
+          const uint32_t inc = wave_incl_sum(sumA);
+          store(d1A, inc, readlane(inc, kWave - 1), s);
+          ++s;
+          P = Pn;
           if (P > lim) status = RPP_TRUNCATED_INPUT;
           break;
         }
+#else
+        const uint32_t nxt = (uint32_t)(s + 1 < nsb_fast) & (uint32_t)(Pn <= pn_read_limit) & header_ok(hB);
+#endif
+        pn_read_limit = pn_limit;
+        const uint32_t fsB = fs_of(hB);
+        lookups(xlB, fsB, e0, e1, e2, e3);
+        deltas(tt, aprev, fs, d1A, sumA);
+#ifdef RPP_PAD_SALU  // (diagnostic builds: N extra independent scalar adds per sub-block)
+        {
+          uint32_t pad = s;
+          asm volatile(".rept " RPP_PAD_SALU "\n\ts_add_u32 %0, %0, 1\n\t.endr" : "+s"(pad)::"scc");
+        }
+#endif
+#ifdef RPP_PAD_VALU  // (diagnostic builds: N extra independent v_perm per sub-block)
+        {
+          uint32_t pad = lane;
+          asm volatile(".rept " RPP_PAD_VALU "\n\tv_perm_b32 %0, %0, %0, %0\n\t.endr" : "+v"(pad));
+        }
+#endif
+        RPP_TSTAMP(2);
+        uint32_t PnB, xlC, xhC;
+        ok = parse(Pn, xlB, xhB, fsB, e0, e1, e2, e3, PnB, xlC, xhC, sumA, incA,
+                   [&](uint32_t inc, uint32_t inc_last) { store(d1A, inc, inc_last, s); });
+        ++s;
+        P = Pn;
+#if RPP_EARLY_EXIT
+        if (!ok) break;  // (the sub-block at P does not end in its window: P <= pn_limit < lim)
+#else
+        if (!(ok & nxt)) {
+          if (P > lim) status = RPP_TRUNCATED_INPUT;
+          break;
+        }
+#endif
         Pn = PnB;
         fs = fsB;
-        if ((Pn >> 5) >= trig_w) {
+        xlB = xlC;
+        xhB = xhC;
+        if (Pn >= trig_bits) {
+          vm_after += (s - s_keep) * kStoresPerSub;  // (the stores since the last keep)
+          s_keep = s;
           ring_keep(Pn);
           ring_bounds();
         }
@@ -2905,7 +3007,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
                 : "scc");
             return r;
           };
-          auto header_ok = [](uint32_t h) { return (h & 15u) - (LO + 1) <= HI - LO; };
+          auto header_ok = [](uint32_t h) { return (uint32_t)((h & 15u) - (LO + 1) <= HI - LO); };
           // end (next header) of the sub-block at bit q, if it lies in the window
           auto parse = [&](uint32_t q, uint32_t fs, uint4 e0, uint4 e1, uint4 e2, uint4 e3, uint32_t& Pe) -> bool {
             const uint32_t k = fs + 1;

@@ -385,8 +385,14 @@ int bench(int argc, char** argv) {
           auto e = ricepp_amd::create_encoder<uint16_t>(c);
           auto d = ricepp_amd::create_decoder<uint16_t>(c);
           for (size_t b = t; b < blocks; b += T) {
-            if (encode) enc[b] = e->encode(std::span<uint8_t>{encbuf[b]}, in[b]);
-            else d->decode(out[b], enc[b]);
+            try {
+              if (encode) enc[b] = e->encode(std::span<uint8_t>{encbuf[b]}, in[b]);
+              else d->decode(out[b], enc[b]);
+            } catch (std::exception const& x) {
+              std::fprintf(stderr, "facade bench: %s of block %zu (%zu encoded bytes): %s\n",
+                           encode ? "encode" : "decode", b, enc[b].size(), x.what());
+              std::exit(3);
+            }
           }
         });
       }

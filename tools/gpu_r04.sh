@@ -22,7 +22,7 @@ run() {  # name seconds cmd...
 }
 for step in "$@"; do
   case $step in
-    isa) run isa 120 ./tools/isa_rate ;;
+    isa) run isa 60 ./tools/isa_rate ;;
     occ) run occ 240 python tools/occupancy_sweep.py ;;
     bench)
       run bench_short 240 python bench.py --no-cpu --steps 20 --warmup 5

@@ -33,6 +33,7 @@
 #define BODY_ADDSCAN "s_nop 1\n v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n s_nop 1\n v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n s_nop 1\n v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n s_nop 1\n v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
 #define BODY_SALU "s_add_u32 %8, %8, 1\n s_add_u32 %9, %9, 1\n s_add_u32 %10, %10, 1\n s_add_u32 %11, %11, 1\n s_add_u32 %8, %8, 1\n s_add_u32 %9, %9, 1\n s_add_u32 %10, %10, 1\n s_add_u32 %11, %11, 1\n"
 #define BODY_MIX "v_add_u32 %0, %0, %12\n s_add_u32 %8, %8, 1\n v_add_u32 %1, %1, %12\n s_add_u32 %9, %9, 1\n v_add_u32 %2, %2, %12\n s_add_u32 %10, %10, 1\n v_add_u32 %3, %3, %12\n s_add_u32 %11, %11, 1\n"
+#define BODY_SMUL "s_mul_i32 %8, %8, %9\n s_mul_i32 %10, %10, %11\n s_mul_i32 %9, %9, %8\n s_mul_i32 %11, %11, %10\n s_mul_i32 %8, %8, %9\n s_mul_i32 %10, %10, %11\n s_mul_i32 %9, %9, %8\n s_mul_i32 %11, %11, %10\n"
 #define BODY_READLANE "v_readlane_b32 %8, %0, 5\n v_readlane_b32 %9, %1, 6\n v_readlane_b32 %10, %2, 7\n v_readlane_b32 %11, %3, 9\n v_readlane_b32 %8, %4, 5\n v_readlane_b32 %9, %5, 6\n v_readlane_b32 %10, %6, 7\n v_readlane_b32 %11, %7, 9\n"
 
 #define KERN(NAME, BODY)                                                                                    \
@@ -47,7 +48,8 @@
       asm volatile(BODY BODY BODY BODY                                                                      \
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), \
                      "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3)                                                 \
-                   : "v"(k), "v"(sel));                                 \
+                   : "v"(k), "v"(sel)                                                                        \
+                   : "scc", "vcc");                                 \
     }                                                                                                       \
     asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");                              \
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ s0 ^ s1 ^ s2 ^ s3;     \
@@ -75,6 +77,7 @@ KERN(k_addscan, BODY_ADDSCAN)
 KERN(k_salu, BODY_SALU)
 KERN(k_mix, BODY_MIX)
 KERN(k_readlane, BODY_READLANE)
+KERN(k_smul, BODY_SMUL)
 
 // LDS: 16-byte table lookups, random (table of 256 entries) vs conflict-free
 template <int MODE>
@@ -107,6 +110,7 @@ typedef void (*kfn)(uint32_t*, unsigned long long*, uint32_t);
 
 static void run(const char* name, kfn f, int per_wave_instrs) {
   printf("%-12s", name);
+  fflush(stdout);
   for (int wps : {1, 2, 4, 8}) {
     const int nb = 256 * wps;  // 4 waves per workgroup -> one per SIMD
     uint32_t* out;
@@ -123,7 +127,7 @@ static void run(const char* name, kfn f, int per_wave_instrs) {
     for (int i = 0; i < nb * 4; ++i) avg += (double)h[i];
     avg /= nb * 4;
     const double per = avg / ((double)per_wave_instrs * ITERS);
-    printf("  w%d: %6.2f/wave %6.2f/SIMD", wps, per, per / wps);
+    printf("  w%d: %6.2f/wave %6.2f/SIMD %5.2f/CU", wps, per, per / wps, per / wps / 4);
     hipFree(out);
     hipFree(cyc);
     free(h);
@@ -132,6 +136,7 @@ static void run(const char* name, kfn f, int per_wave_instrs) {
 }
 
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);
   printf("cycles per instruction (s_memtime ticks), 1/2/4/8 waves per SIMD\n");
   run("v_add", k_vadd, 32);
   run("v_perm", k_perm, 32);
@@ -154,6 +159,7 @@ int main() {
   run("s_add", k_salu, 32);
   run("vadd+sadd", k_mix, 32);
   run("readlane", k_readlane, 32);
+  run("s_mul", k_smul, 32);
   run("lds_rand", k_lds<0>, 8);
   run("lds_16copy", k_lds<1>, 8);
   run("lds_lane", k_lds<2>, 8);

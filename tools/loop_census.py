@@ -55,6 +55,8 @@ def classify(ins: str) -> str:
         return "valu_perm"
     if op.startswith(("v_readlane", "v_readfirstlane", "v_writelane")):
         return "valu_lane"
+    if op.startswith("v_") and (op.endswith("_e32") or op.endswith("_sdwa")):
+        return "valu_vop2"
     if op.startswith("v_"):
         return "valu"
     return "other"
@@ -62,9 +64,8 @@ def classify(ins: str) -> str:
 
 for hi, name in headers:
     # the loop: from the header to the last branch back to it
-    back = max((j for j in range(hi, len(body)) if re.search(rf"\b{re.escape(name)}\b", body[j]) and
-                body[j].strip().startswith("s_cbranch") or (body[j].strip().startswith("s_branch") and name in body[j])),
-               default=None)
+    back = max((j for j in range(hi, len(body)) if re.search(rf"{re.escape(name)}(?!\d)", body[j]) and
+                body[j].strip().startswith(("s_cbranch", "s_branch"))), default=None)
     if back is None:
         continue
     seg = body[hi:back + 1]
@@ -82,3 +83,22 @@ for hi, name in headers:
         c[classify(t)] += 1
     nops = sum(int(m.group(1)) + 1 for l in seg for m in [re.match(r"\s*s_nop (\d+)", l)] if m)
     print(f"{name}: {len(seg)} lines; " + ", ".join(f"{k} {v}" for k, v in sorted(c.items())) + f"; nop wait states {nops}")
+    # the hot path: the header block up to its first conditional branch, then
+    # the fall-through blocks until the first branch back to the header or a
+    # block that only the rare paths reach (heuristic: stop at the 3rd branch)
+    h = Counter()
+    nb = 0
+    for l in seg:
+        t = l.strip()
+        if not t or t.startswith((";", ".", "//")) or t.endswith(":"):
+            continue
+        h[classify(t)] += 1
+        if t.startswith("s_cbranch") or t.startswith("s_branch"):
+            nb += 1
+            if nb >= 3:
+                break
+    # SIMD cycles at 4 waves per SIMD, from tools/isa_rate (profiles/r04_isa_rate.txt):
+    # VOP2 1.57, other VALU (VOP3, DPP, v_perm, lane reads) 2.66, SALU 2.57
+    cyc = 1.57 * h["valu_vop2"] + 2.66 * (h["valu"] + h["valu_dpp"] + h["valu_perm"] + h["valu_lane"]) + 2.57 * h["salu"]
+    print("   hot path (to the 3rd branch): " + ", ".join(f"{k} {v}" for k, v in sorted(h.items())) +
+          f"; total {sum(h.values())}; est. SIMD cycles {cyc:.0f}")
