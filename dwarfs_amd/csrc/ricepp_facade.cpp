@@ -27,6 +27,7 @@
 #include <string>
 #include <thread>
 #include <tuple>
+#include <vector>
 
 namespace ricepp_amd {
 
@@ -99,15 +100,17 @@ class device_guard {
 };
 
 // A private stream plus device and pinned host buffers, bound to one device.
-// Device buffers come from the stream-ordered allocator (hipMallocAsync /
-// hipFreeAsync on the context's stream), so growing one never synchronises the
-// device.  Pinned buffers are mapped into the device's address space (the
+// Device buffers come from hipMalloc and grow geometrically while the context
+// is idle (not from the stream-ordered allocator: with hipMallocAsync /
+// hipFreeAsync, on the default pool or a pool per context, buffers of
+// concurrent streams were overwritten -- tools/h2d_stress.hip reproduces it
+// outside the library, 4 threads x 128 MiB; hipMalloc passes).  Pinned buffers are mapped into the device's address space (the
 // encoder packs its output straight into them) and grow geometrically; a
 // context going back to the pool drops pinned buffers above kPinnedKeep and
 // device buffers above kDeviceKeep, so a burst of huge batches does not keep
 // GiBs of host memory pinned or of device memory reserved.
 constexpr size_t kPinnedKeep = size_t{320} << 20;  // (a batch of 8 x 16 MiB blocks: 128 + 64 MiB)
-constexpr size_t kDeviceKeep = size_t{256} << 20;
+constexpr size_t kDeviceKeep = size_t{1} << 30;  // (hipFree synchronises: trims stay rare)
 
 class device_ctx {
  public:
@@ -168,7 +171,7 @@ class device_ctx {
     for (auto* q : {&dbuf_, &wbuf_}) {
       size_t& cap = q == &dbuf_ ? dcap_ : wcap_;
       if (cap > kDeviceKeep) {
-        (void)hipFreeAsync(*q, stream_);
+        (void)hipFree(*q);
         *q = nullptr;
         cap = 0;
       }
@@ -180,11 +183,11 @@ class device_ctx {
     if (bytes <= cap && p) return p;
     size_t n = cap ? cap : size_t{1} << 20;
     while (n < bytes) n *= 2;
-    if (p) (void)hipFreeAsync(p, stream_);  // (stream-ordered: after the work that used it)
+    if (p) (void)hipFree(p);  // (the context is idle: its last batch has completed)
     p = nullptr;
     cap = 0;
     void* q = nullptr;
-    hip_check(hipMallocAsync(&q, n, stream_), "hipMallocAsync");
+    hip_check(hipMalloc(&q, n), "hipMalloc");
     p = static_cast<uint8_t*>(q);
     cap = n;
     return p;
@@ -344,7 +347,10 @@ constexpr size_t kBatchOut = size_t{16} << 20;
 constexpr size_t kLargeJoin = 8;
 // encode batches whose worst-case output exceeds this go out by a DMA copy of
 // the slots instead of being packed into mapped host memory by a kernel
-constexpr size_t kPackMax = ~size_t{0};  // (no-pack path under investigation: kept off)
+#ifndef RPP_FACADE_PACK_MAX
+#define RPP_FACADE_PACK_MAX (~size_t{0})  // (no-pack path under investigation: kept off)
+#endif
+constexpr size_t kPackMax = RPP_FACADE_PACK_MAX;
 // batches of one queue on the device at once (set_facade_pipeline_depth
 // changes it for benchmarks)
 std::atomic<int> g_max_active{2};
@@ -581,10 +587,32 @@ class batch_queue {
   // are copied in rather than read over PCIe by the encode kernel: reading
   // them in place measured 1.6x slower for 1 MiB blocks and no faster for
   // 64 KiB ones, profiles/r03_facade_bench.jsonl.)
+  // RICEPP_AMD_DEBUG_FACADE: 1 prints failed blocks, 2 also checks each
+  // request's staged input against its source at launch and at completion,
+  // 3 also reads the device copy of the inputs back after the launch
+  static int debug_level() {
+    static const int v = [] {
+      const char* e = std::getenv("RICEPP_AMD_DEBUG_FACADE");
+      return e ? std::max(1, std::atoi(e)) : 0;
+    }();
+    return v;
+  }
+  void check_staged(batch& b, const char* when) {
+    for (size_t i = 0; i < b.reqs.size(); ++i) {
+      request* q = b.reqs[i];
+      if (q->in_bytes && std::memcmp(q->pin_in, q->in, q->in_bytes) != 0) {
+        size_t k = 0;
+        while (q->pin_in[k] == q->in[k]) ++k;
+        std::fprintf(stderr, "ricepp_amd facade: %s: batch %p req %zu/%zu staged input differs at byte %zu of %zu\n",
+                     when, (void*)&b, i, b.reqs.size(), k, q->in_bytes);
+      }
+    }
+  }
   void launch_encode(batch& b) {
     device_ctx& ctx = *b.ctx;
     const size_t nb = b.reqs.size();
     const size_t in_total = b.in_fill, out_total = b.out_fill;
+    if (debug_level() >= 2) check_staged(b, "encode launch");
     const size_t arr = (6 * nb + 1) * 8 + align16(nb * 4);
     auto* h64 = reinterpret_cast<uint64_t*>(b.pin_in + in_total);
     for (size_t i = 0; i < nb; ++i) {
@@ -607,6 +635,16 @@ class batch_queue {
                                  dslots, d64 + 2 * nb, d64 + 3 * nb, dst, b.total_samples, b.max_samples, ws, ws_bytes,
                                  s);
     if (st != RPP_OK) throw_status(st);
+    if (debug_level() >= 3) {
+      std::vector<uint8_t> back(in_total);
+      hip_check(hipMemcpyAsync(back.data(), d, in_total, hipMemcpyDeviceToHost, s), "debug D2H");
+      ctx.sync();
+      for (size_t i = 0; i < nb; ++i) {
+        request* q = b.reqs[i];
+        if (q->in_bytes && std::memcmp(back.data() + q->in_off, q->in, q->in_bytes) != 0)
+          std::fprintf(stderr, "ricepp_amd facade: device copy of req %zu/%zu differs\n", i, nb);
+      }
+    }
     b.packed = out_total <= kPackMax;
     if (b.packed) {
       st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
@@ -625,6 +663,7 @@ class batch_queue {
   }
   void results_encode(batch& b) {
     const size_t nb = b.reqs.size();
+    if (debug_level() >= 2) check_staged(b, "encode done");
     auto const* r64 = reinterpret_cast<uint64_t const*>(b.pin_out + b.out_fill);  // out_bytes | dst_off | total
     auto const* hst = reinterpret_cast<int32_t const*>(b.pin_out + b.out_fill + (3 * nb + 1) * 8);
     for (size_t i = 0; i < nb; ++i) {
@@ -633,7 +672,7 @@ class batch_queue {
       q->result_bytes = hst[i] == RPP_OK ? r64[i] : 0;
       q->pin_out = b.pin_out + (b.packed ? r64[nb + i] : q->out_off);
       if (q->status == RPP_OK && q->result_bytes > q->out_cap) q->status = RPP_OUTPUT_TOO_SMALL;
-      if (q->status != RPP_OK && std::getenv("RICEPP_AMD_DEBUG_FACADE"))
+      if (q->status != RPP_OK && debug_level())
         std::fprintf(stderr, "ricepp_amd facade: encode batch nb=%zu total=%llu max=%llu in_fill=%zu out_fill=%zu "
                      "packed=%d: block %zu n=%llu in_off=%zu out_off=%zu status=%d\n", nb,
                      (unsigned long long)b.total_samples, (unsigned long long)b.max_samples, b.in_fill, b.out_fill,

@@ -22,6 +22,11 @@ namespace rpp_internal {
 // (rerun passes, then one serial pass): the result is the serial parse's,
 // whatever the guesses were.
 // ---------------------------------------------------------------------------
+// Streams the segmented decode (and the four-streams-per-wave kernel) take:
+// their unit and sub-block position lists are 32-bit bit positions.  Longer
+// streams (up to RPP_MAX_STREAM_SAMPLES) are decoded one wave each by the
+// fused kernel, which rebases its positions as it goes.
+constexpr uint64_t kSegMaxSamples = UINT64_C(1) << 27;
 constexpr uint32_t kSegOvr = 16;             // headers recorded past a unit's region
 constexpr uint32_t kSegNone = 0xFFFFFFFFu;   // no position
 constexpr uint32_t kSpecSteps = 12;          // sub-blocks a candidate first header must chain through

@@ -610,6 +610,15 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
   const uint32_t nchunks = (N + chunk_len - 1) / chunk_len;
   const uint32_t segc = p.seg_chunks;
   const bool multi = split && nchunks > segc;
+  // one wave for a whole stream keeps 32-bit bit positions: longer streams
+  // must be split (rpp_encode_batch_ws)
+  if (!multi && n64 >= rpp_internal::kSegMaxSamples) {
+    if (lane == 0 && seg == 0) {
+      p.status[b] = RPP_INVALID_ARGUMENT;
+      p.out_bytes[b] = 0;
+    }
+    return;
+  }
   // this unit's chunks [c_lo, c_hi)
   const uint32_t c_lo = multi ? seg * segc : 0u;
   const uint32_t c_hi = multi ? min(nchunks, c_lo + segc) : nchunks;
@@ -776,15 +785,17 @@ __global__ __launch_bounds__(256) void rpp_enc_concat_kernel(EncParams p, const 
   const uint32_t first = (uint32_t)p.seg_base[b], nseg = (uint32_t)(p.seg_base[b + 1] - first);
   const uint32_t k = u - first;
   if (nseg < 2 || k == 0) return;
+  // (bit offsets in the stream are 64-bit: streams go up to 2^30 samples;
+  // word indices fit 32 bits)
   const uint64_t base = seg_off[first];
-  const uint32_t o_k = (uint32_t)(seg_off[u] - base);
+  const uint64_t o_k = seg_off[u] - base;
   const uint32_t L_k = (uint32_t)p.seg_bits[u];
-  const uint32_t total_bits = (uint32_t)(seg_off[first + nseg - 1] - base) + (uint32_t)p.seg_bits[first + nseg - 1];
-  const uint32_t total_bytes = (total_bits + 7) >> 3;
+  const uint64_t total_bits = (seg_off[first + nseg - 1] - base) + p.seg_bits[first + nseg - 1];
+  const uint64_t total_bytes = (total_bits + 7) >> 3;
   const bool last = k + 1 == nseg;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(p.scratch + (size_t)(u - b - 1) * p.slot_bytes);
   const uint32_t* nxt = last ? nullptr : reinterpret_cast<const uint32_t*>(p.scratch + (size_t)(u - b) * p.slot_bytes);
-  const uint32_t o_n = o_k + L_k;  // next segment's offset
+  const uint64_t o_n = o_k + L_k;  // next segment's offset
   uint8_t* out8 = p.out + p.out_off[b];
   uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
   // bits [x, x + 32) of this segment (zero past its end)
@@ -799,29 +810,29 @@ __global__ __launch_bounds__(256) void rpp_enc_concat_kernel(EncParams p, const 
     return v;
   };
   auto put = [&](uint32_t w, uint32_t v) {
-    if (4 * w + 4 <= total_bytes) {
+    if (4ull * w + 4 <= total_bytes) {
       out32[w] = v;
     } else {
-      for (uint32_t c = 0; 4 * w + c < total_bytes; ++c) out8[4 * w + c] = (uint8_t)(v >> (8 * c));
+      for (uint32_t c = 0; 4ull * w + c < total_bytes; ++c) out8[4ull * w + c] = (uint8_t)(v >> (8 * c));
     }
   };
   // words whose first bit lies in this segment
-  const uint32_t w_begin = (o_k + 31) >> 5, w_end = (o_n + 31) >> 5;
+  const uint32_t w_begin = (uint32_t)((o_k + 31) >> 5), w_end = (uint32_t)((o_n + 31) >> 5);
   for (uint32_t w = w_begin + threadIdx.x; w < w_end; w += blockDim.x) {
-    uint32_t v = seg_bits32(32 * w - o_k);
-    if (!last && 32 * w + 32 > o_n) v |= nxt[0] << (o_n - 32 * w);  // (the next segment is >= 1024 bits)
+    uint32_t v = seg_bits32((uint32_t)(32ull * w - o_k));
+    if (!last && 32ull * w + 32 > o_n) v |= nxt[0] << (uint32_t)(o_n - 32ull * w);  // (the next segment is >= 1024 bits)
     put(w, v);
   }
   // the word holding o_1: segment 0's bits below it, segment 1's above
   if (k == 1 && (o_k & 31u) && threadIdx.x == 0) {
-    const uint32_t w = o_k >> 5, sh = o_k & 31u;
-    const uint32_t have = 4 * w < total_bytes ? min(4u, total_bytes - 4 * w) : 0u;
+    const uint32_t w = (uint32_t)(o_k >> 5), sh = (uint32_t)(o_k & 31u);
+    const uint32_t have = 4ull * w < total_bytes ? (uint32_t)min((uint64_t)4, total_bytes - 4ull * w) : 0u;
     uint32_t old = 0;
     for (uint32_t c = 0; c < 4; ++c)
       if (8 * c < sh) old |= (uint32_t)out8[4 * w + c] << (8 * c);
     old &= (1u << sh) - 1u;
     uint32_t v = old | (src[0] << sh);
-    if (nseg == 2 && o_n < 32 * w + 32 && L_k < 32 - sh) v &= (1u << (sh + L_k)) - 1u;
+    if (nseg == 2 && o_n < 32ull * w + 32 && L_k < 32 - sh) v &= (1u << (sh + L_k)) - 1u;
     for (uint32_t c = 0; c < have; ++c) out8[4 * w + c] = (uint8_t)(v >> (8 * c));
   }
   if (last && threadIdx.x == 0) {
@@ -1141,7 +1152,7 @@ constexpr int kParsePrio = 1;
 #define RPP_END_LIST 1  // the fast loop's sub-block end read back from the list (0: picked by readlane)
 #endif
 #ifndef RPP_EARLY_EXIT
-#define RPP_EARLY_EXIT 1  // the fast loop's continue tests as scalar branches before the parse (0: after it)
+#define RPP_EARLY_EXIT 0  // 1: the fast loop's continue tests as scalar branches before the parse (+5% time, r04 A/B)
 #endif
 #ifndef RPP_RING_VALU
 #define RPP_RING_VALU 1  // window word addresses from q + 24 lane in vector code (0: scalar split of q)
@@ -1380,29 +1391,37 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
 #endif
 
   // ---- per-stream setup (wave-uniform) ----
+  // Bit positions are 32-bit and relative to `in`, which starts at the
+  // 4-aligned word holding the stream's first byte; a stream longer than
+  // 2^30 bits (blocks of more than ~2^26 samples: mkdwarfs -S 28..30) is
+  // rebased as the parse goes (rebase() below), so any stream the C ABI
+  // accepts decodes here.
   int32_t status = RPP_OK;
   uint32_t N = 0, nbytes = 0, mis = 0;
+  uint64_t nb_all = 0, lim_all = 0;  // the stream's bytes (+ mis) and readable bits from the original base
   const uint8_t* in = p.in;
   uint16_t* out = p.out;
   {
     const uint64_t n64 = p.n_samples[b];
     const uint64_t ioff = p.in_off[b];
     const uint64_t nb64 = p.in_bytes[b];
-    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
+    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 32) - 8) {
       status = RPP_INVALID_ARGUMENT;
     } else {
-      // bit positions from the 4-aligned word holding the first byte
       mis = (uint32_t)(ioff & 3u);
       N = (uint32_t)n64;
-      nbytes = (uint32_t)nb64 + mis;
+      nb_all = nb64 + mis;
+      // last readable bit + 1: the reader pulls whole 8-byte packets of the
+      // stream (bitstream_reader.h:149-183), so it only throws past this point.
+      lim_all = 8u * mis + 64u * ((nb64 + 7u) >> 3);
       in = p.in + (ioff - mis);
       out = p.out + p.out_off[b];
     }
   }
   const bool aligned16 = ((uintptr_t)in & 15u) == 0;
-  // last readable bit + 1: the reader pulls whole 8-byte packets of the
-  // stream (bitstream_reader.h:149-183), so it only throws past this point.
-  const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
+  nbytes = (uint32_t)nb_all;
+  uint32_t lim = (uint32_t)min(lim_all, (uint64_t)0xFFFFFFFFu);
+  uint64_t base_w = 0;  // words `in` has moved by
   const uint32_t chunk_len = CS * bs;
   const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
 
@@ -1476,6 +1495,20 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   // codec.h:69-74,81-86: the 16-bit initial value of each component
   uint32_t last0 = 0, last1 = 0;
   uint32_t P = 8 * mis + 16 * CS;
+  // moves `in` forward by a multiple of the ring's size below P (ring slots
+  // and the pending chunk keep their places), once P passes 2^30; between
+  // two rebases the parse advances less than 2^31 bits (the fast loop stops
+  // at 2^31, see ring_bounds), so positions never wrap
+  auto rebase = [&]() {
+    if (P < (1u << 30)) return;
+    const uint32_t sh = ((P >> 5) - kRingWords) & ~(kRingWords - 1u);
+    in += 4ull * sh;
+    base_w += sh;
+    P -= 32u * sh;
+    fill_w -= sh;
+    nbytes = (uint32_t)(nb_all - 4ull * base_w);
+    lim = (uint32_t)min(lim_all - 32ull * base_w, (uint64_t)0xFFFFFFFFu);
+  };
   if (status == RPP_OK) {
     if (P > lim) status = RPP_TRUNCATED_INPUT;
     last0 = __builtin_amdgcn_readfirstlane(peek32(8 * mis) & 0xFFFFu);
@@ -1514,6 +1547,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
   ScanRegs sreg;
 
   for (uint32_t s = 0; s < nsb && status == RPP_OK; ++s) {
+    rebase();
     // ---- fast loop (the common case): Rice sub-blocks of 128 codes with fs
     //      5..7 that lie in one window, ring resident.  Straight-line code: at
     //      most 4 terminators per 24-bit segment (codes are >= 6 bits), every
@@ -1770,7 +1804,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // scalar tests)
       uint32_t pn_limit, trig_bits;
       auto ring_bounds = [&]() {
-        pn_limit = __builtin_amdgcn_readfirstlane(min(lim - 4u, 32u * (fill_w - kAhead) + 31u));
+        pn_limit = __builtin_amdgcn_readfirstlane(min(min(lim - 4u, 32u * (fill_w - kAhead) + 31u), 1u << 31));
         trig_bits =
             __builtin_amdgcn_readfirstlane(32u * (pend ? fill_w - (kAhead + 127u) : (fill_w > 766u ? fill_w - 766u : 0u)));
       };
@@ -1874,6 +1908,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
     // dispatch on the sub-block's fs class; a loop that stops at a
     // sub-block of the other class hands over to the other loop directly
     while (s < nsb_fast && status == RPP_OK && fill_w >= (P >> 5) + kAhead && P + 4 <= lim) {
+      rebase();
       const uint32_t* w = ring + ((P >> 5) & kRingMask);
       const uint32_t h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(w[1], w[0], P & 31u)) & 15u;
       const uint32_t s0 = s;
@@ -2160,8 +2195,8 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
   uint16_t* out = p.out;
   if (active) {
     const uint64_t n64 = p.n_samples[b], ioff = p.in_off[b], nb64 = p.in_bytes[b];
-    if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
-      active = false;  // (the fused kernel reports it)
+    if (n64 % CS != 0 || n64 >= rpp_internal::kSegMaxSamples || nb64 >= (UINT64_C(1) << 29)) {
+      active = false;  // (the fused kernel decodes or reports it)
     } else {
       mis = (uint32_t)(ioff & 3u);
       N = (uint32_t)n64;
@@ -2749,7 +2784,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       const uint64_t n64 = p.n_samples[b];
       const uint64_t ioff = p.in_off[b];
       const uint64_t nb64 = p.in_bytes[b];
-      if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) {
+      if (n64 % CS != 0 || n64 >= rpp_internal::kSegMaxSamples || nb64 >= (UINT64_C(1) << 29)) {
         status = RPP_INVALID_ARGUMENT;
       } else {
         N = (uint32_t)n64;
@@ -3299,7 +3334,7 @@ __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(Parse
   const uint32_t ju = u - u0;
   if (nunits <= 1 || ju == 0) return;
   const uint64_t n64 = p.n_samples[b], ioff = p.in_off[b], nb64 = p.in_bytes[b];
-  if (n64 % CS != 0 || n64 >= RPP_MAX_STREAM_SAMPLES || nb64 >= (UINT64_C(1) << 29)) return;
+  if (n64 % CS != 0 || n64 >= rpp_internal::kSegMaxSamples || nb64 >= (UINT64_C(1) << 29)) return;
   {
     copy_tables(dsm);
   }

@@ -77,8 +77,12 @@ typedef struct rpp_config {
   uint32_t unused_lsb_count;       /* 0..15 */
 } rpp_config;
 
-/* Largest single stream the kernels accept (bit positions are 32-bit). */
-#define RPP_MAX_STREAM_SAMPLES (UINT64_C(1) << 27)
+/* Streams hold fewer samples than this: mkdwarfs blocks go up to 2^30 bytes
+ * (-S 30, tools/src/mkdwarfs_main.cpp:135), i.e. 2^29 samples.  Streams of
+ * 2^27 samples and more are encoded in segments by rpp_encode_batch_ws (the
+ * workspace-free rpp_encode_batch, one wave per stream, takes fewer) and
+ * decoded one wave each (not segmented). */
+#define RPP_MAX_STREAM_SAMPLES (UINT64_C(1) << 30)
 
 /* ABI version, bumped on any signature change. */
 uint32_t rpp_abi_version(void);

@@ -339,6 +339,31 @@ int main(int argc, char** argv) {
                 (unsigned long long)(after.decode_launches - before.decode_launches),
                 (unsigned long long)after.contexts_created);
   }
+  // long blocks from many threads: 16 threads x 3 blocks of 8 MiB, joined into
+  // multi-block segmented launches with two batches in flight on separate
+  // contexts (the case whose device buffers a stream-ordered allocator mixed
+  // up); every stream against the oracle, every decode against its input
+  {
+    auto c = cfg(128, 1, true, 0);
+    std::vector<int> bad(16, 0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < 16; ++t) {
+      pool.emplace_back([&, t] {
+        auto enc = ricepp_amd::create_encoder<uint16_t>(c);
+        auto dec = ricepp_amd::create_decoder<uint16_t>(c);
+        for (int i = 0; i < 3; ++i) {
+          auto x = make_data(size_t{4} << 20, 0, true, 50, 7000 + 10 * t + i);
+          auto bytes = enc->encode(x);
+          if (bytes != oracle_encode(c, x)) ++bad[t];
+          std::vector<uint16_t> y(x.size());
+          dec->decode(y, bytes);
+          if (y != x) ++bad[t];
+        }
+      });
+    }
+    for (auto& th : pool) th.join();
+    for (int t = 0; t < 16; ++t) CHECK(bad[t] == 0);
+  }
   std::printf("facade_test: %s (%d failures)\n", failures ? "FAILED" : "OK", failures);
   return failures ? 1 : 0;
 }
@@ -407,7 +432,27 @@ int bench(int argc, char** argv) {
     double td = run(false);
     auto s2 = ricepp_amd::get_facade_stats();
     bool ok = true;
-    for (size_t b = 0; b < blocks; ++b) ok = ok && out[b] == in[b];
+    int reported = 0;
+    for (size_t b = 0; b < blocks; ++b) {
+      if (out[b] == in[b]) continue;
+      ok = false;
+      if (reported++ >= 8) continue;
+      // which side is wrong: the stream against the oracle's, the samples
+      // against the input (and against the other blocks' inputs)
+      auto want = oracle_encode(c, in[b]);
+      std::vector<uint8_t> got(enc[b].begin(), enc[b].end());
+      size_t ed = 0;
+      while (ed < std::min(got.size(), want.size()) && got[ed] == want[ed]) ++ed;
+      size_t sd = 0;
+      while (sd < n && out[b][sd] == in[b][sd]) ++sd;
+      long other = -1;
+      for (size_t o = 0; o < blocks && other < 0; ++o)
+        if (o != b && out[b] == in[o]) other = (long)o;
+      std::fprintf(stderr,
+                   "facade bench: block %zu mismatch: stream %zu B (oracle %zu B, first diff %zu); first sample diff "
+                   "%zu of %zu; equals input of block %ld\n",
+                   b, got.size(), want.size(), ed, sd, n, other);
+    }
     double gib = double(blocks) * n * 2 / double(1ull << 30);
     const double ne = double(s1.encode_launches - s0.encode_launches), nd = double(s2.decode_launches - s1.decode_launches);
     std::printf("{\"facade_bench\": true, \"threads\": %d, \"depth\": %d, \"blocks\": %zu, \"block_bytes\": %zu, "

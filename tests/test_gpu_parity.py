@@ -546,6 +546,21 @@ def test_segmented_decode_of_a_64mib_stream():
     assert codec.segmented_decode_stats(reset=True)["met"] > 0
 
 
+@pytest.mark.parametrize("cs", [1, 2])
+def test_stream_longer_than_2_27_samples(cs):
+    """One stream of 2**27 + 5 samples (cs 1; 2**27 + 6 for cs 2) with short blocks beside it: past the
+    segmented encode's and decode's 2**27-sample unit range and, with the generator's ~14 bits per sample, past
+    2**30 bits, where the fused decode rebases its bit positions. Encoded on the GPU byte for byte as the oracle
+    (ricepp/ricepp_cpu.cpp encode), decoded back to the input (the default mode and the fused kernel)."""
+    rng = np.random.default_rng(2727 + cs)
+    n = (1 << 27) + (5 if cs == 1 else 6)
+    big = datagen.benchmark_data(rng, n) if cs == 1 else datagen.poisson_data(rng, n, lam=3000.0)
+    blocks = [datagen.poisson_data(rng, 4096 * cs), big, datagen.poisson_data(rng, 777 * cs)]
+    cfg = codec.CodecConfig(128, cs, "big", 0)
+    run_batch(cfg, blocks)
+    run_batch(cfg, blocks[1:2], dec=FUSED)
+
+
 @pytest.mark.parametrize("bs", [17, 99, 200, 256, 512])
 @pytest.mark.parametrize("cs", [1, 2])
 def test_segmented_decode_other_block_sizes(bs, cs):
