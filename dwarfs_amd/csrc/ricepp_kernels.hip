@@ -1081,23 +1081,13 @@ __device__ __forceinline__ Map8 scan_step8(Map8 m) {
   return comp8(m, d);
 }
 
-// The same step in one instruction per dword: v_cndmask_b32 with the DPP
-// source as its false operand -- lanes in the constant lane mask (those
-// without a source: identity) take the identity map held in id (two VGPRs
-// loaded once), the rest the map from the left; out-of-range sources read 0
-// (bound_ctrl) and are always masked.  Saves the per-step identity moves a
-// DPP move into a fresh `old` needs.
 // One scan step as two DPP moves into persistent registers: lanes without a
 // source (row_shr: the first lanes of each row; row_bcast: the rows the row
 // mask leaves out; wave_shr: lane 0) are not written by a DPP move without
 // bound_ctrl, so they keep the identity map the register was initialised
 // with -- no mask, no vcc.  s_nop 1: a DPP read of a VGPR written by the
 // previous VALU instruction needs two wait states.
-#ifndef RPP_ASM_DPP
-#define RPP_ASM_DPP 1
-#endif
-#if RPP_ASM_DPP
-#define RPP_SCAN8_STEP(NAME, CTRL, RM, CT, RMI)                                                           \
+#define RPP_SCAN8_STEP(NAME, CTRL, RM)                                                           \
   __device__ __forceinline__ Map8 NAME(Map8 m, Map8& keep) {                                              \
     asm("s_nop 1\n\t"                                                                                    \
         "v_mov_b32_dpp %0, %2 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"                                \
@@ -1106,22 +1096,12 @@ __device__ __forceinline__ Map8 scan_step8(Map8 m) {
         : "v"(m.lo), "v"(m.hi));                                                                          \
     return comp8(m, keep);                                                                                \
   }
-#else
-// (the intrinsic form: `keep` is loop-carried, so the move writes the same
-// register, and the compiler schedules the moves and their wait states)
-#define RPP_SCAN8_STEP(NAME, CTRL, RM, CT, RMI)                                    \
-  __device__ __forceinline__ Map8 NAME(Map8 m, Map8& keep) {                      \
-    keep.lo = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.lo, (int)m.lo, CT, RMI, 0xF, false); \
-    keep.hi = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.hi, (int)m.hi, CT, RMI, 0xF, false); \
-    return comp8(m, keep);                                                        \
-  }
-#endif
-RPP_SCAN8_STEP(scan8_shr1, "row_shr:1", "0xf", kDppRowShr1, 0xF)
-RPP_SCAN8_STEP(scan8_shr2, "row_shr:2", "0xf", kDppRowShr2, 0xF)
-RPP_SCAN8_STEP(scan8_shr4, "row_shr:4", "0xf", kDppRowShr4, 0xF)
-RPP_SCAN8_STEP(scan8_shr8, "row_shr:8", "0xf", kDppRowShr8, 0xF)
-RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", "0xa", kDppRowBcast15, 0xA)
-RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc", kDppRowBcast31, 0xC)
+RPP_SCAN8_STEP(scan8_shr1, "row_shr:1", "0xf")
+RPP_SCAN8_STEP(scan8_shr2, "row_shr:2", "0xf")
+RPP_SCAN8_STEP(scan8_shr4, "row_shr:4", "0xf")
+RPP_SCAN8_STEP(scan8_shr8, "row_shr:8", "0xf")
+RPP_SCAN8_STEP(scan8_bc15, "row_bcast:15", "0xa")
+RPP_SCAN8_STEP(scan8_bc31, "row_bcast:31", "0xc")
 // the persistent destination registers of the six steps and of the final
 // shift, initialised to the identity map (opaque to the compiler)
 struct ScanRegs {
@@ -1151,14 +1131,8 @@ constexpr int kParsePrio = 1;
 #ifndef RPP_END_LIST
 #define RPP_END_LIST 1  // the fast loop's sub-block end read back from the list (0: picked by readlane)
 #endif
-#ifndef RPP_EARLY_EXIT
-#define RPP_EARLY_EXIT 0  // 1: the fast loop's continue tests as scalar branches before the parse (+5% time, r04 A/B)
-#endif
-#ifndef RPP_RING_VALU
-#define RPP_RING_VALU 1  // window word addresses from q + 24 lane in vector code (0: scalar split of q)
-#endif
-#ifndef RPP_SDWA
-#define RPP_SDWA 1  // table entry offsets by SDWA byte selects (0: bit-field extract + shift-add)
+#ifndef RPP_LIST32
+#define RPP_LIST32 1  // fast-loop list entries (a_i << fs) | rem_i in one dword (0: (a_i, rem_i) pairs)
 #endif
 
 // fs >= 8: states 0..13 (13 remainder bits still to skip at most).  A state
@@ -1184,16 +1158,11 @@ __device__ __forceinline__ uint32_t byte_term(uint32_t S, uint4 e) {
 #undef RPP_SCAN8_STEP
 // exclusive form: the map of lanes 0..l-1 (identity on lane 0)
 __device__ __forceinline__ Map8 shift8_wave(Map8 m, Map8& keep) {
-#if RPP_ASM_DPP
   asm("s_nop 1\n\t"
       "v_mov_b32_dpp %0, %2 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
       "v_mov_b32_dpp %1, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
       : "+v"(keep.lo), "+v"(keep.hi)
       : "v"(m.lo), "v"(m.hi));
-#else
-  keep.lo = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.lo, (int)m.lo, kDppWaveShr1, 0xF, 0xF, false);
-  keep.hi = (uint32_t)__builtin_amdgcn_update_dpp((int)keep.hi, (int)m.hi, kDppWaveShr1, 0xF, 0xF, false);
-#endif
   return keep;
 }
 
@@ -1583,19 +1552,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         } else {
           // (vector addressing from q + lane24 alone: no scalar splitting of
           // q; word wi + 1 <= kRingWords lies in the ring's mirror)
-#if RPP_RING_VALU
           const uint32_t x = q + lane24;
           const uint32_t* w = ring + ((x >> 5) & kRingMask);
           xh = 0u;
           return __builtin_amdgcn_alignbit(w[1], w[0], x);  // (shift x mod 32)
-#else
-          const uint32_t o = lane24 + (q & 31u);
-          uint32_t oi = o >> 5;
-          asm("" : "+v"(oi));  // (else the compiler masks o >> 3: one more op)
-          const uint32_t* w = ring + ((q >> 5) & kRingMask) + oi;
-          xh = 0u;
-          return __builtin_amdgcn_alignbit(w[1], w[0], o);  // (shift o mod 32)
-#endif
         }
       };
       // the header's fs (scalar; not clamped: a header outside [LO+1, HI+1]
@@ -1709,15 +1669,24 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           // (32-bit segments: the remainder may reach into the next word)
           const uint32_t rem = W32 ? __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(xh, xl, t[j]), 1, fs)
                                    : __builtin_amdgcn_ubfe(xr, t[j], fs);
+#if RPP_LIST32
+          // (one dword per code: a_i < 2^12 and fs <= 13)
+          list[base + j] = lshl_or(abase + t[j] - j * k, fs, rem);
+#else
           list2[base + j] = make_uint2(abase + t[j] - j * k, rem);
+#endif
           lds_fence();
         }
 #if RPP_END_LIST
-        // the next sub-block starts after code n-1's remainder: its pair,
+        // the next sub-block starts after code n-1's remainder: its entry,
         // read back from the list (one broadcast LDS read after the writes,
         // instead of picking the terminator out of the lane that holds it);
         // unused when the sub-block does not end in the window
+#if RPP_LIST32
+        Pe = pe_base + (__builtin_amdgcn_readfirstlane(list[n - 1]) >> fs);
+#else
         Pe = pe_base + __builtin_amdgcn_readfirstlane(list[2 * (n - 1)]);
+#endif
         __builtin_amdgcn_s_setprio(0);
         xln = seg_bits(Pe, xhn);
 #endif
@@ -1731,6 +1700,22 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // (aprev: a of the code before this lane's first, read from the list;
       // a_(-1) = 0 lies in the list's lead words)
       auto deltas = [&](uint4 tt, uint32_t aprev, uint32_t fs, uint32_t& d1, uint32_t& dsum) {
+#if RPP_LIST32
+        // entries p_i = (a_i << fs) | rem_i: ((a_i - a_(i-1)) << fs) | rem_i
+        // = p_i - (p_(i-1) & hi), two VOP2 operations per code
+        const uint32_t hi = 0xFFFFFFFFu << fs;
+        if constexpr (TWO) {
+          const uint32_t df0 = tt.x - (aprev & hi), df1 = tt.y - (tt.x & hi);
+          const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
+          d1 = (df1 >> 1) ^ neg_lsb(df1);
+          dsum = d0 + d1;
+        } else {
+          const uint32_t df = tt.x - (aprev & hi);
+          d1 = (df >> 1) ^ neg_lsb(df);
+          dsum = lane < n ? d1 : 0u;
+        }
+        return;
+#endif
         if constexpr (TWO) {
           const uint32_t df0 = lshl_or(tt.x - aprev, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
           const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
@@ -1782,17 +1767,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // instead of a bit-field extract and a shift-add, both VOP3)
       auto lookups = [&](uint32_t xl, uint32_t fs, uint4& e0, uint4& e1, uint4& e2, uint4& e3) {
         const uint4* tb = tab + 256u * fs;
-#if RPP_SDWA
         e0 = tb_entry(tb, sdwa_byte16<0>(xl));
         e1 = tb_entry(tb, sdwa_byte16<1>(xl));
         e2 = tb_entry(tb, sdwa_byte16<2>(xl));
         if constexpr (W32) e3 = tb_entry(tb, sdwa_byte16<3>(xl));
-#else
-        e0 = tb[xl & 0xFFu];
-        e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)];
-        e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
-        if constexpr (W32) e3 = tb[xl >> 24];
-#endif
         if constexpr (!W32) e3 = make_uint4(0u, 0u, 0u, 0u);
       };
 
@@ -1833,7 +1811,18 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         uint4 tt;
         uint32_t aprev;
-        if constexpr (TWO) {
+        if constexpr (RPP_LIST32) {
+          // (codes 2c, 2c+1 on lane c (TWO), code c on lane c; aprev: the
+          // entry before, the lead word 0 for lane 0)
+          if constexpr (TWO) {
+            const uint2 t2 = list2[lane];
+            tt = make_uint4(t2.x, t2.y, 0u, 0u);
+            aprev = list[2 * (int)lane - 1];
+          } else {
+            tt = make_uint4(list[lane], 0u, 0u, 0u);
+            aprev = list[(int)lane - 1];
+          }
+        } else if constexpr (TWO) {
           tt = list4[lane];
           aprev = list[4 * lane - 2];
         } else {
@@ -1845,53 +1834,25 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         RPP_TSTAMP(1);
         RPP_STAT(0, 1);
         uint32_t d1A, sumA, incA;
-        // Does the loop go on to the sub-block at Pn?  Tested before its
-        // parse, as scalar branches (the parse then only tells whether it
-        // ends in its window); if not, sub-block s's values are finished
-        // with a prefix scan of their own and the loop is left.
-#if RPP_EARLY_EXIT
-        if (s + 1 >= nsb_fast || Pn > pn_read_limit || !header_ok(hB)) {
-          deltas(tt, aprev, fs, d1A, sumA);
-          const uint32_t inc = wave_incl_sum(sumA);
-          store(d1A, inc, readlane(inc, kWave - 1), s);
-          ++s;
-          P = Pn;
-          if (P > lim) status = RPP_TRUNCATED_INPUT;
-          break;
-        }
-#else
+        // Does the loop go on to the sub-block at Pn?  (Computed here, tested
+        // with the parse's own result after it, so that sub-block s's values
+        // still ride on that parse's scan; testing it first, as scalar
+        // branches, measured 5 % slower: profiles/r04_decode_ab.jsonl.)
         const uint32_t nxt = (uint32_t)(s + 1 < nsb_fast) & (uint32_t)(Pn <= pn_read_limit) & header_ok(hB);
-#endif
         pn_read_limit = pn_limit;
         const uint32_t fsB = fs_of(hB);
         lookups(xlB, fsB, e0, e1, e2, e3);
         deltas(tt, aprev, fs, d1A, sumA);
-#ifdef RPP_PAD_SALU  // (diagnostic builds: N extra independent scalar adds per sub-block)
-        {
-          uint32_t pad = s;
-          asm volatile(".rept " RPP_PAD_SALU "\n\ts_add_u32 %0, %0, 1\n\t.endr" : "+s"(pad)::"scc");
-        }
-#endif
-#ifdef RPP_PAD_VALU  // (diagnostic builds: N extra independent v_perm per sub-block)
-        {
-          uint32_t pad = lane;
-          asm volatile(".rept " RPP_PAD_VALU "\n\tv_perm_b32 %0, %0, %0, %0\n\t.endr" : "+v"(pad));
-        }
-#endif
         RPP_TSTAMP(2);
         uint32_t PnB, xlC, xhC;
         ok = parse(Pn, xlB, xhB, fsB, e0, e1, e2, e3, PnB, xlC, xhC, sumA, incA,
                    [&](uint32_t inc, uint32_t inc_last) { store(d1A, inc, inc_last, s); });
         ++s;
         P = Pn;
-#if RPP_EARLY_EXIT
-        if (!ok) break;  // (the sub-block at P does not end in its window: P <= pn_limit < lim)
-#else
         if (!(ok & nxt)) {
           if (P > lim) status = RPP_TRUNCATED_INPUT;
           break;
         }
-#endif
         Pn = PnB;
         fs = fsB;
         xlB = xlC;

@@ -38,8 +38,8 @@ for step in "$@"; do
       run facade_16m 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 4 16 ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     trace)
-      rm -rf $O/trace
-      run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu ;;
+      rm -rf gpurun_out/prof/trace
+      run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --no-cpu ;;
     pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

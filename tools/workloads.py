@@ -67,11 +67,11 @@ def poisson_scaled(n: int, lam: float, ulsb: int, seed: int) -> torch.Tensor:
     return out
 
 
-def pipe_for(cfg, x, block_samples):
+def pipe_for(cfg, x, block_samples, dec=None):
     nb = len(block_samples)
     offs = np.zeros(nb, np.int64)
     offs[1:] = np.cumsum(block_samples)[:-1]
-    p = parallel.ShardPipeline(cfg, x, offs, np.asarray(block_samples, np.int64))
+    p = parallel.ShardPipeline(cfg, x, offs, np.asarray(block_samples, np.int64), decode_options=dec)
     p.step()
     torch.cuda.synchronize()
     p.check(x)
@@ -192,6 +192,27 @@ def case_sweep():
             del p
 
 
+def case_paths():
+    """configs[4] bs 16 / 32 decode by each path: the default (rows kernel), one wave per
+    stream (fused) and the segmented decode at three unit sizes."""
+    for bs in (16, 32):
+        for bits in (10, 16):
+            ulsb = 16 - bits
+            lam = 1000.0 / (1 << (2 * ulsb))
+            cfg = codec.CodecConfig(bs, 1, "big", ulsb)
+            x = poisson_scaled(4096 * 32768, max(lam, 4.0), ulsb, 11)
+            raw = 4096 * 32768 * 2
+            res = {}
+            for name, dec in (("auto", None), ("fused", codec.DecodeOptions(path="fused")),
+                              ("seg12", codec.DecodeOptions(path="segmented", seg_log2=12)),
+                              ("seg13", codec.DecodeOptions(path="segmented", seg_log2=13)),
+                              ("seg14", codec.DecodeOptions(path="segmented", seg_log2=14))):
+                p = pipe_for(cfg, x, [32768] * 4096, dec)
+                res[name] = round(raw / timed(p.decode) / GIB, 2)
+                del p
+            report("paths", bs=bs, bits=bits, ulsb=ulsb, decode_GiBps=res)
+
+
 def case_e2e():
     cfg = codec.CodecConfig(128, 1, "big", 0)
     nb, n = 4096, 32768
@@ -225,7 +246,7 @@ def case_e2e():
 
 
 CASES = {"gen": case_gen, "fits": case_fits, "frames": case_frames, "mix": case_mix, "sweep": case_sweep,
-         "e2e": case_e2e}
+         "e2e": case_e2e, "paths": case_paths}
 
 if __name__ == "__main__":
     for name in sys.argv[1:] or list(CASES):
