@@ -182,11 +182,12 @@ def kernel_source_sha256() -> str:
     return h.hexdigest()
 
 
-def profiled_counters(kernel: str):
+def profiled_counters(kernel: str, profile: str = "pmc_latest.json"):
     """PMC figures of `kernel` per launch from profiles/pmc_latest.json (rocprofv3 FETCH_SIZE / WRITE_SIZE
     passes with the gfx950 corrections of MI355X_MICROARCH.md, GRBM_GUI_ACTIVE), only if they were taken
-    of the current kernel sources: (dict or None, provenance)."""
-    pmc = ROOT / "profiles" / "pmc_latest.json"
+    of the current kernel sources: (dict or None, provenance).  (profiles/pmc_mix.json: the mix's
+    "encode" / "decode" calls, every kernel of a call summed: tools/pmc_mix_summary.py.)"""
+    pmc = ROOT / "profiles" / profile
     if not pmc.exists():
         return None, "no PMC profile"
     try:
@@ -348,6 +349,15 @@ def main() -> None:
                 "traffic_source": "not profiled for the mix",
             },
         }
+        # (PMC of a 32 GiB mix: only at that size are the bytes per call this run's)
+        mc, msrc = profiled_counters("decode", "pmc_mix.json") if args.mix_gib == 32 and world == 1 else \
+            (None, "the PMC profile is of the 32 GiB mix on one GPU")
+        if mc and "hbm_bytes_per_call" in mc:
+            result["roofline"]["traffic"] = mc["hbm_bytes_per_call"]
+            result["roofline"]["traffic_source"] = msrc + ": every kernel of one decode call"
+            result["roofline"]["algorithmic_bytes"] = int(dec_bytes)
+        else:
+            result["roofline"]["traffic_source"] = msrc
         if rank == 0:
             print(json.dumps(result), flush=True)
         if world > 1:

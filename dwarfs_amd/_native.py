@@ -60,6 +60,15 @@ EXPORTED_SYMBOLS = (
     "rpp_pcm_check_format",
     "rpp_pcm_unpack",
     "rpp_pcm_pack",
+    "rpp_flac_frame_header",
+    "rpp_flac_parse_frame",
+    "rpp_flac_stream_header",
+    "rpp_flac_parse_stream",
+    "rpp_flac_frame_bound",
+    "rpp_flac_encode_workspace_bytes",
+    "rpp_flac_encode",
+    "rpp_flac_decode_workspace_bytes",
+    "rpp_flac_decode",
 )
 
 
@@ -94,6 +103,28 @@ class RppFrame(C.Structure):
         ("unused_lsb_count", C.c_uint32),
         ("big_endian", C.c_uint32),
         ("ricepp_version", C.c_uint32),
+    ]
+
+
+class RppFlacFrame(C.Structure):
+    """``rpp_flac_frame`` (the flac_block_header fields, thrift/compression.thrift:36-40)."""
+
+    _fields_ = [
+        ("uncompressed_bytes", C.c_uint64),
+        ("num_channels", C.c_uint32),
+        ("bits_per_sample", C.c_uint32),
+        ("flags", C.c_uint32),
+    ]
+
+
+class RppFlacStreamInfo(C.Structure):
+    _fields_ = [
+        ("min_blocksize", C.c_uint32),
+        ("max_blocksize", C.c_uint32),
+        ("sample_rate", C.c_uint32),
+        ("channels", C.c_uint32),
+        ("bits_per_sample", C.c_uint32),
+        ("total_samples", C.c_uint64),
     ]
 
 
@@ -164,6 +195,25 @@ def lib() -> C.CDLL:
         L.rpp_pcm_unpack.restype = C.c_int
         L.rpp_pcm_pack.argtypes = [C.POINTER(RppPcmFormat), P, P, C.c_uint64, P]
         L.rpp_pcm_pack.restype = C.c_int
+        L.rpp_flac_frame_header.argtypes = [C.POINTER(RppFlacFrame), P]
+        L.rpp_flac_frame_header.restype = C.c_size_t
+        L.rpp_flac_parse_frame.argtypes = [P, C.c_size_t, C.POINTER(RppFlacFrame)]
+        L.rpp_flac_parse_frame.restype = C.c_long
+        L.rpp_flac_stream_header.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, P]
+        L.rpp_flac_stream_header.restype = C.c_size_t
+        L.rpp_flac_parse_stream.argtypes = [P, C.c_size_t, C.POINTER(RppFlacStreamInfo)]
+        L.rpp_flac_parse_stream.restype = C.c_long
+        L.rpp_flac_frame_bound.argtypes = [C.c_uint32, C.c_uint32]
+        L.rpp_flac_frame_bound.restype = C.c_uint64
+        L.rpp_flac_encode_workspace_bytes.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+        L.rpp_flac_encode_workspace_bytes.restype = C.c_uint64
+        L.rpp_flac_encode.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, P]
+        L.rpp_flac_encode.restype = C.c_int
+        L.rpp_flac_decode_workspace_bytes.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.rpp_flac_decode_workspace_bytes.restype = C.c_uint64
+        L.rpp_flac_decode.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, P, P,
+                                      C.c_uint32, P, C.c_uint64, P, P]
+        L.rpp_flac_decode.restype = C.c_int
         if L.rpp_abi_version() != 1:
             raise RuntimeError("libricepp_amd.so ABI mismatch")
         _lib = L

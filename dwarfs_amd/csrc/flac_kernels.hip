@@ -1,0 +1,981 @@
+// flac_kernels.hip -- the FLAC block codec on MI355X: RFC 9639 frames of
+// interleaved PCM samples, the compute side of DwarFS's flac_block_compressor
+// and flac_block_decompressor (src/compression/flac.cpp:215-403, :405-489;
+// the reference runs libFLAC++ on the CPU, one block per call).
+//
+// Parity is unpinned: libFLAC is absent here and the reference holds no FLAC
+// fixture.  The decoder accepts every frame kind RFC 9639 defines (constant,
+// verbatim, fixed and LPC subframes, wasted bits, both Rice methods, escape
+// partitions, the four channel assignments, any block size code), so it reads
+// libFLAC's streams; the encoder writes a subset (fixed predictors), so its
+// streams differ from libFLAC's but are valid FLAC.  Checked against the CPU
+// restatement in oracle/flac_oracle.c both ways (tests/test_gpu_flac.py).
+//
+// Encode (rpp_flac_encode): one wave per 4096-sample frame (libFLAC's level-5
+// block size; flac.cpp:311-313 sets level 5 by default, :516).  The frame's
+// channels are staged in LDS; per subframe source the wave finds the wasted
+// low bits, the constant case, the fixed predictor order with the smallest
+// sum of |residual| (orders 0-4, as libFLAC's fixed-order estimate) and the
+// Rice partition order (0-5) and per-partition parameters with the fewest
+// bits, and for two channels the cheapest of the four channel assignments;
+// then every lane writes its samples' codes into an LDS bit window at
+// positions from one wave prefix sum (MSB-first words, byte-swapped on the way
+// out).  Frames go to worst-case slots, are packed back to back
+// (rpp_flac_pack_kernel) and get their CRC-16 on the packed bytes
+// (rpp_flac_crc_kernel: per-lane CRCs combined by GF(2) shifts).
+//
+// Decode (rpp_flac_decode): frames are not indexed, so every byte that starts
+// a valid frame header (sync, fields, CRC-8) is a candidate
+// (rpp_flac_scan_kernel); each candidate is decoded by one lane into a
+// scratch slot and its CRC-16 checked (rpp_flac_frame_kernel,
+// rpp_flac_crc_kernel); one lane walks the chain of frames from the first
+// (rpp_flac_chain_kernel) and the chained frames' samples are placed
+// (rpp_flac_place_kernel).  A false candidate (random bytes passing sync,
+// CRC-8 and CRC-16) can only matter if it lies on the chain, which it cannot:
+// the chain only visits the positions where the previous frame ends.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ricepp_amd.h"
+
+namespace {
+
+constexpr uint32_t kFlacBlock = 4096;   // samples per encoded frame
+constexpr uint32_t kWave = 64;
+constexpr uint32_t kSpl = kFlacBlock / kWave;  // samples per lane
+constexpr uint32_t kMaxPo = 5;          // partition orders 0..5 (libFLAC level 5: -r 5)
+constexpr uint32_t kWinWords = 4352;    // LDS bit window: one subframe (4096 x 33 bits) + slack
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
+  return v;
+}
+__device__ __forceinline__ int32_t wave_min(int32_t v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t& total) {
+  const uint32_t lane = lane_id();
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+    if (lane >= d) x += y;
+  }
+  total = (uint32_t)__shfl((int)x, 63);
+  return x - v;
+}
+
+// ---- CRCs (RFC 9639 9.1.8 CRC-8 poly 0x07, 9.3 CRC-16 poly 0x8005; init 0) ----
+__device__ __forceinline__ uint8_t crc8_byte(uint8_t c, uint8_t b) {
+  c ^= b;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c = (uint8_t)((c & 0x80) ? (c << 1) ^ 0x07 : c << 1);
+  return c;
+}
+__device__ __forceinline__ uint16_t crc16_byte(const uint16_t* tab, uint16_t c, uint8_t b) {
+  return (uint16_t)((c << 8) ^ tab[(c >> 8) ^ b]);
+}
+// a * b mod (x^16 + 0x8005) over GF(2)
+__device__ __forceinline__ uint32_t gf16_mul(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+  for (int i = 15; i >= 0; --i) {
+    r <<= 1;
+    if (r & 0x10000u) r ^= 0x18005u;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r & 0xFFFFu;
+}
+// x^(8 n) mod P: a CRC advanced over n zero bytes is crc * this
+__device__ __forceinline__ uint32_t gf16_xpow8(uint64_t n) {
+  uint32_t result = 1, base = 0x100;  // x^8
+  while (n) {
+    if (n & 1) result = gf16_mul(result, base);
+    base = gf16_mul(base, base);
+    n >>= 1;
+  }
+  return result;
+}
+
+// ---- frame header fields ----
+__device__ __forceinline__ uint32_t bs_code(uint32_t bs, uint32_t& extra_bits) {
+  extra_bits = 0;
+  if (bs == 192) return 1;
+  for (uint32_t c = 2; c <= 5; ++c)
+    if (bs == (576u << (c - 2))) return c;
+  for (uint32_t c = 8; c <= 15; ++c)
+    if (bs == (256u << (c - 8))) return c;
+  extra_bits = bs <= 256 ? 8 : 16;
+  return bs <= 256 ? 6 : 7;
+}
+__device__ __forceinline__ uint32_t ss_code(uint32_t bps) {
+  switch (bps) {
+    case 8: return 1;
+    case 12: return 2;
+    case 16: return 4;
+    case 20: return 5;
+    case 24: return 6;
+    case 32: return 7;
+    default: return 0;
+  }
+}
+// header bytes of frame fn (channel assignment `assign`) into h[]; returns the length before the CRC-8
+__device__ uint32_t build_header(uint8_t* h, uint64_t fn, uint32_t bs, uint32_t assign, uint32_t bps) {
+  uint32_t extra;
+  const uint32_t bc = bs_code(bs, extra);
+  uint32_t n = 0;
+  h[n++] = 0xFF;
+  h[n++] = 0xF8;  // fixed blocking strategy
+  h[n++] = (uint8_t)((bc << 4) | 10u);  // 48 kHz (flac.cpp:311)
+  h[n++] = (uint8_t)((assign << 4) | (ss_code(bps) << 1));
+  if (fn < 0x80) {
+    h[n++] = (uint8_t)fn;
+  } else {
+    const int m = fn < 0x800 ? 2 : fn < 0x10000 ? 3 : fn < 0x200000 ? 4 : fn < 0x4000000 ? 5 : fn < 0x80000000ull ? 6 : 7;
+    h[n++] = m == 7 ? 0xFE : (uint8_t)(((0xFF00u >> m) & 0xFFu) | (uint32_t)(fn >> (6 * (m - 1))));
+    for (int i = m - 2; i >= 0; --i) h[n++] = (uint8_t)(0x80u | ((fn >> (6 * i)) & 0x3Fu));
+  }
+  if (extra == 8) h[n++] = (uint8_t)(bs - 1);
+  if (extra == 16) {
+    h[n++] = (uint8_t)((bs - 1) >> 8);
+    h[n++] = (uint8_t)(bs - 1);
+  }
+  return n;
+}
+
+// ---- encode ----
+struct FlacEncParams {
+  const int32_t* x;     // interleaved samples [nsamples * channels]
+  uint64_t nsamples;    // per channel
+  uint32_t channels, bps;
+  uint8_t* slots;       // frame slots (slot_bytes each)
+  uint64_t slot_bytes;
+  uint64_t* sizes;      // [frames] frame bytes (CRC-16 included)
+  uint32_t frames;
+};
+
+struct SubPlan {
+  uint32_t type;     // 0 constant, 1 verbatim, 2 fixed
+  uint32_t order, wasted, bps;  // bps: of the coded samples (after wasted bits)
+  uint32_t po, method;
+  uint64_t bits;
+};
+
+struct EncShared {
+  int32_t smp[2][kFlacBlock];
+  uint32_t win[kWinWords];
+  uint32_t kpar[4][1u << kMaxPo];  // Rice parameters per source and partition
+  unsigned long long psum[1u << kMaxPo];
+  unsigned long long pbits[kMaxPo + 1][1u << kMaxPo];
+};
+
+// source sample i: 0 / 1 = staged channel, 2 = side (L - R), 3 = mid ((L + R) >> 1)
+__device__ __forceinline__ int64_t src_sample(const EncShared& sh, uint32_t src, uint32_t i) {
+  const int64_t l = sh.smp[0][i];
+  if (src == 0) return l;
+  const int64_t r = sh.smp[1][i];
+  if (src == 1) return r;
+  if (src == 2) return l - r;
+  return (l + r) >> 1;
+}
+__device__ __forceinline__ uint64_t fold(int64_t r) {
+  return r >= 0 ? (uint64_t)r << 1 : ((uint64_t)(-(r + 1)) << 1) | 1u;
+}
+__device__ __forceinline__ int64_t fixed_res(const EncShared& sh, uint32_t src, uint32_t i, uint32_t order,
+                                             uint32_t wasted) {
+  auto s = [&](uint32_t j) { return src_sample(sh, src, j) >> wasted; };
+  switch (order) {
+    case 0: return s(i);
+    case 1: return s(i) - s(i - 1);
+    case 2: return s(i) - 2 * s(i - 1) + s(i - 2);
+    case 3: return s(i) - 3 * s(i - 1) + 3 * s(i - 2) - s(i - 3);
+    default: return s(i) - 4 * s(i - 1) + 6 * s(i - 2) - 4 * s(i - 3) + s(i - 4);
+  }
+}
+
+// The cheapest subframe of source `src` (samples [0, bs), sbps bits each);
+// its Rice parameters go to sh.kpar[src]
+__device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint32_t sbps) {
+  const uint32_t lane = lane_id();
+  SubPlan P{};
+  // wasted bits and the constant case
+  uint32_t orv = 0;
+  int32_t mn = INT32_MAX, mx = INT32_MIN;
+  for (uint32_t i = lane; i < bs; i += kWave) {
+    const int64_t v = src_sample(sh, src, i);
+    orv |= (uint32_t)v;
+    mn = min(mn, (int32_t)v);
+    mx = max(mx, (int32_t)v);
+  }
+  orv = wave_or(orv);
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  uint32_t wasted = 0;
+  if (orv) {
+    wasted = (uint32_t)__builtin_ctz(orv);
+    if (wasted > sbps - 1) wasted = sbps - 1;
+  }
+  // (a side channel of 32 bits would not fit the int32 staging: never formed, bps < 32 for stereo)
+  P.wasted = wasted;
+  P.bps = sbps - wasted;
+  const uint64_t hdr = 8 + (wasted ? wasted : 0);  // type byte (+ unary wasted count)
+  if (mn == mx) {
+    P.type = 0;
+    P.bits = hdr + P.bps;
+    return P;
+  }
+  P.type = 1;
+  P.bits = hdr + (uint64_t)P.bps * bs;
+  // fixed predictor order: the smallest sum of |residual| (residuals must fit 32 bits)
+  uint64_t sabs[5] = {0, 0, 0, 0, 0};
+  uint32_t bad = 0;
+  for (uint32_t i = lane; i < bs; i += kWave) {
+#pragma unroll
+    for (uint32_t o = 0; o <= 4; ++o) {
+      if (i < o) continue;
+      const int64_t r = fixed_res(sh, src, i, o, wasted);
+      if (r < INT32_MIN || r > INT32_MAX) bad |= 1u << o;
+      sabs[o] += (uint64_t)(r < 0 ? -r : r);
+    }
+  }
+  bad = wave_or(bad);
+  uint32_t order = 0xFFFFFFFFu;
+  uint64_t best = ~0ull;
+#pragma unroll
+  for (uint32_t o = 0; o <= 4; ++o) {
+    const uint64_t s = wave_sum(sabs[o]);
+    if (!((bad >> o) & 1u) && o < bs && s < best) {
+      best = s;
+      order = o;
+    }
+  }
+  if (order == 0xFFFFFFFFu) return P;  // verbatim
+  // Rice partitions: orders 0..kMaxPo that divide bs with a first partition
+  // longer than the predictor order; per partition k = floor(log2(mean u))
+  for (uint32_t p = lane; p < (1u << kMaxPo); p += kWave) sh.psum[p] = 0;
+  for (uint32_t p = lane; p < (kMaxPo + 1) * (1u << kMaxPo); p += kWave) (&sh.pbits[0][0])[p] = 0;
+  __syncthreads();
+  uint32_t pomax = 0;
+  while (pomax < kMaxPo && bs % (2u << pomax) == 0 && (bs >> (pomax + 1)) > order) ++pomax;
+  const uint32_t psz = bs >> pomax;  // samples per finest partition
+  for (uint32_t i = lane; i < bs; i += kWave)
+    if (i >= order) atomicAdd(&sh.psum[i / psz], (unsigned long long)fold(fixed_res(sh, src, i, order, wasted)));
+  __syncthreads();
+  for (uint32_t po = 0; po <= pomax; ++po) {
+    const uint32_t np = 1u << po, per = bs >> po;
+    for (uint32_t i = lane; i < bs; i += kWave) {
+      if (i < order) continue;
+      const uint32_t p = i / per;
+      // the partition's sum over the finest ones it covers
+      uint64_t sum = 0;
+      const uint32_t f = 1u << (pomax - po);
+      for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
+      const uint32_t cnt = per - (p == 0 ? order : 0u);
+      const uint64_t mean = cnt ? sum / cnt : 0;
+      const uint32_t k = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
+      const uint64_t u = fold(fixed_res(sh, src, i, order, wasted));
+      atomicAdd(&sh.pbits[po][p], (unsigned long long)((u >> k) + 1 + k));
+    }
+    (void)np;
+  }
+  __syncthreads();
+  uint64_t rbest = ~0ull;
+  uint32_t bpo = 0, bmethod = 0;
+  for (uint32_t po = 0; po <= pomax; ++po) {
+    const uint32_t np = 1u << po, per = bs >> po, f = 1u << (pomax - po);
+    uint64_t tot = 6;
+    uint32_t kmaxp = 0;
+    for (uint32_t p = 0; p < np; ++p) {
+      uint64_t sum = 0;
+      for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
+      const uint32_t cnt = per - (p == 0 ? order : 0u);
+      const uint64_t mean = cnt ? sum / cnt : 0;
+      const uint32_t k = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
+      kmaxp = max(kmaxp, k);
+      tot += sh.pbits[po][p];
+    }
+    const uint32_t method = kmaxp > 14 ? 1u : 0u;
+    tot += (uint64_t)np * (method ? 5 : 4);
+    if (tot < rbest) {
+      rbest = tot;
+      bpo = po;
+      bmethod = method;
+    }
+  }
+  {
+    const uint32_t np = 1u << bpo, per = bs >> bpo, f = 1u << (pomax - bpo);
+    for (uint32_t p = lane; p < np; p += kWave) {
+      uint64_t sum = 0;
+      for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
+      const uint32_t cnt = per - (p == 0 ? order : 0u);
+      const uint64_t mean = cnt ? sum / cnt : 0;
+      sh.kpar[src][p] = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
+    }
+  }
+  __syncthreads();
+  const uint64_t fbits = hdr + (uint64_t)order * P.bps + rbest;
+  if (fbits < P.bits) {
+    P.type = 2;
+    P.order = order;
+    P.po = bpo;
+    P.method = bmethod;
+    P.bits = fbits;
+  }
+  return P;
+}
+
+// ORs the low `len` (<= 33) bits of v into the MSB-first window at bit pos
+__device__ __forceinline__ void put_bits(uint32_t* win, uint32_t pos, uint64_t v, uint32_t len) {
+  if (!len) return;
+  const uint32_t w = pos >> 5, sh = pos & 31u;
+  v &= len >= 64 ? ~0ull : ((1ull << len) - 1);
+  // bits [sh, sh + len) of the 64-bit pair (w, w + 1), MSB first
+  const uint64_t x = v << (64u - len - sh);
+  atomicOr(&win[w], (uint32_t)(x >> 32));
+  if (sh + len > 32) atomicOr(&win[w + 1], (uint32_t)x);
+}
+
+// Emits subframe plan P of source src at window bit `pos`; returns the end
+// (pos is absolute in the frame; the window holds its bits from wbase on)
+__device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src, uint32_t bs, uint32_t pos,
+                                  uint32_t wbase) {
+  const uint32_t lane = lane_id();
+  uint32_t* const win = sh.win;
+  auto put = [&](uint32_t at_abs, uint64_t v, uint32_t len) { put_bits(win, at_abs - wbase, v, len); };
+  // lane 0: header, wasted count, warm-up samples, residual header
+  uint32_t head = 8 + P.wasted;
+  if (P.type == 0) head += P.bps;
+  if (P.type == 2) head += P.order * P.bps + 6;
+  // per-lane bits of its samples
+  const uint32_t per = P.type == 2 ? bs >> P.po : bs;
+  const uint32_t pbits = P.method ? 5u : 4u;
+  uint32_t mine = 0;
+  if (P.type == 1) {
+    for (uint32_t j = 0; j < kSpl; ++j) {
+      const uint32_t i = lane * kSpl + j;
+      if (i < bs) mine += P.bps;
+    }
+  } else if (P.type == 2) {
+    for (uint32_t j = 0; j < kSpl; ++j) {
+      const uint32_t i = lane * kSpl + j;
+      if (i >= bs || i < P.order) continue;
+      const uint32_t p = i / per;
+      if (i == (p == 0 ? P.order : p * per)) mine += pbits;
+      const uint32_t k = sh.kpar[src][p];
+      mine += (uint32_t)(fold(fixed_res(sh, src, i, P.order, P.wasted)) >> k) + 1 + k;
+    }
+  }
+  uint32_t total;
+  uint32_t at = pos + head + wave_excl_sum(mine, total);
+  if (lane == 0) {
+    const uint32_t type6 = P.type == 0 ? 0u : P.type == 1 ? 1u : 8u + P.order;
+    put(pos, (type6 << 1) | (P.wasted ? 1u : 0u), 8);
+    uint32_t q = pos + 8;
+    if (P.wasted) {
+      put(q + P.wasted - 1, 1, 1);  // unary wasted - 1
+      q += P.wasted;
+    }
+    if (P.type == 0) {
+      put(q, (uint64_t)(src_sample(sh, src, 0) >> P.wasted), P.bps);
+    } else if (P.type == 2) {
+      for (uint32_t i = 0; i < P.order; ++i, q += P.bps)
+        put(q, (uint64_t)(src_sample(sh, src, i) >> P.wasted), P.bps);
+      put(q, (P.method << 4) | P.po, 6);
+    }
+  }
+  if (P.type == 1) {
+    for (uint32_t j = 0; j < kSpl; ++j) {
+      const uint32_t i = lane * kSpl + j;
+      if (i >= bs) break;
+      put(at, (uint64_t)(src_sample(sh, src, i) >> P.wasted), P.bps);
+      at += P.bps;
+    }
+  } else if (P.type == 2) {
+    for (uint32_t j = 0; j < kSpl; ++j) {
+      const uint32_t i = lane * kSpl + j;
+      if (i >= bs) break;
+      if (i < P.order) continue;
+      const uint32_t p = i / per;
+      const uint32_t k = sh.kpar[src][p];
+      if (i == (p == 0 ? P.order : p * per)) {
+        put(at, k, pbits);
+        at += pbits;
+      }
+      const uint64_t u = fold(fixed_res(sh, src, i, P.order, P.wasted));
+      at += (uint32_t)(u >> k);  // the unary zeros
+      put(at, (1ull << k) | (u & ((1ull << k) - 1)), k + 1);
+      at += k + 1;
+    }
+  }
+  __syncthreads();
+  return pos + head + total;
+}
+
+// Moves the window's complete words to the slot (byte order of the stream),
+// keeping the partial word; win_w0 = slot word of win[0]
+__device__ void flush(EncShared& sh, uint8_t* slot, uint32_t& win_w0, uint32_t pos, bool all) {
+  const uint32_t lane = lane_id();
+  const uint32_t end = all ? (pos + 31) >> 5 : pos >> 5;  // words to write (slot-relative)
+  uint32_t* out = reinterpret_cast<uint32_t*>(slot);
+  for (uint32_t w = win_w0 + lane; w < end; w += kWave) out[w] = __builtin_bswap32(sh.win[w - win_w0]);
+  __syncthreads();
+  if (!all) {
+    const uint32_t keep = sh.win[end - win_w0];
+    __syncthreads();
+    for (uint32_t w = lane; w < kWinWords; w += kWave) sh.win[w] = 0;
+    __syncthreads();
+    if (lane == 0) sh.win[0] = keep;
+    __syncthreads();
+    win_w0 = end;
+  }
+}
+
+__global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  EncShared& sh = *reinterpret_cast<EncShared*>(smem);
+  const uint32_t fn = blockIdx.x, lane = lane_id();
+  if (fn >= p.frames) return;
+  const uint64_t f0 = (uint64_t)fn * kFlacBlock;
+  const uint32_t bs = (uint32_t)min((uint64_t)kFlacBlock, p.nsamples - f0);
+  const uint32_t C = p.channels;
+  uint8_t* slot = p.slots + (uint64_t)fn * p.slot_bytes;
+  for (uint32_t w = lane; w < kWinWords; w += kWave) sh.win[w] = 0;
+  uint32_t win_w0 = 0;
+  auto stage = [&](uint32_t slotc, uint32_t c) {
+    for (uint32_t i = lane; i < bs; i += kWave) sh.smp[slotc][i] = p.x[(f0 + i) * C + c];
+  };
+  const bool stereo = C == 2 && p.bps < 32;
+  SubPlan plans[4];
+  uint32_t assign = C - 1;
+  if (stereo) {
+    stage(0, 0);
+    stage(1, 1);
+    __syncthreads();
+    // the four sources' plans, Rice parameters kept per source (kpar[src])
+    for (uint32_t s = 0; s < 4; ++s) plans[s] = plan_subframe(sh, s, bs, s == 2 ? p.bps + 1 : p.bps);
+    const uint64_t ind = plans[0].bits + plans[1].bits, ls = plans[0].bits + plans[2].bits,
+                   rs = plans[2].bits + plans[1].bits, ms = plans[3].bits + plans[2].bits;
+    uint64_t best = ind;
+    assign = 1;
+    if (ls < best) best = ls, assign = 8;
+    if (rs < best) best = rs, assign = 9;
+    if (ms < best) best = ms, assign = 10;
+  }
+  // header (byte-aligned at the slot start) and its CRC-8
+  uint8_t hdr[20];
+  const uint32_t hlen = build_header(hdr, fn, bs, assign, p.bps);
+  uint8_t c8 = 0;
+  for (uint32_t i = 0; i < hlen; ++i) c8 = crc8_byte(c8, hdr[i]);
+  hdr[hlen] = c8;
+  if (lane == 0)
+    for (uint32_t i = 0; i <= hlen; ++i) put_bits(sh.win, 8 * i, hdr[i], 8);
+  __syncthreads();
+  uint32_t pos = 8 * (hlen + 1);
+  if (stereo) {
+    const uint32_t s0 = assign == 9 ? 2u : assign == 10 ? 3u : 0u;
+    const uint32_t s1 = assign == 1 ? 1u : assign == 9 ? 1u : 2u;
+    pos = emit_subframe(sh, plans[s0], s0, bs, pos, 32 * win_w0);
+    flush(sh, slot, win_w0, pos, false);
+    pos = emit_subframe(sh, plans[s1], s1, bs, pos, 32 * win_w0);
+    flush(sh, slot, win_w0, pos, false);
+  } else {
+    for (uint32_t c = 0; c < C; ++c) {
+      stage(0, c);
+      __syncthreads();
+      const SubPlan P = plan_subframe(sh, 0, bs, p.bps);
+      pos = emit_subframe(sh, P, 0, bs, pos, 32 * win_w0);
+      flush(sh, slot, win_w0, pos, false);
+    }
+  }
+  pos = (pos + 7) & ~7u;  // zero padding to a byte
+  flush(sh, slot, win_w0, pos, true);
+  if (lane == 0) p.sizes[fn] = pos / 8 + 2;  // + CRC-16 (rpp_flac_crc_kernel)
+}
+
+// ---- pack: frames back to back ----
+__global__ __launch_bounds__(256) void rpp_flac_pack_kernel(const uint8_t* slots, uint64_t slot_bytes,
+                                                          const uint64_t* sizes, const uint64_t* offs,
+                                                          uint8_t* out, uint32_t frames) {
+  const uint32_t f = blockIdx.x;
+  if (f >= frames) return;
+  const uint8_t* s = slots + (uint64_t)f * slot_bytes;
+  uint8_t* d = out + offs[f];
+  const uint64_t n = sizes[f] - 2;
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
+}
+
+// lens = sizes - 2 (the CRC covers the frame before it), total = offs[last] + sizes[last]
+__global__ void rpp_flac_lens_kernel(const uint64_t* sizes, const uint64_t* offs, uint64_t* lens, uint64_t frames,
+                                     uint64_t* total) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < frames) lens[i] = sizes[i] - 2;
+  if (i == frames - 1) *total = offs[i] + sizes[i];
+}
+
+// ---- CRC-16 of frames: per-lane chunks combined by GF(2) shifts ----
+// mode 0: write the CRC after [start, start + len); mode 1: compare with the
+// two bytes there and set ok[f]
+__global__ __launch_bounds__(64) void rpp_flac_crc_kernel(const uint8_t* buf, const uint64_t* starts,
+                                                        const uint64_t* lens, uint32_t frames, uint8_t* wbuf,
+                                                        uint32_t* ok, const uint32_t* count) {
+  __shared__ uint16_t tab[256];
+  const uint32_t lane = lane_id();
+  for (uint32_t i = lane; i < 256; i += kWave) {
+    uint16_t d = (uint16_t)(i << 8);
+    for (int k = 0; k < 8; ++k) d = (uint16_t)((d & 0x8000) ? (d << 1) ^ 0x8005 : d << 1);
+    tab[i] = d;
+  }
+  __syncthreads();
+  const uint32_t nf = count ? min(*count, frames) : frames;
+  for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
+    const uint64_t len = lens[f];
+    if (len == ~0ull) continue;  // (decode: a candidate that did not parse)
+    const uint8_t* s = buf + starts[f];
+    const uint64_t chunk = (len + kWave - 1) / kWave;
+    const uint64_t lo = min(len, chunk * lane), hi = min(len, lo + chunk);
+    uint16_t c = 0;
+    for (uint64_t i = lo; i < hi; ++i) c = crc16_byte(tab, c, s[i]);
+    // advance over the bytes after this lane's chunk
+    uint32_t v = gf16_mul(c, gf16_xpow8(len - hi));
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o);
+    if (lane == 0) {
+      if (wbuf) {
+        wbuf[starts[f] + len] = (uint8_t)(v >> 8);
+        wbuf[starts[f] + len + 1] = (uint8_t)v;
+      } else {
+        ok[f] = (s[len] == (uint8_t)(v >> 8) && s[len + 1] == (uint8_t)v) ? 1u : 0u;
+      }
+    }
+  }
+}
+
+// ---- decode ----
+struct FlacDecParams {
+  const uint8_t* in;   // the frames (after the metadata blocks)
+  uint64_t nbytes;
+  uint32_t channels, bps, max_bs;
+  uint64_t nsamples;   // per channel (STREAMINFO)
+  uint32_t* cand_at;   // [nbytes] candidate index + 1 starting at that byte (0: none)
+  uint64_t* cand_pos;  // [max_cand]
+  uint32_t* cand_info; // [max_cand] block size
+  uint64_t* cand_len;  // [max_cand] bytes before the CRC-16 (~0: did not parse)
+  uint32_t* cand_ok;   // [max_cand] CRC-16 matches
+  uint32_t* ncand;     // candidates found
+  uint32_t max_cand;
+  int32_t* scratch;    // [max_cand][max_bs * channels]
+  uint32_t* chain;     // [frames] candidate of chained frame i
+  uint64_t* chain_off; // [frames] first sample of chained frame i
+  uint32_t* nchain;
+  int32_t* out;        // interleaved samples [nsamples * channels]
+  int32_t* status;
+};
+
+// MSB-first bit reader over global memory
+struct BitReader {
+  const uint8_t* p;
+  uint64_t len;  // bytes readable
+  uint64_t pos;  // bit position
+  bool err;
+  __device__ uint64_t get(uint32_t n) {
+    if (n == 0) return 0;
+    if (pos + n > 8 * len) {
+      err = true;
+      pos = 8 * len;
+      return 0;
+    }
+    uint64_t v = 0;
+    uint32_t left = n;
+    while (left) {
+      const uint32_t bi = (uint32_t)(pos & 7);
+      const uint32_t take = min(left, 8u - bi);
+      const uint32_t byte = p[pos >> 3];
+      v = (v << take) | ((byte >> (8 - bi - take)) & ((1u << take) - 1));
+      pos += take;
+      left -= take;
+    }
+    return v;
+  }
+  __device__ int64_t get_signed(uint32_t n) {
+    if (n == 0) return 0;
+    uint64_t v = get(n);
+    if (n < 64 && ((v >> (n - 1)) & 1u)) v |= ~0ull << n;
+    return (int64_t)v;
+  }
+  __device__ uint64_t unary() {
+    uint64_t q = 0;
+    for (;;) {
+      if (pos >= 8 * len) {
+        err = true;
+        return q;
+      }
+      const uint32_t bi = (uint32_t)(pos & 7);
+      const uint32_t rest = ((uint32_t)p[pos >> 3] << bi) & 0xFFu;  // remaining bits at the top
+      if (rest) {
+        const uint32_t z = (uint32_t)__builtin_clz(rest) - 24;
+        pos += z + 1;
+        return q + z;
+      }
+      q += 8 - bi;
+      pos += 8 - bi;
+    }
+  }
+};
+
+// Parses a frame header at byte p (no CRC-16); returns its length (0: not a
+// valid header for this stream) and the block size and channel assignment
+__device__ uint32_t parse_header(const uint8_t* in, uint64_t nbytes, uint64_t p, uint32_t channels, uint32_t bps,
+                                 uint32_t& bs, uint32_t& assign) {
+  if (p + 6 > nbytes) return 0;
+  const uint8_t* h = in + p;
+  if (h[0] != 0xFF || (h[1] & 0xFE) != 0xF8) return 0;
+  const uint32_t bc = h[2] >> 4, rc = h[2] & 15u;
+  assign = h[3] >> 4;
+  const uint32_t sc = (h[3] >> 1) & 7u;
+  if (h[3] & 1u) return 0;
+  if (bc == 0 || rc == 15 || assign > 10 || sc == 3) return 0;
+  const uint32_t sizes[8] = {0, 8, 12, 0, 16, 20, 24, 32};
+  if (sc && sizes[sc] != bps) return 0;
+  if ((assign < 8 ? assign + 1 : 2u) != channels) return 0;
+  uint64_t q = p + 4;
+  // coded number
+  const uint32_t b0 = in[q++];
+  uint32_t more;
+  if (!(b0 & 0x80)) more = 0;
+  else if ((b0 & 0xE0) == 0xC0) more = 1;
+  else if ((b0 & 0xF0) == 0xE0) more = 2;
+  else if ((b0 & 0xF8) == 0xF0) more = 3;
+  else if ((b0 & 0xFC) == 0xF8) more = 4;
+  else if ((b0 & 0xFE) == 0xFC) more = 5;
+  else if (b0 == 0xFE) more = 6;
+  else return 0;
+  if (q + more + 4 > nbytes) return 0;
+  for (uint32_t i = 0; i < more; ++i)
+    if ((in[q++] & 0xC0) != 0x80) return 0;
+  if (bc == 1) bs = 192;
+  else if (bc <= 5) bs = 576u << (bc - 2);
+  else if (bc == 6) bs = (uint32_t)in[q++] + 1;
+  else if (bc == 7) {
+    bs = (((uint32_t)in[q] << 8) | in[q + 1]) + 1;
+    q += 2;
+  } else bs = 256u << (bc - 8);
+  if (rc == 12) q += 1;
+  else if (rc == 13 || rc == 14) q += 2;
+  if (q + 1 > nbytes) return 0;
+  uint8_t c8 = 0;
+  for (uint64_t i = p; i < q; ++i) c8 = crc8_byte(c8, in[i]);
+  if (c8 != in[q]) return 0;
+  return (uint32_t)(q + 1 - p);
+}
+
+__global__ __launch_bounds__(256) void rpp_flac_scan_kernel(FlacDecParams d) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= d.nbytes) return;
+  uint32_t at = 0;
+  if (d.in[p] == 0xFF && p + 1 < d.nbytes && (d.in[p + 1] & 0xFE) == 0xF8) {
+    uint32_t bs, assign;
+    const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign);
+    if (hl && bs <= d.max_bs) {
+      const uint32_t c = atomicAdd(d.ncand, 1u);
+      if (c < d.max_cand) {
+        d.cand_pos[c] = p;
+        d.cand_info[c] = bs;
+        at = c + 1;
+      }
+    }
+  }
+  d.cand_at[p] = at;
+}
+
+// residual of one subframe into s[order..bs)
+__device__ bool decode_residual(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t order) {
+  const uint32_t method = (uint32_t)r.get(2);
+  if (method > 1) return false;
+  const uint32_t pb = method ? 5u : 4u, esc = (1u << pb) - 1;
+  const uint32_t po = (uint32_t)r.get(4);
+  if (bs % (1u << po) || (bs >> po) < order) return false;
+  const uint32_t per = bs >> po;
+  for (uint32_t p = 0; p < (1u << po); ++p) {
+    const uint32_t lo = p == 0 ? order : p * per, hi = (p + 1) * per;
+    const uint32_t k = (uint32_t)r.get(pb);
+    if (k == esc) {
+      const uint32_t n = (uint32_t)r.get(5);
+      for (uint32_t i = lo; i < hi; ++i) s[(uint64_t)i * stride] = r.get_signed(n);
+    } else {
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint64_t q = r.unary();
+        const uint64_t u = (q << k) | r.get(k);
+        s[(uint64_t)i * stride] = (u & 1u) ? -(int64_t)(u >> 1) - 1 : (int64_t)(u >> 1);
+        if (r.err) return false;
+      }
+    }
+    if (r.err) return false;
+  }
+  return true;
+}
+
+// one subframe into s[i * stride], i < bs (int64 working values)
+__device__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t sbps) {
+  if (r.get(1)) return false;
+  const uint32_t type = (uint32_t)r.get(6);
+  uint32_t wasted = 0;
+  if (r.get(1)) wasted = (uint32_t)r.unary() + 1;
+  if (r.err || wasted >= sbps) return false;
+  const uint32_t b = sbps - wasted;
+  if (type == 0) {
+    const int64_t v = r.get_signed(b);
+    for (uint32_t i = 0; i < bs; ++i) s[(uint64_t)i * stride] = v;
+  } else if (type == 1) {
+    for (uint32_t i = 0; i < bs; ++i) s[(uint64_t)i * stride] = r.get_signed(b);
+  } else if (type >= 8 && type <= 12) {
+    const uint32_t order = type - 8;
+    if (order > bs) return false;
+    for (uint32_t i = 0; i < order; ++i) s[(uint64_t)i * stride] = r.get_signed(b);
+    if (!decode_residual(r, s, stride, bs, order)) return false;
+    for (uint32_t i = order; i < bs; ++i) {
+      int64_t* x = s + (uint64_t)i * stride;
+      switch (order) {
+        case 1: *x += x[-(int64_t)stride]; break;
+        case 2: *x += 2 * x[-(int64_t)stride] - x[-2 * (int64_t)stride]; break;
+        case 3: *x += 3 * x[-(int64_t)stride] - 3 * x[-2 * (int64_t)stride] + x[-3 * (int64_t)stride]; break;
+        case 4:
+          *x += 4 * x[-(int64_t)stride] - 6 * x[-2 * (int64_t)stride] + 4 * x[-3 * (int64_t)stride] -
+                x[-4 * (int64_t)stride];
+          break;
+        default: break;
+      }
+    }
+  } else if (type >= 32) {
+    const uint32_t order = type - 31;
+    if (order > bs) return false;
+    for (uint32_t i = 0; i < order; ++i) s[(uint64_t)i * stride] = r.get_signed(b);
+    const uint32_t prec = (uint32_t)r.get(4) + 1;
+    if (prec == 16) return false;
+    const int32_t shift = (int32_t)r.get_signed(5);
+    if (shift < 0) return false;
+    int32_t q[32];
+    for (uint32_t j = 0; j < order; ++j) q[j] = (int32_t)r.get_signed(prec);
+    if (r.err || !decode_residual(r, s, stride, bs, order)) return false;
+    for (uint32_t i = order; i < bs; ++i) {
+      int64_t* x = s + (uint64_t)i * stride;
+      int64_t acc = 0;
+      for (uint32_t j = 0; j < order; ++j) acc += (int64_t)q[j] * x[-(int64_t)(j + 1) * stride];
+      *x += acc >> shift;
+    }
+  } else {
+    return false;
+  }
+  if (r.err) return false;
+  if (wasted)
+    for (uint32_t i = 0; i < bs; ++i) s[(uint64_t)i * stride] = (int64_t)((uint64_t)s[(uint64_t)i * stride] << wasted);
+  return true;
+}
+
+// One lane per candidate: the whole frame into its scratch slot (int32,
+// interleaved, decorrelated); cand_len = bytes before the CRC-16
+__global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d, int64_t* work) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nc = min(*d.ncand, d.max_cand);
+  if (c >= nc) return;
+  d.cand_len[c] = ~0ull;
+  const uint64_t p = d.cand_pos[c];
+  uint32_t bs, assign;
+  const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign);
+  if (!hl) return;
+  const uint32_t C = d.channels;
+  // per-candidate working samples, int64, interleaved [bs][C]
+  int64_t* s = work + (uint64_t)c * d.max_bs * C;
+  BitReader r{d.in + p, d.nbytes - p, 8ull * hl, false};
+  for (uint32_t ch = 0; ch < C; ++ch) {
+    uint32_t sb = d.bps;
+    if ((assign == 8 && ch == 1) || (assign == 9 && ch == 0) || (assign == 10 && ch == 1)) sb = d.bps + 1;
+    if (!decode_subframe(r, s + ch, C, bs, sb)) return;
+  }
+  const uint64_t end = ((r.pos + 7) >> 3);
+  if (end + 2 > d.nbytes - p) return;
+  int32_t* o = d.scratch + (uint64_t)c * d.max_bs * C;
+  for (uint32_t i = 0; i < bs; ++i) {
+    const int64_t* x = s + (uint64_t)i * C;
+    if (assign >= 8) {
+      int64_t L, R;
+      if (assign == 8) L = x[0], R = x[0] - x[1];
+      else if (assign == 9) R = x[1], L = x[0] + x[1];
+      else {
+        const int64_t m = (x[0] * 2) | (x[1] & 1);
+        L = (m + x[1]) >> 1;
+        R = (m - x[1]) >> 1;
+      }
+      o[2 * i] = (int32_t)L;
+      o[2 * i + 1] = (int32_t)R;
+    } else {
+      for (uint32_t ch = 0; ch < C; ++ch) o[(uint64_t)i * C + ch] = (int32_t)x[ch];
+    }
+  }
+  d.cand_len[c] = end;
+}
+
+// One lane: the chain of frames from byte 0
+__global__ void rpp_flac_chain_kernel(FlacDecParams d) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint64_t pos = 0, done = 0;
+  uint32_t n = 0;
+  int32_t st = RPP_OK;
+  while (done < d.nsamples) {
+    if (pos >= d.nbytes) {
+      st = RPP_TRUNCATED_INPUT;
+      break;
+    }
+    const uint32_t at = d.cand_at[pos];
+    if (!at) {
+      st = RPP_INVALID_ARGUMENT;
+      break;
+    }
+    const uint32_t c = at - 1;
+    if (d.cand_len[c] == ~0ull || !d.cand_ok[c]) {
+      st = RPP_INVALID_ARGUMENT;
+      break;
+    }
+    const uint32_t bs = d.cand_info[c];
+    if (done + bs > d.nsamples) {
+      st = RPP_INVALID_ARGUMENT;
+      break;
+    }
+    d.chain[n] = c;
+    d.chain_off[n] = done;
+    ++n;
+    done += bs;
+    pos += d.cand_len[c] + 2;
+  }
+  *d.nchain = n;
+  *d.status = st;
+}
+
+__global__ __launch_bounds__(256) void rpp_flac_place_kernel(FlacDecParams d) {
+  const uint32_t f = blockIdx.x;
+  if (f >= *d.nchain || *d.status != RPP_OK) return;
+  const uint32_t c = d.chain[f];
+  const uint64_t n = (uint64_t)d.cand_info[c] * d.channels;
+  const int32_t* s = d.scratch + (uint64_t)c * d.max_bs * d.channels;
+  int32_t* o = d.out + d.chain_off[f] * d.channels;
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) o[i] = s[i];
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t rpp_flac_frame_bound(uint32_t channels, uint32_t bps) {
+  // header <= 16 bytes; a subframe at most its verbatim size (+1 bit for a
+  // side channel) plus 2 bytes of type / wasted fields; padding; CRC-16
+  return 16 + (uint64_t)channels * (2 + ((uint64_t)(bps + 1) * kFlacBlock + 7) / 8) + 2 + 16;
+}
+
+uint64_t rpp_flac_encode_workspace_bytes(uint64_t nsamples, uint32_t channels, uint32_t bps) {
+  const uint64_t frames = (nsamples + kFlacBlock - 1) / kFlacBlock;
+  const uint64_t slot = (rpp_flac_frame_bound(channels, bps) + 15) & ~15ull;
+  return frames * slot + 3 * 8 * (frames + 1) + 256;
+}
+
+int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint8_t* d_out,
+                    uint64_t* d_total, void* d_workspace, uint64_t workspace_bytes, void* stream) {
+  if (channels < 1 || channels > 8 || bps < 4 || bps > 32) return RPP_UNSUPPORTED_CONFIG;
+  if (!d_total) return RPP_INVALID_ARGUMENT;
+  hipStream_t s = (hipStream_t)stream;
+  if (nsamples == 0) return hipMemsetAsync(d_total, 0, 8, s) == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+  if (!d_samples || !d_out || !d_workspace) return RPP_INVALID_ARGUMENT;
+  if (workspace_bytes < rpp_flac_encode_workspace_bytes(nsamples, channels, bps)) return RPP_INVALID_ARGUMENT;
+  const uint64_t frames = (nsamples + kFlacBlock - 1) / kFlacBlock;
+  if (frames > 0x7FFFFFFFu) return RPP_INVALID_ARGUMENT;
+  const uint64_t slot = (rpp_flac_frame_bound(channels, bps) + 15) & ~15ull;
+  uint8_t* ws = static_cast<uint8_t*>(d_workspace);
+  uint8_t* slots = ws;
+  uint64_t* sizes = reinterpret_cast<uint64_t*>(ws + frames * slot);
+  uint64_t* offs = sizes + frames + 1;
+  uint64_t* lens = offs + frames + 1;
+  FlacEncParams p{d_samples, nsamples, channels, bps, slots, slot, sizes, (uint32_t)frames};
+  const size_t lds = sizeof(EncShared);
+  hipLaunchKernelGGL(rpp_flac_encode_kernel, dim3((uint32_t)frames), dim3(64), lds, s, p);
+  int st = rpp_exclusive_scan_u64(sizes, frames, offs, s);
+  if (st != RPP_OK) return st;
+  hipLaunchKernelGGL(rpp_flac_pack_kernel, dim3((uint32_t)frames), dim3(256), 0, s, slots, slot, sizes, offs, d_out,
+                     (uint32_t)frames);
+  hipLaunchKernelGGL(rpp_flac_lens_kernel, dim3((uint32_t)((frames + 255) / 256)), dim3(256), 0, s, sizes, offs, lens, frames,
+                     d_total);
+  hipLaunchKernelGGL(rpp_flac_crc_kernel, dim3((uint32_t)(frames < 4096 ? frames : 4096)), dim3(64), 0, s, d_out, offs,
+                     lens, (uint32_t)frames, d_out, nullptr, nullptr);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
+uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t max_blocksize,
+                                         uint32_t max_candidates) {
+  const uint64_t mc = max_candidates;
+  const uint64_t per = (uint64_t)max_blocksize * channels;
+  return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 8) + 64 + mc * per * 4 + mc * per * 8 + 256;
+}
+
+int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
+                    uint32_t max_blocksize, uint64_t nsamples, int32_t* d_out, int32_t* d_status,
+                    uint32_t max_candidates, void* d_workspace, uint64_t workspace_bytes, uint32_t* d_ncand,
+                    void* stream) {
+  if (channels < 1 || channels > 8 || bps < 4 || bps > 32 || max_blocksize < 1 || max_blocksize > 65536)
+    return RPP_UNSUPPORTED_CONFIG;
+  if (!d_status || !d_ncand) return RPP_INVALID_ARGUMENT;
+  hipStream_t s = (hipStream_t)stream;
+  if (workspace_bytes < rpp_flac_decode_workspace_bytes(nbytes, channels, max_blocksize, max_candidates))
+    return RPP_INVALID_ARGUMENT;
+  if ((nbytes && !d_frames) || (nsamples && !d_out) || !d_workspace || max_candidates == 0)
+    return RPP_INVALID_ARGUMENT;
+  const uint64_t mc = max_candidates, per = (uint64_t)max_blocksize * channels;
+  uint8_t* ws = static_cast<uint8_t*>(d_workspace);
+  auto take = [&](uint64_t bytes) {
+    uint8_t* q = ws;
+    ws += (bytes + 15) & ~15ull;
+    return q;
+  };
+  FlacDecParams d{};
+  d.in = d_frames;
+  d.nbytes = nbytes;
+  d.channels = channels;
+  d.bps = bps;
+  d.max_bs = max_blocksize;
+  d.nsamples = nsamples;
+  d.cand_at = reinterpret_cast<uint32_t*>(take(4 * (nbytes + 1)));
+  d.cand_pos = reinterpret_cast<uint64_t*>(take(8 * mc));
+  d.cand_info = reinterpret_cast<uint32_t*>(take(4 * mc));
+  d.cand_len = reinterpret_cast<uint64_t*>(take(8 * mc));
+  d.cand_ok = reinterpret_cast<uint32_t*>(take(4 * mc));
+  d.chain = reinterpret_cast<uint32_t*>(take(4 * mc));
+  d.chain_off = reinterpret_cast<uint64_t*>(take(8 * mc));
+  d.nchain = reinterpret_cast<uint32_t*>(take(16));
+  d.scratch = reinterpret_cast<int32_t*>(take(4 * mc * per));
+  int64_t* work = reinterpret_cast<int64_t*>(take(8 * mc * per));
+  d.ncand = d_ncand;
+  d.max_cand = max_candidates;
+  d.out = d_out;
+  d.status = d_status;
+  if (hipMemsetAsync(d_ncand, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
+  if (nbytes) hipLaunchKernelGGL(rpp_flac_scan_kernel, dim3((uint32_t)((nbytes + 255) / 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(rpp_flac_frame_kernel, dim3((uint32_t)((mc + 63) / 64)), dim3(64), 0, s, d, work);
+  hipLaunchKernelGGL(rpp_flac_crc_kernel, dim3((uint32_t)(mc < 4096 ? mc : 4096)), dim3(64), 0, s, d.in, d.cand_pos,
+                     d.cand_len, (uint32_t)mc, nullptr, d.cand_ok, d.ncand);
+  hipLaunchKernelGGL(rpp_flac_chain_kernel, dim3(1), dim3(1), 0, s, d);
+  hipLaunchKernelGGL(rpp_flac_place_kernel, dim3((uint32_t)mc), dim3(256), 0, s, d);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
+}  // extern "C"

@@ -167,4 +167,105 @@ long rpp_parse_frame(const uint8_t* in, size_t in_len, rpp_frame* f) {
   return static_cast<long>(r.p - in);
 }
 
+// ---- FLAC blocks (src/compression/flac.cpp:284-304, :477-484) ----
+// varint(uncompressed bytes) + thrift-compact flac_block_header
+// (thrift/compression.thrift:36-40) + a native FLAC stream.
+
+size_t rpp_flac_frame_header(const rpp_flac_frame* f, uint8_t* out) {
+  size_t n = put_varint(out, f->uncompressed_bytes);
+  out[n++] = 0x14;  // field 1 num_channels: i16
+  n += put_varint(out + n, zz(static_cast<int16_t>(f->num_channels)));
+  out[n++] = 0x13;  // field 2 bits_per_sample: byte
+  out[n++] = static_cast<uint8_t>(f->bits_per_sample);
+  out[n++] = 0x13;  // field 3 flags: byte
+  out[n++] = static_cast<uint8_t>(f->flags);
+  out[n++] = CT_STOP;
+  return n;
+}
+
+long rpp_flac_parse_frame(const uint8_t* in, size_t in_len, rpp_flac_frame* f) {
+  reader r{in, in + in_len};
+  memset(f, 0, sizeof *f);
+  f->uncompressed_bytes = r.varint();
+  int16_t last = 0;
+  for (;;) {
+    uint8_t h = r.u8();
+    if (!r.ok) return RPP_INVALID_ARGUMENT;
+    uint8_t t = h & 0x0f;
+    if (t == CT_STOP) break;
+    uint8_t delta = h >> 4;
+    int16_t id = delta ? static_cast<int16_t>(last + delta) : static_cast<int16_t>(unzz(r.varint()));
+    last = id;
+    uint64_t v = 0;
+    if (t == CT_BYTE) {
+      v = r.u8();
+    } else if (t == CT_I16 || t == CT_I32 || t == CT_I64) {
+      v = static_cast<uint64_t>(unzz(r.varint()));
+    } else {
+      if (!skip(r, t, 0)) return RPP_INVALID_ARGUMENT;
+      continue;
+    }
+    if (!r.ok) return RPP_INVALID_ARGUMENT;
+    switch (id) {
+      case 1: f->num_channels = static_cast<uint16_t>(v); break;
+      case 2: f->bits_per_sample = static_cast<uint8_t>(v); break;
+      case 3: f->flags = static_cast<uint8_t>(v); break;
+      default: break;
+    }
+  }
+  return static_cast<long>(r.p - in);
+}
+
+// "fLaC" + STREAMINFO (RFC 9639 8.2): block sizes 4096, frame sizes unknown,
+// 48 kHz (flac.cpp:311), MD5 unknown (the reference's decoder does not check
+// it: flac.cpp:411)
+size_t rpp_flac_stream_header(uint32_t channels, uint32_t bps, uint64_t nsamples, uint8_t* out) {
+  memset(out, 0, 42);
+  memcpy(out, "fLaC", 4);
+  out[4] = 0x80;  // last metadata block, STREAMINFO
+  out[7] = 34;
+  out[8] = 0x10;  // min block size 4096
+  out[10] = 0x10;  // max block size 4096
+  const uint32_t rate = 48000;
+  out[18] = static_cast<uint8_t>(rate >> 12);
+  out[19] = static_cast<uint8_t>(rate >> 4);
+  out[20] = static_cast<uint8_t>(((rate & 15u) << 4) | (((channels - 1) & 7u) << 1) | (((bps - 1) >> 4) & 1u));
+  out[21] = static_cast<uint8_t>((((bps - 1) & 15u) << 4) | ((nsamples >> 32) & 15u));
+  out[22] = static_cast<uint8_t>(nsamples >> 24);
+  out[23] = static_cast<uint8_t>(nsamples >> 16);
+  out[24] = static_cast<uint8_t>(nsamples >> 8);
+  out[25] = static_cast<uint8_t>(nsamples);
+  return 42;
+}
+
+long rpp_flac_parse_stream(const uint8_t* in, size_t len, rpp_flac_stream_info* info) {
+  memset(info, 0, sizeof *info);
+  if (len < 4 || memcmp(in, "fLaC", 4) != 0) return RPP_INVALID_ARGUMENT;
+  size_t p = 4;
+  bool have_info = false;
+  for (bool last = false; !last;) {
+    if (p + 4 > len) return RPP_TRUNCATED_INPUT;
+    last = (in[p] & 0x80) != 0;
+    const uint32_t type = in[p] & 0x7f;
+    const size_t blen = (static_cast<size_t>(in[p + 1]) << 16) | (static_cast<size_t>(in[p + 2]) << 8) | in[p + 3];
+    p += 4;
+    if (p + blen > len) return RPP_TRUNCATED_INPUT;
+    if (type == 0) {
+      if (blen < 34) return RPP_INVALID_ARGUMENT;
+      const uint8_t* s = in + p;
+      info->min_blocksize = (static_cast<uint32_t>(s[0]) << 8) | s[1];
+      info->max_blocksize = (static_cast<uint32_t>(s[2]) << 8) | s[3];
+      info->sample_rate = (static_cast<uint32_t>(s[10]) << 12) | (static_cast<uint32_t>(s[11]) << 4) | (s[12] >> 4);
+      info->channels = ((s[12] >> 1) & 7u) + 1;
+      info->bits_per_sample = (((s[12] & 1u) << 4) | (s[13] >> 4)) + 1;
+      info->total_samples = (static_cast<uint64_t>(s[13] & 15u) << 32) | (static_cast<uint64_t>(s[14]) << 24) |
+                            (static_cast<uint64_t>(s[15]) << 16) | (static_cast<uint64_t>(s[16]) << 8) | s[17];
+      have_info = true;
+    }
+    p += blen;
+  }
+  if (!have_info) return RPP_INVALID_ARGUMENT;
+  return static_cast<long>(p);
+}
+
 }  // extern "C"

@@ -1814,13 +1814,14 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         if constexpr (RPP_LIST32) {
           // (codes 2c, 2c+1 on lane c (TWO), code c on lane c; aprev: the
           // entry before, the lead word 0 for lane 0)
+          // (aprev from lane c-1's last entry by a DPP move, not an LDS read)
           if constexpr (TWO) {
             const uint2 t2 = list2[lane];
             tt = make_uint4(t2.x, t2.y, 0u, 0u);
-            aprev = list[2 * (int)lane - 1];
+            aprev = from_left(t2.y);
           } else {
             tt = make_uint4(list[lane], 0u, 0u, 0u);
-            aprev = list[(int)lane - 1];
+            aprev = from_left(tt.x);
           }
         } else if constexpr (TWO) {
           tt = list4[lane];

@@ -307,6 +307,68 @@ int rpp_pcm_check_format(const rpp_pcm_format* f);
 int rpp_pcm_unpack(const rpp_pcm_format* f, const uint8_t* d_src, int32_t* d_dst, uint64_t n_samples, void* stream);
 int rpp_pcm_pack(const rpp_pcm_format* f, const int32_t* d_src, uint8_t* d_dst, uint64_t n_samples, void* stream);
 
+/*
+ * FLAC blocks (src/compression/flac.cpp).  Parity unpinned: the reference
+ * codes them with libFLAC (absent here; no FLAC fixture in the reference).
+ *
+ * Framing, host side: varint(uncompressed bytes) + thrift-compact
+ * flac_block_header (thrift/compression.thrift:36-40; written by
+ * flac_block_compressor::compress, flac.cpp:284-304, parsed by
+ * flac_block_decompressor, :477-484) + a native FLAC stream.  flags: bit 7
+ * big endian, bit 6 signed, bit 5 LSB padding, bits 0-1 bytes per sample - 1
+ * (flac.cpp:41-44).  rpp_flac_stream_header writes "fLaC" + STREAMINFO
+ * (42 bytes: 4096-sample blocks, 48 kHz as flac.cpp:311, MD5 unknown);
+ * rpp_flac_parse_stream reads any stream's metadata blocks and returns the
+ * offset of its first frame (or an RPP_* error).
+ */
+typedef struct rpp_flac_frame {
+  uint64_t uncompressed_bytes;
+  uint32_t num_channels;
+  uint32_t bits_per_sample;
+  uint32_t flags;
+} rpp_flac_frame;
+
+typedef struct rpp_flac_stream_info {
+  uint32_t min_blocksize, max_blocksize;
+  uint32_t sample_rate, channels, bits_per_sample;
+  uint64_t total_samples;
+} rpp_flac_stream_info;
+
+size_t rpp_flac_frame_header(const rpp_flac_frame* f, uint8_t* out);
+long rpp_flac_parse_frame(const uint8_t* in, size_t in_len, rpp_flac_frame* f);
+size_t rpp_flac_stream_header(uint32_t channels, uint32_t bps, uint64_t nsamples, uint8_t* out);
+long rpp_flac_parse_stream(const uint8_t* in, size_t len, rpp_flac_stream_info* info);
+
+/*
+ * FLAC frames on the device (replaces the libFLAC stream encoder /
+ * decoder calls of flac.cpp:306-349 and :442-472).
+ *
+ * rpp_flac_encode: nsamples interleaved frames of `channels` int32 samples
+ * of `bps` significant bits (8..32; channels 1..8, flac.cpp:243-245) ->
+ * FLAC frames of 4096 samples (fixed predictors, stereo decorrelation,
+ * partitioned Rice codes, CRC-8 / CRC-16) back to back at d_out
+ * (rpp_flac_frame_bound bytes per frame at most); *d_total = their size.
+ * Workspace: rpp_flac_encode_workspace_bytes.
+ *
+ * rpp_flac_decode: the frames of a stream (after its metadata blocks) ->
+ * nsamples interleaved frames of int32 samples; every RFC 9639 frame kind is
+ * accepted.  Frame starts are found by a sync-code scan: at most
+ * max_candidates of them are kept; *d_ncand receives how many there were
+ * (more than max_candidates: call again with a larger workspace).  *d_status:
+ * RPP_OK, RPP_TRUNCATED_INPUT or RPP_INVALID_ARGUMENT (a frame that does not
+ * parse or fails its CRC).  Workspace: rpp_flac_decode_workspace_bytes.
+ */
+uint64_t rpp_flac_frame_bound(uint32_t channels, uint32_t bps);
+uint64_t rpp_flac_encode_workspace_bytes(uint64_t nsamples, uint32_t channels, uint32_t bps);
+int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint8_t* d_out,
+                    uint64_t* d_total, void* d_workspace, uint64_t workspace_bytes, void* stream);
+uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t max_blocksize,
+                                         uint32_t max_candidates);
+int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
+                    uint32_t max_blocksize, uint64_t nsamples, int32_t* d_out, int32_t* d_status,
+                    uint32_t max_candidates, void* d_workspace, uint64_t workspace_bytes, uint32_t* d_ncand,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

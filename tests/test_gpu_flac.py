@@ -1,0 +1,123 @@
+"""FLAC block codec on the GPU (dwarfs_amd.flac over rpp_flac_encode /
+rpp_flac_decode).  Parity unpinned (libFLAC absent, no FLAC fixture in the
+reference): every GPU stream is decoded by the CPU restatement
+(oracle/flac_oracle.c) as well as by the GPU, and the GPU decoder reads the
+restatement's streams of every subframe kind.  The matrix is the reference's
+own (test/flac_compressor_test.cpp:138-205: endianness x signedness x padding
+x data shapes, compressed below half the input, exact round trip)."""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from dwarfs_amd import flac as FL
+from dwarfs_amd.pcm import PcmSampleEndianness as E, PcmSamplePadding as Pd, PcmSampleSignedness as S
+from dwarfs_amd.pcm import PcmSampleTransformer
+from oracle import flac as F
+from test_flac import DATA_PARAMS, OPTS, sines
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def pcm_bytes(x: np.ndarray, end, sig, pad, nbytes, bits) -> bytes:
+    """make_test_data (flac_compressor_test.cpp:65-81): the samples packed by pcm_sample_transformer."""
+    t = PcmSampleTransformer(end, sig, pad, nbytes, bits)
+    out = torch.empty(x.size * nbytes, dtype=torch.uint8, device=DEV)
+    t.pack(out, torch.from_numpy(x.astype(np.int32)).to(DEV))
+    return out.cpu().numpy().tobytes()
+
+
+def meta(end, sig, pad, channels, nbytes, bits):
+    return json.dumps({"endianness": "big" if end is E.Big else "little",
+                       "signedness": "signed" if sig is S.Signed else "unsigned",
+                       "padding": "msb" if pad is Pd.Msb else "lsb",
+                       "bytes_per_sample": nbytes, "bits_per_sample": bits, "number_of_channels": channels})
+
+
+def test_basic():
+    """TEST(flac_compressor, basic) (flac_compressor_test.cpp:138-158)."""
+    x = sines(2, 1000, 16)
+    data = pcm_bytes(x, E.Little, S.Signed, Pd.Msb, 2, 16)
+    comp = FL.block_compressor("flac").compress(data, meta(E.Little, S.Signed, Pd.Msb, 2, 2, 16))
+    assert len(comp) < len(data) / 2
+    assert FL.decompress(comp) == data
+
+
+@pytest.mark.parametrize("channels,n,nbytes,bits", DATA_PARAMS)
+@pytest.mark.parametrize("end", [E.Big, E.Little])
+@pytest.mark.parametrize("sig", [S.Signed, S.Unsigned])
+@pytest.mark.parametrize("pad", [Pd.Lsb, Pd.Msb])
+def test_combinations(channels, n, nbytes, bits, end, sig, pad):
+    """TEST_P(flac_param, combinations) (flac_compressor_test.cpp:165-196), plus the GPU stream checked by
+    the CPU restatement's decoder."""
+    x = sines(channels, n, bits)
+    data = pcm_bytes(x, end, sig, pad, nbytes, bits)
+    comp = FL.FlacBlockCompressor().compress(data, meta(end, sig, pad, channels, nbytes, bits))
+    assert len(comp) < len(data) / 2
+    d = FL.FlacBlockDecompressor(comp)
+    assert json.loads(d.metadata()) == json.loads(meta(end, sig, pad, channels, nbytes, bits))
+    assert d.decompress() == data
+    # the stream itself, by an independent decoder: the samples as unpacked by the transformer
+    t = PcmSampleTransformer(end, sig, pad, nbytes, bits)
+    want = torch.empty(x.size, dtype=torch.int32, device=DEV)
+    t.unpack(want, torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(DEV))
+    st, y, ch, b = F.decode(d.stream, x.size)
+    assert st == F.OK and (ch, b) == (channels, bits)
+    assert np.array_equal(y, want.cpu().numpy())
+
+
+@pytest.mark.parametrize("name", sorted(OPTS))
+@pytest.mark.parametrize("channels,bits", [(1, 16), (2, 16), (2, 24), (3, 8), (2, 32)])
+def test_gpu_decodes_every_oracle_stream(name, channels, bits):
+    """The restatement's streams -- LPC up to order 32, escape partitions, 5-bit Rice parameters, partition
+    orders 0-8, a PADDING block, variable blocking, verbatim and constant subframes, block sizes that need
+    the 8 / 16-bit size field -- decoded by the GPU."""
+    rng = np.random.default_rng(len(name) * 11 + channels + bits)
+    x = sines(channels, 9000, bits).astype(np.int64)
+    x += rng.integers(-3, 4, x.size)
+    x[::997] = rng.integers(-(1 << (bits - 1)), 1 << (bits - 1), x[::997].size)
+    x = np.clip(x, -(1 << (bits - 1)), (1 << (bits - 1)) - 1).astype(np.int32)
+    nbytes = (bits + 7) // 8
+    for blocksize in (4096, 1152, 200):
+        stream = F.encode(x, channels, bits, blocksize, OPTS[name])
+        block = FL.frame_header(x.size * nbytes, channels, bits, 0x40 | (nbytes - 1)) + stream
+        want = pcm_bytes(x, E.Little, S.Signed, Pd.Msb, nbytes, bits)
+        assert FL.decompress(block) == want, (name, blocksize)
+
+
+def test_gpu_encoder_kinds():
+    """Silence (constant subframes), low bits always zero (wasted bits), one channel constant and one not,
+    a frame of white noise (verbatim), a ragged last frame -- round trip and the oracle's decode."""
+    rng = np.random.default_rng(5)
+    n = 3 * 4096 + 77
+    x = np.zeros((n, 2), np.int64)
+    x[4096:8192, 0] = sines(1, 4096, 16)[:4096].astype(np.int64) << 3
+    x[4096:8192, 1] = 1000
+    x[8192:, 0] = rng.integers(-32768, 32768, n - 8192)
+    x[8192:, 1] = rng.integers(-32768, 32768, n - 8192) & ~7
+    x = x.reshape(-1).astype(np.int32)
+    data = pcm_bytes(x, E.Big, S.Signed, Pd.Msb, 2, 16)
+    comp = FL.FlacBlockCompressor().compress(data, meta(E.Big, S.Signed, Pd.Msb, 2, 2, 16))
+    d = FL.FlacBlockDecompressor(comp)
+    assert d.decompress() == data
+    st, y, _, _ = F.decode(d.stream, x.size)
+    assert st == F.OK and np.array_equal(y, x)
+
+
+def test_empty_block():
+    comp = FL.FlacBlockCompressor().compress(b"", meta(E.Big, S.Signed, Pd.Msb, 2, 2, 16))
+    assert FL.decompress(comp) == b""
+
+
+def test_corrupt_frame_is_an_error():
+    x = sines(2, 20000, 16)
+    data = pcm_bytes(x, E.Little, S.Signed, Pd.Msb, 2, 16)
+    comp = bytearray(FL.FlacBlockCompressor().compress(data, meta(E.Little, S.Signed, Pd.Msb, 2, 2, 16)))
+    comp[len(comp) // 2] ^= 0x04
+    with pytest.raises(RuntimeError, match="FLAC"):
+        FL.decompress(bytes(comp))
+    with pytest.raises(RuntimeError, match="FLAC"):
+        FL.decompress(bytes(comp[: len(comp) - 100]))

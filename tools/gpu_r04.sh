@@ -8,6 +8,12 @@
 #   tests    the GPU test suite
 #   trace    rocprofv3 kernel trace of the bench workload
 #   pmc      PMC passes of the bench workload (tools/gpu_pmc.sh)
+#   f16      facade 16 MiB blocks at 4 / 16 / 32 threads, packed and (LD_LIBRARY_PATH) slot-copy encode
+#   mix      bench.py --workload mix at 32 GiB, 10 steps
+#   mixpmc   PMC passes of the 32 GiB mix (tools/gpu_pmc_mix.sh)
+#   sbl      small-batch decode latency per path (tools/small_batch_latency.py)
+#   paths    bs 16 / 32 decode per path (tools/workloads.py paths)
+#   flac     the FLAC GPU tests, then tools/flac_bench.py
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/r04
@@ -41,6 +47,16 @@ for step in "$@"; do
       rm -rf gpurun_out/prof/trace
       run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --no-cpu ;;
     pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
+    f16)
+      run f16_main 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 4 16 32
+      LD_LIBRARY_PATH=$PWD/dwarfs_amd/lib/nopack run f16_nopack 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 4 16 32 ;;
+    mix) run bench_mix 600 python bench.py --workload mix --mix-gib 32 --steps 10 --warmup 2 ;;
+    mixpmc) run mixpmc 1300 bash tools/gpu_pmc_mix.sh ;;
+    sbl) run sbl 200 python tools/small_batch_latency.py ;;
+    paths) run paths 400 python tools/workloads.py paths ;;
+    flac)
+      run flac_tests 600 python -u -m pytest tests/test_gpu_flac.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
+      run flac_bench 300 python tools/flac_bench.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
