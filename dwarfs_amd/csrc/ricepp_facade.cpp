@@ -27,6 +27,7 @@
 #include <string>
 #include <thread>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 namespace ricepp_amd {
@@ -114,7 +115,9 @@ constexpr size_t kDeviceKeep = size_t{1} << 30;  // (hipFree synchronises: trims
 
 class device_ctx {
  public:
-  explicit device_ctx(int dev) : dev_{dev} {
+  // kind: the pool a context returns to (encode batches, decode batches,
+  // PCM calls), so that a context keeps buffers sized for one use
+  device_ctx(int dev, int kind) : dev_{dev}, kind_{kind} {
     for (uint32_t n = g_ctx_faults.load(); n;)
       if (g_ctx_faults.compare_exchange_weak(n, n - 1)) throw std::runtime_error("hipStreamCreate: injected failure");
     device_guard g{dev_};
@@ -130,6 +133,7 @@ class device_ctx {
   device_ctx& operator=(device_ctx const&) = delete;
 
   int device() const { return dev_; }
+  int kind() const { return kind_; }
   hipStream_t stream() const { return stream_; }
   hipEvent_t event() const { return event_; }
   uint8_t* dev(size_t bytes) { return grow_dev(dbuf_, dcap_, bytes); }
@@ -208,6 +212,7 @@ class device_ctx {
   }
 
   int dev_;
+  int kind_;
   hipStream_t stream_ = nullptr;
   hipEvent_t event_ = nullptr;
   uint8_t* dbuf_ = nullptr;
@@ -228,17 +233,21 @@ class ctx_pool {
     static ctx_pool* p = new ctx_pool;
     return *p;
   }
-  device_ctx* acquire(int dev) {
+  // kind: 0 encode batches, 1 decode batches, 2 other (PCM): encode and
+  // decode size their device and pinned buffers differently, and a context
+  // handed from one to the other regrew them (hipFree / hipHostFree
+  // synchronise the device) -- one pool per kind keeps them grown
+  device_ctx* acquire(int dev, int kind) {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      auto& v = free_[dev];
+      auto& v = free_[{dev, kind}];
       if (!v.empty()) {
         device_ctx* c = v.back();
         v.pop_back();
         return c;
       }
     }
-    return new device_ctx(dev);
+    return new device_ctx(dev, kind);
   }
   // Drains the context's stream (idle in the normal case: a batch ends with
   // its event; after a failed launch it may still hold work) and pools it,
@@ -257,17 +266,17 @@ class ctx_pool {
       return;
     }
     std::lock_guard<std::mutex> lk(mu_);
-    free_[c->device()].push_back(c);
+    free_[{c->device(), c->kind()}].push_back(c);
   }
 
  private:
   std::mutex mu_;
-  std::map<int, std::vector<device_ctx*>> free_;
+  std::map<std::pair<int, int>, std::vector<device_ctx*>> free_;
 };
 
 class ctx_lease {
  public:
-  explicit ctx_lease(int dev) : c_{ctx_pool::get().acquire(dev)} {}
+  explicit ctx_lease(int dev) : c_{ctx_pool::get().acquire(dev, 2)} {}
   ~ctx_lease() { ctx_pool::get().release(c_); }
   ctx_lease(ctx_lease const&) = delete;
   ctx_lease& operator=(ctx_lease const&) = delete;
@@ -434,7 +443,7 @@ class batch_queue {
     device_ctx* c = nullptr;
     auto* b = new batch;
     try {
-      c = ctx_pool::get().acquire(dev_);
+      c = ctx_pool::get().acquire(dev_, encode_ ? 0 : 1);
       const size_t join = need_out(r) > kBatchOut / 4 || need_in(r) > kBatchIn / 4 ? kLargeJoin : 1;
       b->in_cap = std::max(kBatchIn, join * need_in(r) + arrays_in(join));
       b->out_cap = std::max(kBatchOut, join * need_out(r) + arrays_out(join));

@@ -1131,9 +1131,6 @@ constexpr int kParsePrio = 1;
 #ifndef RPP_END_LIST
 #define RPP_END_LIST 1  // the fast loop's sub-block end read back from the list (0: picked by readlane)
 #endif
-#ifndef RPP_LIST32
-#define RPP_LIST32 1  // fast-loop list entries (a_i << fs) | rem_i in one dword (0: (a_i, rem_i) pairs)
-#endif
 
 // fs >= 8: states 0..13 (13 remainder bits still to skip at most).  A state
 // is kept replicated in all four bytes of a dword (a v_perm selector that
@@ -1669,12 +1666,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           // (32-bit segments: the remainder may reach into the next word)
           const uint32_t rem = W32 ? __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(xh, xl, t[j]), 1, fs)
                                    : __builtin_amdgcn_ubfe(xr, t[j], fs);
-#if RPP_LIST32
-          // (one dword per code: a_i < 2^12 and fs <= 13)
-          list[base + j] = lshl_or(abase + t[j] - j * k, fs, rem);
-#else
           list2[base + j] = make_uint2(abase + t[j] - j * k, rem);
-#endif
           lds_fence();
         }
 #if RPP_END_LIST
@@ -1682,11 +1674,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // read back from the list (one broadcast LDS read after the writes,
         // instead of picking the terminator out of the lane that holds it);
         // unused when the sub-block does not end in the window
-#if RPP_LIST32
-        Pe = pe_base + (__builtin_amdgcn_readfirstlane(list[n - 1]) >> fs);
-#else
         Pe = pe_base + __builtin_amdgcn_readfirstlane(list[2 * (n - 1)]);
-#endif
         __builtin_amdgcn_s_setprio(0);
         xln = seg_bits(Pe, xhn);
 #endif
@@ -1700,22 +1688,6 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
       // (aprev: a of the code before this lane's first, read from the list;
       // a_(-1) = 0 lies in the list's lead words)
       auto deltas = [&](uint4 tt, uint32_t aprev, uint32_t fs, uint32_t& d1, uint32_t& dsum) {
-#if RPP_LIST32
-        // entries p_i = (a_i << fs) | rem_i: ((a_i - a_(i-1)) << fs) | rem_i
-        // = p_i - (p_(i-1) & hi), two VOP2 operations per code
-        const uint32_t hi = 0xFFFFFFFFu << fs;
-        if constexpr (TWO) {
-          const uint32_t df0 = tt.x - (aprev & hi), df1 = tt.y - (tt.x & hi);
-          const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
-          d1 = (df1 >> 1) ^ neg_lsb(df1);
-          dsum = d0 + d1;
-        } else {
-          const uint32_t df = tt.x - (aprev & hi);
-          d1 = (df >> 1) ^ neg_lsb(df);
-          dsum = lane < n ? d1 : 0u;
-        }
-        return;
-#endif
         if constexpr (TWO) {
           const uint32_t df0 = lshl_or(tt.x - aprev, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
           const uint32_t d0 = (df0 >> 1) ^ neg_lsb(df0);
@@ -1811,19 +1783,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
         // sub-block s at P (ends at Pn) is parsed, its pairs are in the list
         uint4 tt;
         uint32_t aprev;
-        if constexpr (RPP_LIST32) {
-          // (codes 2c, 2c+1 on lane c (TWO), code c on lane c; aprev: the
-          // entry before, the lead word 0 for lane 0)
-          // (aprev from lane c-1's last entry by a DPP move, not an LDS read)
-          if constexpr (TWO) {
-            const uint2 t2 = list2[lane];
-            tt = make_uint4(t2.x, t2.y, 0u, 0u);
-            aprev = from_left(t2.y);
-          } else {
-            tt = make_uint4(list[lane], 0u, 0u, 0u);
-            aprev = from_left(tt.x);
-          }
-        } else if constexpr (TWO) {
+        if constexpr (TWO) {
           tt = list4[lane];
           aprev = list[4 * lane - 2];
         } else {
@@ -2203,6 +2163,16 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
   if (active && nsb == 0) {
     active = false;
     status = RPP_OK;
+  }
+  // A stream whose first sub-block codes at fs >= 5 goes to the one-wave
+  // kernel (kSegFallback): its fs 5-7 fast loop decodes such data faster than
+  // four rows per wave (configs[4] 16-bit: bs 16 171 vs 156, bs 32 335 vs 292
+  // GiB/s, profiles/r04_paths.jsonl); the rows keep the low-fs streams (10-bit:
+  // 130 vs 112, 242 vs 224), where the one-wave kernel needs its 12-slot class.
+  if (active) {
+    const uint32_t* w0 = word_at(P >> 5);
+    const uint32_t h0 = __builtin_amdgcn_alignbit(w0[1], w0[0], P & 31u) & 15u;
+    if (h0 - 6u <= 8u) active = false;
   }
   uint32_t s = 0;  // the row's sub-block
   ScanRegs sreg;

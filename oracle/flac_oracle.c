@@ -39,6 +39,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -228,6 +229,7 @@ static uint64_t part_bits(const int64_t* r, uint32_t n, int k, unsigned pbits) {
       unsigned w = r[i] ? signed_width(r[i]) : 0;
       if (w > wmax) wmax = w;
     }
+    if (wmax > 31) return ~0ull >> 2; /* the 5-bit width field holds 0..31 */
     return pbits + 5 + (uint64_t)wmax * n;
   }
   uint64_t b = pbits;
@@ -236,9 +238,10 @@ static uint64_t part_bits(const int64_t* r, uint32_t n, int k, unsigned pbits) {
 }
 
 /* residual section for samples [order, bs) of res (res[i] for i >= order);
-   returns bits (write = 0: cost only) */
-static uint64_t code_residual(bw_t* w, const int64_t* res, uint32_t bs, uint32_t order, const fo_opts* o, int write) {
-  const int method = o->rice2 ? 1 : 0;
+   returns bits (write = 0: cost only).  Method 0 (4-bit parameters) unless
+   asked for method 1 or cheaper with it (parameters above 14). */
+static uint64_t code_residual_m(bw_t* w, const int64_t* res, uint32_t bs, uint32_t order, const fo_opts* o, int write,
+                                int method) {
   const unsigned pbits = method ? 5 : 4;
   const int kmax = method ? 30 : 14;
   uint64_t best = ~0ull;
@@ -249,7 +252,7 @@ static uint64_t code_residual(bw_t* w, const int64_t* res, uint32_t bs, uint32_t
     for (uint32_t p = 0; p < (1u << po); ++p) {
       const uint32_t lo = p == 0 ? order : p * (bs >> po), hi = (p + 1) * (bs >> po);
       uint64_t pb = part_bits(res + lo, hi - lo, -1, pbits);
-      if (!o->escape)
+      if (!o->escape || pb >= (~0ull >> 2))
         for (int k = 0; k <= kmax; ++k) {
           const uint64_t b = part_bits(res + lo, hi - lo, k, pbits);
           if (b < pb) pb = b;
@@ -268,7 +271,7 @@ static uint64_t code_residual(bw_t* w, const int64_t* res, uint32_t bs, uint32_t
     const uint32_t lo = p == 0 ? order : p * (bs >> best_po), hi = (p + 1) * (bs >> best_po);
     int bk = -1;
     uint64_t pb = part_bits(res + lo, hi - lo, -1, pbits);
-    if (!o->escape)
+    if (!o->escape || pb >= (~0ull >> 2))
       for (int k = 0; k <= kmax; ++k) {
         const uint64_t b = part_bits(res + lo, hi - lo, k, pbits);
         if (b < pb) {
@@ -295,6 +298,15 @@ static uint64_t code_residual(bw_t* w, const int64_t* res, uint32_t bs, uint32_t
     }
   }
   return best;
+}
+static uint64_t code_residual(bw_t* w, const int64_t* res, uint32_t bs, uint32_t order, const fo_opts* o, int write) {
+  int method = 1;
+  if (!o->rice2) {
+    const uint64_t b0 = code_residual_m(NULL, res, bs, order, o, 0, 0);
+    const uint64_t b1 = code_residual_m(NULL, res, bs, order, o, 0, 1);
+    method = b1 < b0 ? 1 : 0;
+  }
+  return code_residual_m(w, res, bs, order, o, write, method);
 }
 
 static const int64_t fixed_coef[5][4] = {{0, 0, 0, 0}, {1, 0, 0, 0}, {2, -1, 0, 0}, {3, -3, 1, 0}, {4, -6, 4, -1}};
@@ -603,11 +615,16 @@ static int decode_residual(br_t* r, int64_t* res, uint32_t bs, uint32_t order) {
   return FO_OK;
 }
 
+static int fo_trace = 0; /* FO_TRACE=1: one line per subframe on stderr (diagnostics) */
 static int decode_subframe(br_t* r, int64_t* s, uint32_t bs, unsigned sbps) {
+  const uint64_t at = r->pos;
   if (br_get(r, 1)) return FO_BAD_STREAM;
   const unsigned type = (unsigned)br_get(r, 6);
   unsigned wasted = 0;
   if (br_get(r, 1)) wasted = (unsigned)br_unary(r) + 1;
+  if (fo_trace)
+    fprintf(stderr, "  subframe at bit %llu: type %u wasted %u bs %u sbps %u\n", (unsigned long long)at, type, wasted,
+            bs, sbps);
   if (r->err) return r->err;
   if (wasted >= sbps) return FO_BAD_STREAM;
   const unsigned bps = sbps - wasted;
@@ -658,6 +675,7 @@ static int decode_subframe(br_t* r, int64_t* s, uint32_t bs, unsigned sbps) {
 int fo_decode(const uint8_t* in, size_t len, int32_t* out, uint64_t cap, uint32_t* channels_out, uint32_t* bps_out,
               uint64_t* nsamples_out) {
   crc_init();
+  fo_trace = getenv("FO_TRACE") != NULL;
   br_t r = {in, len, 0, 0};
   if (br_get(&r, 32) != 0x664C6143u) return r.err ? r.err : FO_BAD_STREAM;
   uint32_t channels = 0, bps = 0, maxbs = 0;
@@ -738,6 +756,9 @@ int fo_decode(const uint8_t* in, size_t len, int32_t* out, uint64_t cap, uint32_
       err = FO_BAD_STREAM;
       break;
     }
+    if (fo_trace)
+      fprintf(stderr, "frame at byte %llu: bs %u assign %u samples %llu..\n", (unsigned long long)(start >> 3), bs,
+              assign, (unsigned long long)done);
     const uint8_t hcrc = crc8(in + (start >> 3), (size_t)((r.pos - start) >> 3));
     if ((uint8_t)br_get(&r, 8) != hcrc) {
       err = r.err ? r.err : FO_BAD_STREAM;

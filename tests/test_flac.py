@@ -71,7 +71,7 @@ OPTS = {
 
 
 @pytest.mark.parametrize("name", sorted(OPTS))
-@pytest.mark.parametrize("channels,bits", [(1, 16), (2, 16), (2, 24), (3, 8)])
+@pytest.mark.parametrize("channels,bits", [(1, 16), (2, 16), (2, 24), (3, 8), (2, 32)])
 def test_oracle_every_option_round_trips(name, channels, bits):
     rng = np.random.default_rng(len(name) * 7 + channels + bits)
     n = 9000

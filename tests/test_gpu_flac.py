@@ -94,7 +94,7 @@ def test_gpu_encoder_kinds():
     rng = np.random.default_rng(5)
     n = 3 * 4096 + 77
     x = np.zeros((n, 2), np.int64)
-    x[4096:8192, 0] = sines(1, 4096, 16)[:4096].astype(np.int64) << 3
+    x[4096:8192, 0] = sines(1, 4096, 13)[:4096].astype(np.int64) << 3  # (16-bit samples, 3 wasted bits)
     x[4096:8192, 1] = 1000
     x[8192:, 0] = rng.integers(-32768, 32768, n - 8192)
     x[8192:, 1] = rng.integers(-32768, 32768, n - 8192) & ~7
@@ -104,7 +104,18 @@ def test_gpu_encoder_kinds():
     d = FL.FlacBlockDecompressor(comp)
     assert d.decompress() == data
     st, y, _, _ = F.decode(d.stream, x.size)
-    assert st == F.OK and np.array_equal(y, x)
+    assert st == F.OK
+    if not np.array_equal(y, x):
+        bad = np.flatnonzero(y != x)
+        import os
+        import subprocess
+        import sys
+        open("/tmp/flac_kinds.bin", "wb").write(d.stream)
+        trace = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, '.'); from oracle import flac as F; "
+                                "F.decode(open('/tmp/flac_kinds.bin','rb').read(), %d)" % x.size],
+                               env={**os.environ, "FO_TRACE": "1"}, capture_output=True, text=True).stderr
+        raise AssertionError(f"{bad.size} samples differ, first {bad[:8].tolist()}: oracle {y[bad[:8]].tolist()} "
+                             f"want {x[bad[:8]].tolist()}\n{trace[:3000]}")
 
 
 def test_empty_block():

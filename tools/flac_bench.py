@@ -30,7 +30,7 @@ for channels, nbytes, bits in ((2, 2, 16), (8, 4, 24)):
                        "bits_per_sample": bits, "number_of_channels": channels})
     xt = torch.from_numpy(x).to(dev)
     raw = torch.empty(x.size * nbytes, dtype=torch.uint8, device=dev)
-    FL._transformer(nbytes - 1, bits).pack(raw, xt)
+    FL._transformer((nbytes - 1) | FL.FLAG_SIGNED, bits).pack(raw, xt)  # (LE, signed, MSB: the meta above)
     data = raw.cpu().numpy().tobytes()
     comp = FL.FlacBlockCompressor().compress(data, meta)
     assert FL.decompress(comp) == data
