@@ -2164,15 +2164,25 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
     active = false;
     status = RPP_OK;
   }
-  // A stream whose first sub-block codes at fs >= 5 goes to the one-wave
-  // kernel (kSegFallback): its fs 5-7 fast loop decodes such data faster than
-  // four rows per wave (configs[4] 16-bit: bs 16 171 vs 156, bs 32 335 vs 292
-  // GiB/s, profiles/r04_paths.jsonl); the rows keep the low-fs streams (10-bit:
-  // 130 vs 112, 242 vs 224), where the one-wave kernel needs its 12-slot class.
-  if (active) {
-    const uint32_t* w0 = word_at(P >> 5);
-    const uint32_t h0 = __builtin_amdgcn_alignbit(w0[1], w0[0], P & 31u) & 15u;
-    if (h0 - 6u <= 8u) active = false;
+  // Batches whose streams code at fs >= 5 go to the one-wave kernel whole
+  // (every row kSegFallback): its fs 5-7 fast loop decodes such data faster
+  // than four rows per wave (configs[4] 16-bit: bs 16 174 vs 156, bs 32 343 vs
+  // 292 GiB/s, profiles/r04_paths.jsonl); the rows keep low-fs batches (10-bit:
+  // 130 vs 115, 242 vs 228), where the one-wave kernel needs its 12-slot
+  // class.  The choice is the batch's, not the stream's: streams left to the
+  // rows would run before the one-wave launch, not beside it (a per-stream
+  // choice measured 82 GiB/s at bs 16 16-bit).  It is made identically by
+  // every wave from the first headers of 8 streams spread over the batch.
+  {
+    uint32_t votes = 0;
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t sb = (uint32_t)(((uint64_t)p.nblocks * k) / 8);
+      const uint64_t n64 = p.n_samples[sb], off = p.in_off[sb], nb = p.in_bytes[sb];
+      if (n64 < (uint64_t)CS * BS || nb < 2u * CS + 1u) continue;  // (too short to tell)
+      const uint8_t* q = p.in + off + 2u * CS;  // the first header: after the initial values
+      if (((uint32_t)q[0] & 15u) - 6u <= 8u) ++votes;
+    }
+    if (votes >= 5) active = false;
   }
   uint32_t s = 0;  // the row's sub-block
   ScanRegs sreg;

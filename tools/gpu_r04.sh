@@ -8,6 +8,8 @@
 #   tests    the GPU test suite
 #   trace    rocprofv3 kernel trace of the bench workload
 #   pmc      PMC passes of the bench workload (tools/gpu_pmc.sh)
+#   benchcpu the default bench line with its CPU baseline
+#   sweep    configs[4] bs 16 / 32 / 128 x 10-16 bits (tools/workloads.py sweep)
 #   f16      facade 16 MiB blocks at 4 / 16 / 32 threads, packed and (LD_LIBRARY_PATH) slot-copy encode
 #   mix      bench.py --workload mix at 32 GiB, 10 steps
 #   mixpmc   PMC passes of the 32 GiB mix (tools/gpu_pmc_mix.sh)
@@ -33,6 +35,8 @@ for step in "$@"; do
     bench)
       run bench_short 240 python bench.py --no-cpu --steps 20 --warmup 5
       run bench_def 240 python bench.py --no-cpu ;;
+    benchcpu) run bench_cpu 300 python bench.py ;;
+    sweep) run sweep 600 python tools/workloads.py sweep ;;
     variants)
       for v in ${VARIANTS:-}; do
         RICEPP_AMD_LIB=$PWD/dwarfs_amd/lib/libricepp_amd_$v.so run "bench_$v" 240 python bench.py --no-cpu
