@@ -1065,7 +1065,13 @@ uint32_t seg_log2_for(const rpp_config* cfg, uint64_t total_samples, uint64_t ma
   if (path == RPP_DECODE_FUSED) return 0;
   if (path != RPP_DECODE_SEGMENTED) {
     if (max_stream_samples < (1u << 18)) return 0;
-    if (max_stream_samples * 1024 < total_samples) return 0;
+    // the one-wave kernel when the batch is long enough for its longest
+    // stream to finish inside the batch's time: that stream takes ~10.7 ns
+    // per sample on one wave, the batch ~1.6 ps per sample over the whole
+    // chip, and the segmented decode ~3 ps per sample (configs[3]'s 32 GiB
+    // mix of 1/4/16 MiB blocks: one-wave 86 ms, segmented 51 ms,
+    // profiles/r04_bench_mix*.json)
+    if (max_stream_samples * 3072 < total_samples) return 0;
     // bs 256 / 512: a unit's guess parses lane by lane only (2-8 Kib
     // sub-blocks), so units cost several times more; 1 MiB streams decode
     // faster one wave each (16 x 1 MiB at bs 512: 3.8 ms fused, 21 ms split)

@@ -25,20 +25,24 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE", "GRBM_GUI_ACTIVE"):
         continue
     rows = [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    calls = []  # (kind, {kernel: value})
+    # the marker-delimited segments after the checked round trip
+    segs, cur = [], None
     for r in rows:
         name = r["Kernel_Name"]
         if "rpp_" not in name:
             continue
-        short = name.split("(")[0].replace("void ", "").split("<")[0]
-        if "rpp_seg_plan_kernel" in name:
-            calls.append(("decode", collections.Counter()))
-        elif "rpp_enc_units_kernel" in name:
-            calls.append(("encode", collections.Counter()))
-        if calls:
-            calls[-1][1][short] += float(r["Counter_Value"])
+        if "rpp_pcm_unpack_kernel" in name:
+            cur = collections.Counter()
+            segs.append(cur)
+            continue
+        if cur is not None:
+            short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+            cur[short] += float(r["Counter_Value"])
+    segs = [c for c in segs if c]  # (the last marker closes the last call)
+    n_enc = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    calls = [("encode", c) for c in segs[:n_enc]] + [("decode", c) for c in segs[n_enc:]]
     for kind in ("encode", "decode"):
-        cs = [c for k, c in calls if k == kind][1:]
+        cs = [c for k, c in calls if k == kind]
         if not cs:
             continue
         tot = sum(sum(c.values()) for c in cs) / len(cs)
