@@ -356,10 +356,8 @@ constexpr size_t kBatchOut = size_t{16} << 20;
 constexpr size_t kLargeJoin = 8;
 // encode batches whose worst-case output exceeds this go out by a DMA copy of
 // the slots instead of being packed into mapped host memory by a kernel
-#ifndef RPP_FACADE_PACK_MAX
-#define RPP_FACADE_PACK_MAX (~size_t{0})  // (no-pack path under investigation: kept off)
-#endif
-constexpr size_t kPackMax = RPP_FACADE_PACK_MAX;
+// (set_facade_pack_limit changes it for benchmarks; default: always pack)
+std::atomic<size_t> g_pack_max{~size_t{0}};
 // batches of one queue on the device at once (set_facade_pipeline_depth
 // changes it for benchmarks)
 std::atomic<int> g_max_active{2};
@@ -654,7 +652,7 @@ class batch_queue {
           std::fprintf(stderr, "ricepp_amd facade: device copy of req %zu/%zu differs\n", i, nb);
       }
     }
-    b.packed = out_total <= kPackMax;
+    b.packed = out_total <= g_pack_max.load(std::memory_order_relaxed);
     if (b.packed) {
       st = rpp_pack_batch(dslots, d64 + 2 * nb, d64 + 3 * nb, static_cast<uint32_t>(nb), pout_dev, d64 + 4 * nb,
                           d64 + 5 * nb, s);
@@ -919,6 +917,7 @@ void inject_context_failures(uint32_t n) { g_ctx_faults.store(n); }
 void inject_launch_failures(uint32_t n) { g_launch_faults.store(n); }
 
 void set_facade_pipeline_depth(int batches) { g_max_active.store(std::max(1, std::min(batches, 16))); }
+void set_facade_pack_limit(size_t bytes) { g_pack_max.store(bytes); }
 
 facade_stats get_facade_stats() {
   return facade_stats{g_enc_launches.load(), g_enc_blocks.load(), g_dec_launches.load(), g_dec_blocks.load(),

@@ -202,5 +202,9 @@ void inject_launch_failures(uint32_t n);
 // launches on different streams overlap on the device, more do not; clamped
 // to 1..16).
 void set_facade_pipeline_depth(int batches);
+// Benchmarks: encode batches whose worst-case output exceeds `bytes` go to
+// the host by one DMA copy of their slots instead of being packed into mapped
+// host memory by a kernel (default: always packed).
+void set_facade_pack_limit(size_t bytes);
 
 }  // namespace ricepp_amd

@@ -382,6 +382,8 @@ int bench(int argc, char** argv) {
   for (int i = 3; i < argc; ++i) {
     if (std::string(argv[i]).rfind("--kib=", 0) == 0) kib = std::strtoul(argv[i] + 6, nullptr, 10);
     else if (std::string(argv[i]).rfind("--depth=", 0) == 0) depth = std::atoi(argv[i] + 8);
+    else if (std::string(argv[i]).rfind("--pack-max-mib=", 0) == 0)
+      ricepp_amd::set_facade_pack_limit(std::strtoull(argv[i] + 15, nullptr, 10) << 20);
     else threads.push_back(std::atoi(argv[i]));
   }
   if (threads.empty()) threads = {1, 8, 64};

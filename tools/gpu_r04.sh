@@ -10,7 +10,7 @@
 #   pmc      PMC passes of the bench workload (tools/gpu_pmc.sh)
 #   benchcpu the default bench line with its CPU baseline
 #   sweep    configs[4] bs 16 / 32 / 128 x 10-16 bits (tools/workloads.py sweep)
-#   f16      facade 16 MiB blocks at 4 / 16 / 32 threads, packed and (LD_LIBRARY_PATH) slot-copy encode
+#   f16      facade 16 MiB blocks at 8 / 16 / 32 threads: packed / slot-copy encode, 2 / 1 batches in flight
 #   mix      bench.py --workload mix at 32 GiB, 10 steps
 #   mixpmc   PMC passes of the 32 GiB mix (tools/gpu_pmc_mix.sh)
 #   sbl      small-batch decode latency per path (tools/small_batch_latency.py)
@@ -52,8 +52,10 @@ for step in "$@"; do
       run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --no-cpu ;;
     pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
     f16)
-      run f16_main 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 4 16 32
-      LD_LIBRARY_PATH=$PWD/dwarfs_amd/lib/nopack run f16_nopack 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 4 16 32 ;;
+      run f16_main 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 8 16 32
+      run f16_nopack 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 --pack-max-mib=16 8 16 32
+      run f16_d1 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 --depth=1 8 16 32
+      run f16_nopack_d1 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 --pack-max-mib=16 --depth=1 8 16 32 ;;
     mix) run bench_mix 600 python bench.py --workload mix --mix-gib 32 --steps 10 --warmup 2 ;;
     mixpmc) run mixpmc 1300 bash tools/gpu_pmc_mix.sh ;;
     sbl) run sbl 200 python tools/small_batch_latency.py ;;
