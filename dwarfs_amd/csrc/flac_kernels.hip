@@ -587,29 +587,43 @@ struct FlacDecParams {
 };
 
 // MSB-first bit reader over global memory
+// (a 64-bit window of the stream, MSB-aligned: w holds the wbits bits from
+// bit position pos on; refilled a byte at a time up to 57+ bits, so one
+// code costs a clz and shifts instead of a loop over bytes; bytes past the
+// end read as zero and consuming them sets err)
 struct BitReader {
   const uint8_t* p;
   uint64_t len;  // bytes readable
-  uint64_t pos;  // bit position
+  uint64_t pos;  // bit position of w's top bit
   bool err;
-  __device__ uint64_t get(uint32_t n) {
+  uint64_t w = 0;
+  uint32_t wbits = 0;
+  uint64_t next = 0;  // next byte to load (pos + wbits == 8 next)
+  __device__ BitReader(const uint8_t* p_, uint64_t len_, uint64_t bitpos)
+      : p{p_}, len{len_}, pos{bitpos & ~7ull}, err{false}, next{bitpos >> 3} {
+    fill();
+    skip((uint32_t)(bitpos & 7));
+  }
+  __device__ void fill() {
+    while (wbits <= 56) {
+      const uint64_t b = next < len ? p[next] : 0u;
+      w |= b << (56 - wbits);
+      wbits += 8;
+      ++next;
+    }
+  }
+  __device__ void skip(uint32_t n) {  // n <= wbits
+    w = n >= 64 ? 0 : w << n;
+    wbits -= n;
+    pos += n;
+    if (pos > 8 * len) err = true;
+  }
+  __device__ uint64_t get(uint32_t n) {  // n <= 56
     if (n == 0) return 0;
-    if (pos + n > 8 * len) {
-      err = true;
-      pos = 8 * len;
-      return 0;
-    }
-    uint64_t v = 0;
-    uint32_t left = n;
-    while (left) {
-      const uint32_t bi = (uint32_t)(pos & 7);
-      const uint32_t take = min(left, 8u - bi);
-      const uint32_t byte = p[pos >> 3];
-      v = (v << take) | ((byte >> (8 - bi - take)) & ((1u << take) - 1));
-      pos += take;
-      left -= take;
-    }
-    return v;
+    fill();
+    const uint64_t v = w >> (64 - n);
+    skip(n);
+    return err ? 0 : v;
   }
   __device__ int64_t get_signed(uint32_t n) {
     if (n == 0) return 0;
@@ -620,19 +634,15 @@ struct BitReader {
   __device__ uint64_t unary() {
     uint64_t q = 0;
     for (;;) {
-      if (pos >= 8 * len) {
-        err = true;
-        return q;
-      }
-      const uint32_t bi = (uint32_t)(pos & 7);
-      const uint32_t rest = ((uint32_t)p[pos >> 3] << bi) & 0xFFu;  // remaining bits at the top
-      if (rest) {
-        const uint32_t z = (uint32_t)__builtin_clz(rest) - 24;
-        pos += z + 1;
+      fill();
+      if (w != 0) {
+        const uint32_t z = (uint32_t)__builtin_clzll(w);  // < wbits: w's bits past wbits are zero
+        skip(z + 1);
         return q + z;
       }
-      q += 8 - bi;
-      pos += 8 - bi;
+      q += wbits;
+      skip(wbits);
+      if (err) return q;
     }
   }
 };
@@ -800,7 +810,7 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d, int
   const uint32_t C = d.channels;
   // per-candidate working samples, int64, interleaved [bs][C]
   int64_t* s = work + (uint64_t)c * d.max_bs * C;
-  BitReader r{d.in + p, d.nbytes - p, 8ull * hl, false};
+  BitReader r(d.in + p, d.nbytes - p, 8ull * hl);
   for (uint32_t ch = 0; ch < C; ++ch) {
     uint32_t sb = d.bps;
     if ((assign == 8 && ch == 1) || (assign == 9 && ch == 0) || (assign == 10 && ch == 1)) sb = d.bps + 1;
