@@ -712,8 +712,10 @@ __global__ __launch_bounds__(256) void rpp_flac_scan_kernel(FlacDecParams d) {
   d.cand_at[p] = at;
 }
 
-// residual of one subframe into s[order..bs)
-__device__ bool decode_residual(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t order) {
+// The residual section of a subframe, each residual handed to emit(i, r)
+// in sample order (i in [order, bs))
+template <class Emit>
+__device__ bool decode_residual(BitReader& r, uint32_t bs, uint32_t order, Emit&& emit) {
   const uint32_t method = (uint32_t)r.get(2);
   if (method > 1) return false;
   const uint32_t pb = method ? 5u : 4u, esc = (1u << pb) - 1;
@@ -725,12 +727,12 @@ __device__ bool decode_residual(BitReader& r, int64_t* s, uint32_t stride, uint3
     const uint32_t k = (uint32_t)r.get(pb);
     if (k == esc) {
       const uint32_t n = (uint32_t)r.get(5);
-      for (uint32_t i = lo; i < hi; ++i) s[(uint64_t)i * stride] = r.get_signed(n);
+      for (uint32_t i = lo; i < hi; ++i) emit(i, r.get_signed(n));
     } else {
       for (uint32_t i = lo; i < hi; ++i) {
         const uint64_t q = r.unary();
         const uint64_t u = (q << k) | r.get(k);
-        s[(uint64_t)i * stride] = (u & 1u) ? -(int64_t)(u >> 1) - 1 : (int64_t)(u >> 1);
+        emit(i, (u & 1u) ? -(int64_t)(u >> 1) - 1 : (int64_t)(u >> 1));
         if (r.err) return false;
       }
     }
@@ -739,66 +741,78 @@ __device__ bool decode_residual(BitReader& r, int64_t* s, uint32_t stride, uint3
   return true;
 }
 
-// one subframe into s[i * stride], i < bs (int64 working values)
-__device__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t sbps) {
+// One subframe into s[i * stride], i < bs (int64).  The prediction runs on
+// values held in registers (fixed) or in this lane's LDS ring (LPC), never on
+// the stores, so a sample costs no dependent global-memory round trip.
+__device__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t sbps, int64_t* ring,
+                                int32_t* coef) {
   if (r.get(1)) return false;
   const uint32_t type = (uint32_t)r.get(6);
   uint32_t wasted = 0;
   if (r.get(1)) wasted = (uint32_t)r.unary() + 1;
   if (r.err || wasted >= sbps) return false;
   const uint32_t b = sbps - wasted;
+  auto put = [&](uint32_t i, int64_t v) { s[(uint64_t)i * stride] = (int64_t)((uint64_t)v << wasted); };
   if (type == 0) {
     const int64_t v = r.get_signed(b);
-    for (uint32_t i = 0; i < bs; ++i) s[(uint64_t)i * stride] = v;
+    for (uint32_t i = 0; i < bs; ++i) put(i, v);
   } else if (type == 1) {
-    for (uint32_t i = 0; i < bs; ++i) s[(uint64_t)i * stride] = r.get_signed(b);
+    for (uint32_t i = 0; i < bs; ++i) put(i, r.get_signed(b));
   } else if (type >= 8 && type <= 12) {
     const uint32_t order = type - 8;
     if (order > bs) return false;
-    for (uint32_t i = 0; i < order; ++i) s[(uint64_t)i * stride] = r.get_signed(b);
-    if (!decode_residual(r, s, stride, bs, order)) return false;
-    for (uint32_t i = order; i < bs; ++i) {
-      int64_t* x = s + (uint64_t)i * stride;
-      switch (order) {
-        case 1: *x += x[-(int64_t)stride]; break;
-        case 2: *x += 2 * x[-(int64_t)stride] - x[-2 * (int64_t)stride]; break;
-        case 3: *x += 3 * x[-(int64_t)stride] - 3 * x[-2 * (int64_t)stride] + x[-3 * (int64_t)stride]; break;
-        case 4:
-          *x += 4 * x[-(int64_t)stride] - 6 * x[-2 * (int64_t)stride] + 4 * x[-3 * (int64_t)stride] -
-                x[-4 * (int64_t)stride];
-          break;
-        default: break;
-      }
+    int64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;  // the last four samples, newest first
+    for (uint32_t i = 0; i < order; ++i) {
+      const int64_t v = r.get_signed(b);
+      put(i, v);
+      h3 = h2, h2 = h1, h1 = h0, h0 = v;
     }
+    const bool ok = decode_residual(r, bs, order, [&](uint32_t i, int64_t res) {
+      int64_t v;
+      switch (order) {
+        case 0: v = res; break;
+        case 1: v = res + h0; break;
+        case 2: v = res + 2 * h0 - h1; break;
+        case 3: v = res + 3 * h0 - 3 * h1 + h2; break;
+        default: v = res + 4 * h0 - 6 * h1 + 4 * h2 - h3; break;
+      }
+      put(i, v);
+      h3 = h2, h2 = h1, h1 = h0, h0 = v;
+    });
+    if (!ok) return false;
   } else if (type >= 32) {
     const uint32_t order = type - 31;
     if (order > bs) return false;
-    for (uint32_t i = 0; i < order; ++i) s[(uint64_t)i * stride] = r.get_signed(b);
+    for (uint32_t i = 0; i < order; ++i) {
+      const int64_t v = r.get_signed(b);
+      put(i, v);
+      ring[i & 31u] = v;
+    }
     const uint32_t prec = (uint32_t)r.get(4) + 1;
     if (prec == 16) return false;
     const int32_t shift = (int32_t)r.get_signed(5);
     if (shift < 0) return false;
-    int32_t q[32];
-    for (uint32_t j = 0; j < order; ++j) q[j] = (int32_t)r.get_signed(prec);
-    if (r.err || !decode_residual(r, s, stride, bs, order)) return false;
-    for (uint32_t i = order; i < bs; ++i) {
-      int64_t* x = s + (uint64_t)i * stride;
+    for (uint32_t j = 0; j < order; ++j) coef[j] = (int32_t)r.get_signed(prec);
+    if (r.err) return false;
+    const bool ok = decode_residual(r, bs, order, [&](uint32_t i, int64_t res) {
       int64_t acc = 0;
-      for (uint32_t j = 0; j < order; ++j) acc += (int64_t)q[j] * x[-(int64_t)(j + 1) * stride];
-      *x += acc >> shift;
-    }
+      for (uint32_t j = 0; j < order; ++j) acc += (int64_t)coef[j] * ring[(i - 1 - j) & 31u];
+      const int64_t v = res + (acc >> shift);
+      put(i, v);
+      ring[i & 31u] = v;
+    });
+    if (!ok) return false;
   } else {
     return false;
   }
-  if (r.err) return false;
-  if (wasted)
-    for (uint32_t i = 0; i < bs; ++i) s[(uint64_t)i * stride] = (int64_t)((uint64_t)s[(uint64_t)i * stride] << wasted);
-  return true;
+  return !r.err;
 }
 
 // One lane per candidate: the whole frame into its scratch slot (int32,
 // interleaved, decorrelated); cand_len = bytes before the CRC-16
 __global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d, int64_t* work) {
+  __shared__ int64_t rings[64][32];  // each lane's last 32 samples (LPC)
+  __shared__ int32_t coefs[64][32];  // each lane's LPC coefficients
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nc = min(*d.ncand, d.max_cand);
   if (c >= nc) return;
@@ -814,7 +828,7 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d, int
   for (uint32_t ch = 0; ch < C; ++ch) {
     uint32_t sb = d.bps;
     if ((assign == 8 && ch == 1) || (assign == 9 && ch == 0) || (assign == 10 && ch == 1)) sb = d.bps + 1;
-    if (!decode_subframe(r, s + ch, C, bs, sb)) return;
+    if (!decode_subframe(r, s + ch, C, bs, sb, rings[threadIdx.x], coefs[threadIdx.x])) return;
   }
   const uint64_t end = ((r.pos + 7) >> 3);
   if (end + 2 > d.nbytes - p) return;
