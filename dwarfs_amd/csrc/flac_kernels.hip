@@ -604,12 +604,21 @@ struct BitReader {
     fill();
     skip((uint32_t)(bitpos & 7));
   }
+  // at least 33 bits in w afterwards; whole aligned dwords where it can
+  // (one load per 4 bytes: a lane's loads are a dependent chain)
   __device__ void fill() {
-    while (wbits <= 56) {
-      const uint64_t b = next < len ? p[next] : 0u;
-      w |= b << (56 - wbits);
-      wbits += 8;
-      ++next;
+    while (wbits <= 32) {
+      uint32_t v, nb;
+      if ((((uintptr_t)(p + next)) & 3u) == 0 && next + 4 <= len) {
+        v = __builtin_bswap32(*reinterpret_cast<const uint32_t*>(p + next));
+        nb = 4;
+      } else {
+        v = (next < len ? (uint32_t)p[next] : 0u) << 24;
+        nb = 1;
+      }
+      w |= (uint64_t)v << (32 - wbits);
+      wbits += 8 * nb;
+      next += nb;
     }
   }
   __device__ void skip(uint32_t n) {  // n <= wbits
@@ -618,7 +627,7 @@ struct BitReader {
     pos += n;
     if (pos > 8 * len) err = true;
   }
-  __device__ uint64_t get(uint32_t n) {  // n <= 56
+  __device__ uint64_t get(uint32_t n) {  // n <= 33
     if (n == 0) return 0;
     fill();
     const uint64_t v = w >> (64 - n);
