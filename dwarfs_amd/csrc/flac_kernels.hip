@@ -753,6 +753,8 @@ __device__ bool decode_residual(BitReader& r, uint32_t bs, uint32_t order, Emit&
 // One subframe into s[i * stride], i < bs (int64).  The prediction runs on
 // values held in registers (fixed) or in this lane's LDS ring (LPC), never on
 // the stores, so a sample costs no dependent global-memory round trip.
+// (ring / coef: this lane's column of [32][64] LDS arrays, element j at
+// [j * 64]: lanes on distinct banks)
 __device__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t sbps, int64_t* ring,
                                 int32_t* coef) {
   if (r.get(1)) return false;
@@ -795,20 +797,20 @@ __device__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint3
     for (uint32_t i = 0; i < order; ++i) {
       const int64_t v = r.get_signed(b);
       put(i, v);
-      ring[i & 31u] = v;
+      ring[(i & 31u) * 64] = v;
     }
     const uint32_t prec = (uint32_t)r.get(4) + 1;
     if (prec == 16) return false;
     const int32_t shift = (int32_t)r.get_signed(5);
     if (shift < 0) return false;
-    for (uint32_t j = 0; j < order; ++j) coef[j] = (int32_t)r.get_signed(prec);
+    for (uint32_t j = 0; j < order; ++j) coef[j * 64] = (int32_t)r.get_signed(prec);
     if (r.err) return false;
     const bool ok = decode_residual(r, bs, order, [&](uint32_t i, int64_t res) {
       int64_t acc = 0;
-      for (uint32_t j = 0; j < order; ++j) acc += (int64_t)coef[j] * ring[(i - 1 - j) & 31u];
+      for (uint32_t j = 0; j < order; ++j) acc += (int64_t)coef[j * 64] * ring[((i - 1 - j) & 31u) * 64];
       const int64_t v = res + (acc >> shift);
       put(i, v);
-      ring[i & 31u] = v;
+      ring[(i & 31u) * 64] = v;
     });
     if (!ok) return false;
   } else {
@@ -820,8 +822,8 @@ __device__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint3
 // One lane per candidate: the whole frame into its scratch slot (int32,
 // interleaved, decorrelated); cand_len = bytes before the CRC-16
 __global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d, int64_t* work) {
-  __shared__ int64_t rings[64][32];  // each lane's last 32 samples (LPC)
-  __shared__ int32_t coefs[64][32];  // each lane's LPC coefficients
+  __shared__ int64_t rings[32][64];  // each lane's last 32 samples (LPC), lane-minor
+  __shared__ int32_t coefs[32][64];  // each lane's LPC coefficients
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nc = min(*d.ncand, d.max_cand);
   if (c >= nc) return;
@@ -837,7 +839,7 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d, int
   for (uint32_t ch = 0; ch < C; ++ch) {
     uint32_t sb = d.bps;
     if ((assign == 8 && ch == 1) || (assign == 9 && ch == 0) || (assign == 10 && ch == 1)) sb = d.bps + 1;
-    if (!decode_subframe(r, s + ch, C, bs, sb, rings[threadIdx.x], coefs[threadIdx.x])) return;
+    if (!decode_subframe(r, s + ch, C, bs, sb, &rings[0][threadIdx.x], &coefs[0][threadIdx.x])) return;
   }
   const uint64_t end = ((r.pos + 7) >> 3);
   if (end + 2 > d.nbytes - p) return;
