@@ -724,7 +724,7 @@ __global__ __launch_bounds__(256) void rpp_flac_scan_kernel(FlacDecParams d) {
 // The residual section of a subframe, each residual handed to emit(i, r)
 // in sample order (i in [order, bs))
 template <class Emit>
-__device__ bool decode_residual(BitReader& r, uint32_t bs, uint32_t order, Emit&& emit) {
+__device__ __forceinline__ bool decode_residual(BitReader& r, uint32_t bs, uint32_t order, Emit&& emit) {
   const uint32_t method = (uint32_t)r.get(2);
   if (method > 1) return false;
   const uint32_t pb = method ? 5u : 4u, esc = (1u << pb) - 1;
@@ -755,7 +755,7 @@ __device__ bool decode_residual(BitReader& r, uint32_t bs, uint32_t order, Emit&
 // the stores, so a sample costs no dependent global-memory round trip.
 // (ring / coef: this lane's column of [32][64] LDS arrays, element j at
 // [j * 64]: lanes on distinct banks)
-__device__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t sbps, int64_t* ring,
+__device__ __forceinline__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t sbps, int64_t* ring,
                                 int32_t* coef) {
   if (r.get(1)) return false;
   const uint32_t type = (uint32_t)r.get(6);
