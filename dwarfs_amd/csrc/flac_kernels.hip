@@ -45,6 +45,7 @@ constexpr uint32_t kWave = 64;
 constexpr uint32_t kSpl = kFlacBlock / kWave;  // samples per lane
 constexpr uint32_t kMaxPo = 5;          // partition orders 0..5 (libFLAC level 5: -r 5)
 constexpr uint32_t kWinWords = 4352;    // LDS bit window: one subframe (4096 x 33 bits) + slack
+constexpr uint32_t kFlacWaveLds = 144 * 1024;  // dynamic LDS cap of the wave decoder
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
@@ -576,9 +577,11 @@ struct FlacDecParams {
   uint32_t* cand_info; // [max_cand] block size
   uint64_t* cand_len;  // [max_cand] bytes before the CRC-16 (~0: did not parse)
   uint32_t* cand_ok;   // [max_cand] CRC-16 matches
+  uint32_t* cand_redo; // [max_cand] left to the lane decoder by the wave decoder
+  uint32_t redo_only;  // lane decoder: only the candidates marked in cand_redo
   uint32_t* ncand;     // candidates found
   uint32_t max_cand;
-  int32_t* scratch;    // [max_cand][max_bs * channels]
+  void* scratch;       // [max_cand][channels][max_bs] int32 (int64 for 32-bit samples)
   uint32_t* chain;     // [frames] candidate of chained frame i
   uint64_t* chain_off; // [frames] first sample of chained frame i
   uint32_t* nchain;
@@ -750,20 +753,45 @@ __device__ __forceinline__ bool decode_residual(BitReader& r, uint32_t bs, uint3
   return true;
 }
 
-// One subframe into s[i * stride], i < bs (int64).  The prediction runs on
-// values held in registers (fixed) or in this lane's LDS ring (LPC), never on
-// the stores, so a sample costs no dependent global-memory round trip.
-// (ring / coef: this lane's column of [32][64] LDS arrays, element j at
+// A lane's staged samples stg[j * 64], j < n, to dst[j]: 16-byte stores when
+// the chunk is whole and aligned
+template <class T>
+__device__ __forceinline__ void flush_stage(T* dst, const T* stg, uint32_t n) {
+  if (n == 64 && (((uintptr_t)dst) & 15u) == 0) {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (uint32_t j = 0; j < 64; j += 4)
+        *reinterpret_cast<int4*>(dst + j) = make_int4(stg[j * 64], stg[(j + 1) * 64], stg[(j + 2) * 64], stg[(j + 3) * 64]);
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < 64; j += 2)
+        *reinterpret_cast<longlong2*>(dst + j) = make_longlong2(stg[j * 64], stg[(j + 1) * 64]);
+    }
+  } else {
+    for (uint32_t j = 0; j < n; ++j) dst[j] = stg[j * 64];
+  }
+}
+
+// One subframe into dst[i], i < bs.  The prediction runs on values held in
+// registers (fixed) or in this lane's LDS ring (LPC), and samples go to a
+// 64-sample LDS stage flushed with vector stores: on gfx950 one counter
+// orders a lane's global loads and stores, so a store per sample would make
+// every bit-reader refill wait for the previous sample's write to land.
+// (ring / coef / stg: this lane's column of [n][64] LDS arrays, element j at
 // [j * 64]: lanes on distinct banks)
-__device__ __forceinline__ bool decode_subframe(BitReader& r, int64_t* s, uint32_t stride, uint32_t bs, uint32_t sbps, int64_t* ring,
-                                int32_t* coef) {
+template <class T>
+__device__ __forceinline__ bool decode_subframe(BitReader& r, T* dst, uint32_t bs, uint32_t sbps, int64_t* ring,
+                                                int32_t* coef, T* stg) {
   if (r.get(1)) return false;
   const uint32_t type = (uint32_t)r.get(6);
   uint32_t wasted = 0;
   if (r.get(1)) wasted = (uint32_t)r.unary() + 1;
   if (r.err || wasted >= sbps) return false;
   const uint32_t b = sbps - wasted;
-  auto put = [&](uint32_t i, int64_t v) { s[(uint64_t)i * stride] = (int64_t)((uint64_t)v << wasted); };
+  auto put = [&](uint32_t i, int64_t v) {
+    stg[(i & 63u) * 64] = (T)((uint64_t)v << wasted);
+    if ((i & 63u) == 63u || i + 1 == bs) flush_stage(dst + (i & ~63u), stg, (i & 63u) + 1);
+  };
   if (type == 0) {
     const int64_t v = r.get_signed(b);
     for (uint32_t i = 0; i < bs; ++i) put(i, v);
@@ -819,49 +847,389 @@ __device__ __forceinline__ bool decode_subframe(BitReader& r, int64_t* s, uint32
   return !r.err;
 }
 
-// One lane per candidate: the whole frame into its scratch slot (int32,
-// interleaved, decorrelated); cand_len = bytes before the CRC-16
-__global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d, int64_t* work) {
+// The lane decoder (rpp_flac_frame_kernel): one lane per candidate, each subframe into the candidate's scratch slot,
+// planar [channel][max_bs] (T: int32, or int64 for 32-bit samples, whose side
+// channel has 33 bits); cand_len = bytes before the CRC-16.  Inter-channel
+// decorrelation and interleaving are left to rpp_flac_place_kernel.
+template <class T>
+__global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d) {
   __shared__ int64_t rings[32][64];  // each lane's last 32 samples (LPC), lane-minor
   __shared__ int32_t coefs[32][64];  // each lane's LPC coefficients
+  __shared__ T stage[64][64];        // each lane's next 64 output samples
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nc = min(*d.ncand, d.max_cand);
-  if (c >= nc) return;
+  if (c >= nc || (d.redo_only && !d.cand_redo[c])) return;
   d.cand_len[c] = ~0ull;
   const uint64_t p = d.cand_pos[c];
   uint32_t bs, assign;
   const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign);
   if (!hl) return;
   const uint32_t C = d.channels;
-  // per-candidate working samples, int64, interleaved [bs][C]
-  int64_t* s = work + (uint64_t)c * d.max_bs * C;
+  T* s = static_cast<T*>(d.scratch) + (uint64_t)c * d.max_bs * C;
   BitReader r(d.in + p, d.nbytes - p, 8ull * hl);
   for (uint32_t ch = 0; ch < C; ++ch) {
     uint32_t sb = d.bps;
     if ((assign == 8 && ch == 1) || (assign == 9 && ch == 0) || (assign == 10 && ch == 1)) sb = d.bps + 1;
-    if (!decode_subframe(r, s + ch, C, bs, sb, &rings[0][threadIdx.x], &coefs[0][threadIdx.x])) return;
+    if (!decode_subframe(r, s + (uint64_t)ch * d.max_bs, bs, sb, &rings[0][threadIdx.x], &coefs[0][threadIdx.x],
+                         &stage[0][threadIdx.x]))
+      return;
   }
   const uint64_t end = ((r.pos + 7) >> 3);
   if (end + 2 > d.nbytes - p) return;
-  int32_t* o = d.scratch + (uint64_t)c * d.max_bs * C;
-  for (uint32_t i = 0; i < bs; ++i) {
-    const int64_t* x = s + (uint64_t)i * C;
-    if (assign >= 8) {
-      int64_t L, R;
-      if (assign == 8) L = x[0], R = x[0] - x[1];
-      else if (assign == 9) R = x[1], L = x[0] + x[1];
-      else {
-        const int64_t m = (x[0] * 2) | (x[1] & 1);
-        L = (m + x[1]) >> 1;
-        R = (m - x[1]) >> 1;
+  d.cand_len[c] = end;
+}
+
+// ---- the wave decoder: one wave per candidate frame ----
+// The frame's bits pass through an LDS window of kFWin big-endian words.  A
+// Rice partition (n codes, parameter k) is decoded by all 64 lanes at once:
+// lane l takes the 32-bit segment l words after the partition's current
+// position and parses it speculatively from its first bit; a lane's true
+// entry is the previous lane's exit, so the lanes re-parse until every entry
+// agrees (a parse that already visited the true entry needs no re-parse:
+// parses that meet continue identically), which Rice codes reach within a
+// few codes.  A wave prefix sum over the lanes' code counts then gives each
+// code its sample index.  Residuals, warm-up and verbatim samples go to LDS
+// ([channel][max_bs] int32); afterwards lane ch runs channel ch's predictor
+// (fixed or LPC) over its column, and the wave writes the planar slot.
+// Anything this path does not take (32-bit samples, a block too large for
+// LDS, a code longer than the window's look-ahead, a residual or sample
+// beyond 32 bits) is marked in cand_redo and left to the lane decoder.
+constexpr uint32_t kFWin = 512;   // LDS window words
+constexpr uint32_t kFLook = 64;   // words a round keeps past its 64 lane segments
+constexpr uint64_t kInf = ~0ull;
+
+struct FWin {
+  const uint8_t* base;  // the stream, aligned down to a word
+  uint64_t lim;         // bytes readable from base
+  uint32_t* w;          // LDS: kFWin + 2 words
+  uint64_t W;           // word index of w[0] (kInf: none yet)
+};
+
+__device__ __forceinline__ uint32_t load_be_word(const FWin& f, uint64_t wi) {
+  const uint64_t b = 4 * wi;
+  if (b + 4 <= f.lim) return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(f.base + b));
+  uint32_t v = 0;
+  for (uint32_t j = 0; j < 4; ++j) v = (v << 8) | (b + j < f.lim ? (uint32_t)f.base[b + j] : 0u);
+  return v;
+}
+// (uniform) the window holds words [bitpos / 32, + words)
+__device__ __forceinline__ void win_cover(FWin& f, uint64_t bitpos, uint32_t words) {
+  const uint64_t wi = bitpos >> 5;
+  if (f.W != kInf && wi >= f.W && wi + words <= f.W + kFWin) return;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < kFWin + 2; j += kWave) f.w[j] = load_be_word(f, wi + j);
+  f.W = wi;
+  __syncthreads();
+}
+// n (1..32) bits at absolute bit x, which the window holds
+__device__ __forceinline__ uint32_t wbits(const FWin& f, uint64_t x, uint32_t n) {
+  const uint32_t i = (uint32_t)((x >> 5) - f.W);
+  const uint64_t v = (((uint64_t)f.w[i] << 32) | f.w[i + 1]) << (x & 31u);
+  return (uint32_t)(v >> (64 - n));
+}
+// the first 1 bit at or after x inside the window (kInf: none)
+__device__ __forceinline__ uint64_t next_one(const FWin& f, uint64_t x) {
+  uint32_t i = (uint32_t)((x >> 5) - f.W);
+  const uint32_t w = f.w[i] << (x & 31u);
+  if (w) return x + (uint32_t)__builtin_clz(w);
+  for (++i; i < kFWin; ++i)
+    if (f.w[i]) return 32 * (f.W + i) + (uint32_t)__builtin_clz(f.w[i]);
+  return kInf;
+}
+__device__ __forceinline__ int32_t sext(uint32_t v, uint32_t n) {  // n in 1..32
+  return n >= 32 ? (int32_t)v : (int32_t)(v << (32 - n)) >> (32 - n);
+}
+// (uniform) n <= 32 bits at pos, advancing it
+__device__ __forceinline__ uint32_t ubits(FWin& f, uint64_t& pos, uint32_t n) {
+  if (!n) return 0;
+  win_cover(f, pos, 2);
+  const uint32_t v = wbits(f, pos, n);
+  pos += n;
+  return v;
+}
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+enum : int { kSfOk = 0, kSfBad = 1, kSfRedo = 2 };
+
+// n values of w (0..32) bits each from pos into s[0, n), all lanes
+__device__ void wave_raw(FWin& f, uint64_t& pos, int32_t* s, uint32_t n, uint32_t w) {
+  for (uint32_t j0 = 0; j0 < n; j0 += kWave) {
+    const uint64_t at = pos + (uint64_t)j0 * w;
+    win_cover(f, at, (kWave * w + 31) / 32 + 2);
+    const uint32_t i = j0 + threadIdx.x;
+    if (i < n) s[i] = w ? sext(wbits(f, at + (uint64_t)threadIdx.x * w, w), w) : 0;
+  }
+  pos += (uint64_t)n * w;
+}
+
+// this lane's parse from entry e of its segment [ss, ss + 32): M = code
+// starts (bit j: ss + j), X = the first start at or past the segment end
+__device__ __forceinline__ void rice_parse(const FWin& f, uint64_t e, uint64_t ss, uint32_t k, uint32_t& M, uint64_t& X,
+                                           bool& ovf) {
+  M = 0;
+  ovf = false;
+  uint64_t x = e;
+  while (x < ss + 32) {
+    M |= 1u << (uint32_t)(x - ss);
+    const uint64_t t = next_one(f, x);
+    if (t == kInf) {
+      ovf = true;
+      X = kInf;
+      return;
+    }
+    x = t + 1 + k;
+  }
+  X = x;
+}
+
+// n Rice codes of parameter k from pos, zigzag residuals into s[0, n)
+__device__ int wave_rice(FWin& f, uint64_t& pos, int32_t* s, uint32_t n, uint32_t k) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t done = 0;
+  while (done < n) {
+    win_cover(f, pos, kWave + kFLook);
+    const uint64_t ss = ((pos >> 5) + lane) << 5;
+    const uint32_t need = n - done;
+    uint64_t e = lane == 0 ? pos : ss;
+    uint32_t M;
+    uint64_t X;
+    bool ovf;
+    rice_parse(f, e, ss, k, M, X, ovf);
+    for (;;) {
+      const uint64_t px = shfl_up_u64(X);
+      const uint64_t ne = lane == 0 ? pos : px;
+      bool moved = false;
+      if (ne != e) {
+        moved = true;
+        e = ne;
+        if (ne >= ss + 32) {  // the previous lane's last code covers this segment
+          M = 0;
+          X = ne;
+          ovf = false;
+        } else if ((M >> (uint32_t)(ne - ss)) & 1u) {  // joins the parse already made
+          M &= ~0u << (uint32_t)(ne - ss);
+        } else {
+          rice_parse(f, ne, ss, k, M, X, ovf);
+        }
       }
-      o[2 * i] = (int32_t)L;
-      o[2 * i + 1] = (int32_t)R;
+      const uint64_t mv = __ballot(moved);
+      if (!mv) break;
+      // the lanes below the first that moved are final: enough codes there?
+      uint32_t tot;
+      const uint32_t ex = wave_excl_sum((uint32_t)__builtin_popcount(M), tot);
+      if ((uint32_t)__shfl((int)ex, (int)__builtin_ctzll(mv)) >= need) break;
+    }
+    const uint32_t cnt = (uint32_t)__builtin_popcount(M);
+    uint32_t tot;
+    const uint32_t idx = wave_excl_sum(cnt, tot);
+    // a needed code that runs past the window
+    if (__ballot(ovf && idx + cnt - 1 < need)) return kSfRedo;
+    // (the bound as two tests: a single min(cnt, need - idx) behind an idx < need
+    // select was observed to take codes past need on gfx950)
+    bool wide = false;
+    uint32_t m = M;
+    for (uint32_t j = 0; j < cnt && idx + j < need; ++j) {
+      const uint64_t x = ss + (uint32_t)__builtin_ctz(m);
+      m &= m - 1;
+      const uint64_t t = next_one(f, x);
+      const uint64_t u = ((t - x) << k) | (k ? wbits(f, t + 1, k) : 0u);
+      const int64_t r = (int64_t)(u >> 1) ^ -(int64_t)(u & 1u);
+      wide |= r != (int64_t)(int32_t)r;
+      s[done + idx + j] = (int32_t)r;
+    }
+    if (__ballot(wide)) return kSfRedo;
+    if (tot >= need) {
+      // the partition ends where code `need` would start
+      const bool own = idx < need && need - 1 < idx + cnt;
+      uint64_t endp = 0;
+      if (own) {
+        const uint32_t r = need - idx;
+        if (r == cnt) {
+          endp = X;
+        } else {
+          uint32_t mm = M;
+          for (uint32_t j = 0; j < r; ++j) mm &= mm - 1;
+          endp = ss + (uint32_t)__builtin_ctz(mm);
+        }
+      }
+      pos = shfl_u64(endp, (uint32_t)__builtin_ctzll(__ballot(own)));
+      done = n;
     } else {
-      for (uint32_t ch = 0; ch < C; ++ch) o[(uint64_t)i * C + ch] = (int32_t)x[ch];
+      pos = shfl_u64(X, kWave - 1);
+      done += tot;
+    }
+    if (pos == kInf) return kSfRedo;
+  }
+  return kSfOk;
+}
+
+struct SubInfo {
+  uint32_t kind;  // 0: samples final (constant, verbatim), 1: fixed, 2: LPC
+  uint32_t order, wasted;
+  int32_t shift;
+  int32_t coef[32];
+};
+
+// One subframe's samples (constant, verbatim) or warm-up samples and
+// residuals (fixed, LPC) into s[0, bs); inf: what the predictor needs
+__device__ int wave_subframe(FWin& f, uint64_t& pos, int32_t* s, uint32_t bs, uint32_t sbps, SubInfo& inf) {
+  if (ubits(f, pos, 1)) return kSfBad;
+  const uint32_t type = ubits(f, pos, 6);
+  uint32_t wasted = 0;
+  if (ubits(f, pos, 1)) {
+    uint32_t z = 0;
+    for (;;) {
+      win_cover(f, pos, 2);
+      const uint32_t w = wbits(f, pos, 32);
+      if (w) {
+        z += (uint32_t)__builtin_clz(w);
+        pos += (uint32_t)__builtin_clz(w) + 1;
+        break;
+      }
+      z += 32;
+      pos += 32;
+      if (z >= sbps) return kSfBad;
+    }
+    wasted = z + 1;
+  }
+  if (wasted >= sbps) return kSfBad;
+  const uint32_t b = sbps - wasted;
+  uint32_t kind = 0, order = 0;
+  int32_t shift = 0;
+  if (type == 0) {
+    const int32_t v = sext(ubits(f, pos, b), b);
+    for (uint32_t i = threadIdx.x; i < bs; i += kWave) s[i] = v;
+  } else if (type == 1) {
+    wave_raw(f, pos, s, bs, b);
+  } else {
+    if (type >= 8 && type <= 12) kind = 1, order = type - 8;
+    else if (type >= 32) kind = 2, order = type - 31;
+    else return kSfBad;
+    if (order > bs) return kSfBad;
+    for (uint32_t i = 0; i < order; ++i) {
+      const int32_t v = sext(ubits(f, pos, b), b);
+      if (threadIdx.x == 0) s[i] = v;
+    }
+    if (kind == 2) {
+      const uint32_t prec = ubits(f, pos, 4) + 1;
+      if (prec == 16) return kSfBad;
+      shift = sext(ubits(f, pos, 5), 5);
+      if (shift < 0) return kSfBad;
+      for (uint32_t j = 0; j < order; ++j) {
+        const int32_t cf = sext(ubits(f, pos, prec), prec);
+        if (threadIdx.x == 0) inf.coef[j] = cf;
+      }
+    }
+    const uint32_t method = ubits(f, pos, 2);
+    if (method > 1) return kSfBad;
+    const uint32_t pb = method ? 5u : 4u, esc = (1u << pb) - 1;
+    const uint32_t po = ubits(f, pos, 4);
+    if (bs % (1u << po) || (bs >> po) < order) return kSfBad;
+    const uint32_t per = bs >> po;
+    uint32_t i0 = order;
+    for (uint32_t p = 0; p < (1u << po); ++p) {
+      const uint32_t k = ubits(f, pos, pb), n = per - (p == 0 ? order : 0u);
+      if (k == esc) {
+        wave_raw(f, pos, s + i0, n, ubits(f, pos, 5));
+      } else if (n) {
+        const int st = wave_rice(f, pos, s + i0, n, k);
+        if (st != kSfOk) return st;
+      }
+      i0 += n;
+      if (pos > 8 * f.lim) return kSfBad;
     }
   }
-  d.cand_len[c] = end;
+  if (threadIdx.x == 0) {
+    inf.kind = kind;
+    inf.order = order;
+    inf.wasted = wasted;
+    inf.shift = shift;
+  }
+  return pos > 8 * f.lim ? kSfBad : kSfOk;
+}
+
+// Channel prediction over its LDS column, one lane; false: a sample beyond 32 bits
+__device__ bool predict_column(int32_t* s, uint32_t bs, const SubInfo& inf) {
+  const uint32_t o = inf.order;
+  bool ok = true;
+  if (inf.kind == 1) {
+    int64_t h0 = o > 0 ? s[o - 1] : 0, h1 = o > 1 ? s[o - 2] : 0, h2 = o > 2 ? s[o - 3] : 0, h3 = o > 3 ? s[o - 4] : 0;
+    for (uint32_t i = o; i < bs; ++i) {
+      const int64_t r = s[i];
+      int64_t v;
+      switch (o) {
+        case 0: v = r; break;
+        case 1: v = r + h0; break;
+        case 2: v = r + 2 * h0 - h1; break;
+        case 3: v = r + 3 * h0 - 3 * h1 + h2; break;
+        default: v = r + 4 * h0 - 6 * h1 + 4 * h2 - h3; break;
+      }
+      ok &= v == (int64_t)(int32_t)v;
+      s[i] = (int32_t)v;
+      h3 = h2, h2 = h1, h1 = h0, h0 = v;
+    }
+  } else if (inf.kind == 2) {
+    const int32_t sh = inf.shift;
+    for (uint32_t i = o; i < bs; ++i) {
+      int64_t acc = 0;
+      for (uint32_t j = 0; j < o; ++j) acc += (int64_t)inf.coef[j] * s[i - 1 - j];
+      const int64_t v = (int64_t)s[i] + (acc >> sh);
+      ok &= v == (int64_t)(int32_t)v;
+      s[i] = (int32_t)v;
+    }
+  }
+  return ok;
+}
+
+__global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(FlacDecParams d) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ SubInfo info[8];
+  __shared__ uint32_t wide;
+  const uint32_t c = blockIdx.x, lane = threadIdx.x;
+  const uint32_t nc = min(*d.ncand, d.max_cand);
+  if (c >= nc) return;
+  if (lane == 0) {
+    d.cand_len[c] = ~0ull;
+    d.cand_redo[c] = 0;
+    wide = 0;
+  }
+  const uint64_t p = d.cand_pos[c];
+  uint32_t bs, assign;
+  const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign);
+  if (!hl) return;
+  const uint32_t C = d.channels, mb = d.max_bs;
+  const uint32_t mis = (uint32_t)((uintptr_t)d.in & 3u);
+  FWin f{d.in - mis, d.nbytes + mis, lds, kInf};
+  int32_t* smp = reinterpret_cast<int32_t*>(lds + kFWin + 2);  // [C][max_bs]
+  uint64_t pos = 8 * (mis + p + hl);
+  for (uint32_t ch = 0; ch < C; ++ch) {
+    uint32_t sb = d.bps;
+    if ((assign == 8 && ch == 1) || (assign == 9 && ch == 0) || (assign == 10 && ch == 1)) sb = d.bps + 1;
+    const int st = wave_subframe(f, pos, smp + (uint64_t)ch * mb, bs, sb, info[ch]);
+    if (st == kSfRedo && lane == 0) d.cand_redo[c] = 1;
+    if (st != kSfOk) return;
+  }
+  __syncthreads();
+  if (lane < C && !predict_column(smp + (uint64_t)lane * mb, bs, info[lane])) wide = 1;
+  __syncthreads();
+  if (wide) {
+    if (lane == 0) d.cand_redo[c] = 1;
+    return;
+  }
+  int32_t* o = static_cast<int32_t*>(d.scratch) + (uint64_t)c * mb * C;
+  for (uint32_t ch = 0; ch < C; ++ch) {
+    const uint32_t ws = info[ch].wasted;
+    for (uint32_t i = lane; i < bs; i += kWave) o[(uint64_t)ch * mb + i] = (int32_t)((uint32_t)smp[(uint64_t)ch * mb + i] << ws);
+  }
+  const uint64_t end = ((pos + 7) >> 3) - mis - p;
+  if (lane == 0 && end + 2 <= d.nbytes - p) d.cand_len[c] = end;
 }
 
 // One lane: the chain of frames from byte 0
@@ -900,14 +1268,38 @@ __global__ void rpp_flac_chain_kernel(FlacDecParams d) {
   *d.status = st;
 }
 
+// One block per chained frame: planar subframes to interleaved samples,
+// undoing the stereo decorrelation (left/side, side/right, mid/side)
+template <class T>
 __global__ __launch_bounds__(256) void rpp_flac_place_kernel(FlacDecParams d) {
   const uint32_t f = blockIdx.x;
   if (f >= *d.nchain || *d.status != RPP_OK) return;
   const uint32_t c = d.chain[f];
-  const uint64_t n = (uint64_t)d.cand_info[c] * d.channels;
-  const int32_t* s = d.scratch + (uint64_t)c * d.max_bs * d.channels;
-  int32_t* o = d.out + d.chain_off[f] * d.channels;
-  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) o[i] = s[i];
+  uint32_t bs, assign;
+  if (!parse_header(d.in, d.nbytes, d.cand_pos[c], d.channels, d.bps, bs, assign)) return;
+  const uint32_t C = d.channels, mb = d.max_bs;
+  const T* s = static_cast<const T*>(d.scratch) + (uint64_t)c * mb * C;
+  int32_t* o = d.out + d.chain_off[f] * C;
+  if (assign >= 8) {
+    for (uint32_t i = threadIdx.x; i < bs; i += blockDim.x) {
+      const int64_t x0 = s[i], x1 = s[mb + i];
+      int64_t L, R;
+      if (assign == 8) L = x0, R = x0 - x1;
+      else if (assign == 9) R = x1, L = x0 + x1;
+      else {
+        const int64_t m = (x0 * 2) | (x1 & 1);
+        L = (m + x1) >> 1;
+        R = (m - x1) >> 1;
+      }
+      *reinterpret_cast<int2*>(o + 2 * i) = make_int2((int32_t)L, (int32_t)R);
+    }
+  } else {
+    const uint64_t n = (uint64_t)bs * C;
+    for (uint64_t e = threadIdx.x; e < n; e += blockDim.x) {
+      const uint32_t i = (uint32_t)(e / C), ch = (uint32_t)(e - (uint64_t)i * C);
+      o[e] = (int32_t)s[(uint64_t)ch * mb + i];
+    }
+  }
 }
 
 }  // namespace
@@ -960,7 +1352,7 @@ uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uin
                                          uint32_t max_candidates) {
   const uint64_t mc = max_candidates;
   const uint64_t per = (uint64_t)max_blocksize * channels;
-  return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 8) + 64 + mc * per * 4 + mc * per * 8 + 256;
+  return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 4 + 8) + 64 + mc * per * 8 + 256;
 }
 
 int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
@@ -994,22 +1386,37 @@ int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels,
   d.cand_info = reinterpret_cast<uint32_t*>(take(4 * mc));
   d.cand_len = reinterpret_cast<uint64_t*>(take(8 * mc));
   d.cand_ok = reinterpret_cast<uint32_t*>(take(4 * mc));
+  d.cand_redo = reinterpret_cast<uint32_t*>(take(4 * mc));
   d.chain = reinterpret_cast<uint32_t*>(take(4 * mc));
   d.chain_off = reinterpret_cast<uint64_t*>(take(8 * mc));
   d.nchain = reinterpret_cast<uint32_t*>(take(16));
-  d.scratch = reinterpret_cast<int32_t*>(take(4 * mc * per));
-  int64_t* work = reinterpret_cast<int64_t*>(take(8 * mc * per));
+  const bool wide = bps == 32;
+  d.scratch = take((wide ? 8 : 4) * mc * per);
   d.ncand = d_ncand;
   d.max_cand = max_candidates;
   d.out = d_out;
   d.status = d_status;
   if (hipMemsetAsync(d_ncand, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
   if (nbytes) hipLaunchKernelGGL(rpp_flac_scan_kernel, dim3((uint32_t)((nbytes + 255) / 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(rpp_flac_frame_kernel, dim3((uint32_t)((mc + 63) / 64)), dim3(64), 0, s, d, work);
+  // the wave decoder where the frame's samples fit LDS, the lane decoder for the rest
+  const uint64_t lds = 4ull * (kFWin + 2) + 4ull * per;
+  bool wave = !wide && lds <= kFlacWaveLds;
+  if (wave) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rpp_flac_frame_wave_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFlacWaveLds);
+    wave = attr == hipSuccess;
+  }
+  if (wave) {
+    hipLaunchKernelGGL(rpp_flac_frame_wave_kernel, dim3((uint32_t)mc), dim3(64), (size_t)lds, s, d);
+    d.redo_only = 1;
+  }
+  if (wide) hipLaunchKernelGGL(rpp_flac_frame_kernel<int64_t>, dim3((uint32_t)((mc + 63) / 64)), dim3(64), 0, s, d);
+  else hipLaunchKernelGGL(rpp_flac_frame_kernel<int32_t>, dim3((uint32_t)((mc + 63) / 64)), dim3(64), 0, s, d);
   hipLaunchKernelGGL(rpp_flac_crc_kernel, dim3((uint32_t)(mc < 4096 ? mc : 4096)), dim3(64), 0, s, d.in, d.cand_pos,
                      d.cand_len, (uint32_t)mc, nullptr, d.cand_ok, d.ncand);
   hipLaunchKernelGGL(rpp_flac_chain_kernel, dim3(1), dim3(1), 0, s, d);
-  hipLaunchKernelGGL(rpp_flac_place_kernel, dim3((uint32_t)mc), dim3(256), 0, s, d);
+  if (wide) hipLaunchKernelGGL(rpp_flac_place_kernel<int64_t>, dim3((uint32_t)mc), dim3(256), 0, s, d);
+  else hipLaunchKernelGGL(rpp_flac_place_kernel<int32_t>, dim3((uint32_t)mc), dim3(256), 0, s, d);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 

@@ -3,7 +3,8 @@ stereo 16-bit and 8-channel 24-in-32-bit PCM sines + noise), compress and
 decompress through dwarfs_amd.flac (host bytes in and out, so PCIe and host
 copies are included) and the kernels alone (device-resident), against the CPU
 restatement (oracle/flac_oracle.c, one thread; libFLAC itself is absent).
-One JSON line per case."""
+One JSON line per case.  --gpu-only: the kernels alone, no CPU oracle or
+host path (for profiling)."""
 import json
 import sys
 import time
@@ -21,6 +22,7 @@ from test_flac import sines  # noqa: E402
 import ctypes as C  # noqa: E402
 
 dev = torch.device("cuda:0")
+gpu_only = "--gpu-only" in sys.argv
 for channels, nbytes, bits in ((2, 2, 16), (8, 4, 24)):
     n = (16 << 20) // (channels * nbytes)
     rng = np.random.default_rng(1)
@@ -44,8 +46,10 @@ for channels, nbytes, bits in ((2, 2, 16), (8, 4, 24)):
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps
 
-    te = timed(lambda: FL.FlacBlockCompressor().compress(data, meta))
-    td = timed(lambda: FL.decompress(comp))
+    te = td = float("nan")
+    if not gpu_only:
+        te = timed(lambda: FL.FlacBlockCompressor().compress(data, meta))
+        td = timed(lambda: FL.decompress(comp))
     # kernels alone
     L = N.lib()
     frames = (n + 4095) // 4096
@@ -70,12 +74,14 @@ for channels, nbytes, bits in ((2, 2, 16), (8, 4, 24)):
                                            C.c_void_p(wd.data_ptr()), wdb, C.c_void_p(nc.data_ptr()),
                                            C.c_void_p(s.cuda_stream)))
     assert int(st.item()) == 0 and torch.equal(y, xt)
-    t0 = time.perf_counter()
-    cs = F.encode(x, channels, bits, 4096, F.EncodeOptions(max_lpc_order=0))
-    tc_e = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    F.decode(cs, x.size)
-    tc_d = time.perf_counter() - t0
+    tc_e = tc_d = float("nan")
+    if not gpu_only:
+        t0 = time.perf_counter()
+        cs = F.encode(x, channels, bits, 4096, F.EncodeOptions(max_lpc_order=0))
+        tc_e = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        F.decode(cs, x.size)
+        tc_d = time.perf_counter() - t0
     mib = len(data) / 2**20
     print(json.dumps({"case": "flac", "block_MiB": round(mib, 1), "channels": channels, "bits": bits,
                       "ratio": round(len(comp) / len(data), 4),
