@@ -70,16 +70,18 @@ __device__ __forceinline__ int32_t wave_max(int32_t v) {
   for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o));
   return v;
 }
+// exclusive wave prefix sum by DPP (row_shr 1/2/4/8, row_bcast 15/31: no
+// LDS round trips); total = the wave's sum
 __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t& total) {
-  const uint32_t lane = lane_id();
-  uint32_t x = v;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-    if (lane >= d) x += y;
-  }
-  total = (uint32_t)__shfl((int)x, 63);
-  return x - v;
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
+  total = (uint32_t)__builtin_amdgcn_readlane(x, 63);
+  return (uint32_t)x - v;
 }
 
 // ---- CRCs (RFC 9639 9.1.8 CRC-8 poly 0x07, 9.3 CRC-16 poly 0x8005; init 0) ----
@@ -947,12 +949,17 @@ __device__ __forceinline__ uint32_t ubits(FWin& f, uint64_t& pos, uint32_t n) {
   pos += n;
   return v;
 }
+// lane l gets lane l-1's v (DPP wave_shr:1; lane 0 keeps its own)
 __device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1);
-  return ((uint64_t)hi << 32) | lo;
+  const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+  const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp(lo, lo, 0x138, 0xF, 0xF, false);
+  const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp(hi, hi, 0x138, 0xF, 0xF, false);
+  return ((uint64_t)h << 32) | l;
 }
+// lane src's v (src uniform)
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)src),
+                 hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)src);
   return ((uint64_t)hi << 32) | lo;
 }
 
@@ -1024,7 +1031,7 @@ __device__ int wave_rice(FWin& f, uint64_t& pos, int32_t* s, uint32_t n, uint32_
       // the lanes below the first that moved are final: enough codes there?
       uint32_t tot;
       const uint32_t ex = wave_excl_sum((uint32_t)__builtin_popcount(M), tot);
-      if ((uint32_t)__shfl((int)ex, (int)__builtin_ctzll(mv)) >= need) break;
+      if ((uint32_t)__builtin_amdgcn_readlane((int)ex, (int)__builtin_ctzll(mv)) >= need) break;
     }
     const uint32_t cnt = (uint32_t)__builtin_popcount(M);
     uint32_t tot;
