@@ -584,9 +584,8 @@ struct FlacDecParams {
   uint32_t* ncand;     // candidates found
   uint32_t max_cand;
   void* scratch;       // [max_cand][channels][max_bs] int32 (int64 for 32-bit samples)
-  uint32_t* chain;     // [frames] candidate of chained frame i
-  uint64_t* chain_off; // [frames] first sample of chained frame i
-  uint32_t* nchain;
+  uint64_t* place;     // [max_cand] first sample of the candidate's frame (kNoPlace: not on the chain)
+  uint64_t* link_acc;  // [2] block sizes of the linked candidates, link failures
   int32_t* out;        // interleaved samples [nsamples * channels]
   int32_t* status;
 };
@@ -662,9 +661,10 @@ struct BitReader {
 };
 
 // Parses a frame header at byte p (no CRC-16); returns its length (0: not a
-// valid header for this stream) and the block size and channel assignment
+// valid header for this stream) and the block size, channel assignment and
+// coded number (frame number, or first sample with variable blocking)
 __device__ uint32_t parse_header(const uint8_t* in, uint64_t nbytes, uint64_t p, uint32_t channels, uint32_t bps,
-                                 uint32_t& bs, uint32_t& assign) {
+                                 uint32_t& bs, uint32_t& assign, uint64_t& coded) {
   if (p + 6 > nbytes) return 0;
   const uint8_t* h = in + p;
   if (h[0] != 0xFF || (h[1] & 0xFE) != 0xF8) return 0;
@@ -689,8 +689,12 @@ __device__ uint32_t parse_header(const uint8_t* in, uint64_t nbytes, uint64_t p,
   else if (b0 == 0xFE) more = 6;
   else return 0;
   if (q + more + 4 > nbytes) return 0;
-  for (uint32_t i = 0; i < more; ++i)
-    if ((in[q++] & 0xC0) != 0x80) return 0;
+  uint64_t num = more ? (b0 & (0x7Fu >> (more + 1))) : b0;
+  for (uint32_t i = 0; i < more; ++i) {
+    if ((in[q] & 0xC0) != 0x80) return 0;
+    num = (num << 6) | (in[q++] & 0x3Fu);
+  }
+  coded = num;
   if (bc == 1) bs = 192;
   else if (bc <= 5) bs = 576u << (bc - 2);
   else if (bc == 6) bs = (uint32_t)in[q++] + 1;
@@ -713,7 +717,8 @@ __global__ __launch_bounds__(256) void rpp_flac_scan_kernel(FlacDecParams d) {
   uint32_t at = 0;
   if (d.in[p] == 0xFF && p + 1 < d.nbytes && (d.in[p + 1] & 0xFE) == 0xF8) {
     uint32_t bs, assign;
-    const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign);
+    uint64_t coded;
+    const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign, coded);
     if (hl && bs <= d.max_bs) {
       const uint32_t c = atomicAdd(d.ncand, 1u);
       if (c < d.max_cand) {
@@ -864,7 +869,8 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d) {
   d.cand_len[c] = ~0ull;
   const uint64_t p = d.cand_pos[c];
   uint32_t bs, assign;
-  const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign);
+  uint64_t coded;
+  const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign, coded);
   if (!hl) return;
   const uint32_t C = d.channels;
   T* s = static_cast<T*>(d.scratch) + (uint64_t)c * d.max_bs * C;
@@ -1209,7 +1215,8 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(FlacDecParams d
   }
   const uint64_t p = d.cand_pos[c];
   uint32_t bs, assign;
-  const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign);
+  uint64_t coded;
+  const uint32_t hl = parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign, coded);
   if (!hl) return;
   const uint32_t C = d.channels, mb = d.max_bs;
   const uint32_t mis = (uint32_t)((uintptr_t)d.in & 3u);
@@ -1239,11 +1246,77 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(FlacDecParams d
   if (lane == 0 && end + 2 <= d.nbytes - p) d.cand_len[c] = end;
 }
 
-// One lane: the chain of frames from byte 0
+constexpr uint64_t kNoPlace = ~0ull;
+
+__device__ __forceinline__ bool cand_valid(const FlacDecParams& d, uint32_t c) {
+  return d.cand_len[c] != ~0ull && d.cand_ok[c];
+}
+// the first sample of candidate c's frame by its coded number (fixed
+// blocking: frame number x the block size of the frame at byte 0)
+__device__ __forceinline__ bool cand_first_sample(const FlacDecParams& d, uint32_t c, uint64_t nominal, uint32_t& bs,
+                                                  uint64_t& first) {
+  const uint64_t p = d.cand_pos[c];
+  uint32_t assign;
+  uint64_t coded;
+  if (!parse_header(d.in, d.nbytes, p, d.channels, d.bps, bs, assign, coded)) return false;
+  if (d.in[p + 1] & 1u) first = coded;  // variable blocking: the sample number
+  else if (coded > (d.nsamples / (nominal ? nominal : 1))) return false;
+  else first = coded * nominal;
+  return true;
+}
+
+// Every valid candidate checks its link to the frame after it: that one is a
+// valid candidate too and its coded number puts it right after this one (or
+// this one ends the stream at the last sample).  When every link holds, the
+// valid candidates' block sizes add up to the stream and a valid frame at
+// byte 0 starts at sample 0, the valid candidates are exactly the chain the
+// serial walk visits (one contiguous run of samples from 0 covers them all)
+// and place[] is final; otherwise rpp_flac_chain_kernel walks.
+__global__ __launch_bounds__(256) void rpp_flac_link_kernel(FlacDecParams d) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nc = min(*d.ncand, d.max_cand);
+  if (c >= nc) return;
+  d.place[c] = kNoPlace;
+  if (!cand_valid(d, c)) return;
+  const uint32_t head = d.nbytes ? d.cand_at[0] : 0u;
+  bool ok = head != 0;
+  uint32_t bs = 0, bs_next;
+  uint64_t first = 0, first_next;
+  if (ok) ok = cand_first_sample(d, c, d.cand_info[head - 1], bs, first);
+  if (ok) ok = first + bs <= d.nsamples;
+  if (ok) {
+    const uint64_t e = d.cand_pos[c] + d.cand_len[c] + 2;
+    if (e == d.nbytes) {
+      ok = first + bs == d.nsamples;
+    } else if (e > d.nbytes) {
+      ok = false;
+    } else {
+      const uint32_t at = d.cand_at[e];
+      ok = at && cand_valid(d, at - 1) && cand_first_sample(d, at - 1, d.cand_info[head - 1], bs_next, first_next) &&
+           first_next == first + bs;
+    }
+  }
+  if (!ok) {
+    atomicOr(reinterpret_cast<unsigned long long*>(&d.link_acc[1]), 1ull);
+    return;
+  }
+  d.place[c] = first;
+  atomicAdd(reinterpret_cast<unsigned long long*>(&d.link_acc[0]), (unsigned long long)bs);
+}
+
+// One lane: accepts the links, or walks the chain of frames from byte 0
+// (each frame starts where the previous one's CRC-16 ends) and places the
+// frames it visits
 __global__ void rpp_flac_chain_kernel(FlacDecParams d) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const uint32_t nc = min(*d.ncand, d.max_cand);
+  const uint32_t head = d.nbytes ? d.cand_at[0] : 0u;
+  if (d.nsamples && !d.link_acc[1] && d.link_acc[0] == d.nsamples && head && d.place[head - 1] == 0) {
+    *d.status = RPP_OK;
+    return;
+  }
+  for (uint32_t c = 0; c < nc; ++c) d.place[c] = kNoPlace;
   uint64_t pos = 0, done = 0;
-  uint32_t n = 0;
   int32_t st = RPP_OK;
   while (done < d.nsamples) {
     if (pos >= d.nbytes) {
@@ -1256,7 +1329,7 @@ __global__ void rpp_flac_chain_kernel(FlacDecParams d) {
       break;
     }
     const uint32_t c = at - 1;
-    if (d.cand_len[c] == ~0ull || !d.cand_ok[c]) {
+    if (!cand_valid(d, c)) {
       st = RPP_INVALID_ARGUMENT;
       break;
     }
@@ -1265,28 +1338,27 @@ __global__ void rpp_flac_chain_kernel(FlacDecParams d) {
       st = RPP_INVALID_ARGUMENT;
       break;
     }
-    d.chain[n] = c;
-    d.chain_off[n] = done;
-    ++n;
+    d.place[c] = done;
     done += bs;
     pos += d.cand_len[c] + 2;
   }
-  *d.nchain = n;
   *d.status = st;
 }
 
-// One block per chained frame: planar subframes to interleaved samples,
-// undoing the stereo decorrelation (left/side, side/right, mid/side)
+// One block per candidate on the chain: planar subframes to interleaved
+// samples, undoing the stereo decorrelation (left/side, side/right, mid/side)
 template <class T>
 __global__ __launch_bounds__(256) void rpp_flac_place_kernel(FlacDecParams d) {
-  const uint32_t f = blockIdx.x;
-  if (f >= *d.nchain || *d.status != RPP_OK) return;
-  const uint32_t c = d.chain[f];
+  const uint32_t c = blockIdx.x;
+  if (c >= min(*d.ncand, d.max_cand) || *d.status != RPP_OK) return;
+  const uint64_t first = d.place[c];
+  if (first == kNoPlace) return;
   uint32_t bs, assign;
-  if (!parse_header(d.in, d.nbytes, d.cand_pos[c], d.channels, d.bps, bs, assign)) return;
+  uint64_t coded;
+  if (!parse_header(d.in, d.nbytes, d.cand_pos[c], d.channels, d.bps, bs, assign, coded)) return;
   const uint32_t C = d.channels, mb = d.max_bs;
   const T* s = static_cast<const T*>(d.scratch) + (uint64_t)c * mb * C;
-  int32_t* o = d.out + d.chain_off[f] * C;
+  int32_t* o = d.out + first * C;
   if (assign >= 8) {
     for (uint32_t i = threadIdx.x; i < bs; i += blockDim.x) {
       const int64_t x0 = s[i], x1 = s[mb + i];
@@ -1359,7 +1431,7 @@ uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uin
                                          uint32_t max_candidates) {
   const uint64_t mc = max_candidates;
   const uint64_t per = (uint64_t)max_blocksize * channels;
-  return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 4 + 8) + 64 + mc * per * 8 + 256;
+  return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 8) + 64 + mc * per * 8 + 256;
 }
 
 int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
@@ -1394,9 +1466,8 @@ int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels,
   d.cand_len = reinterpret_cast<uint64_t*>(take(8 * mc));
   d.cand_ok = reinterpret_cast<uint32_t*>(take(4 * mc));
   d.cand_redo = reinterpret_cast<uint32_t*>(take(4 * mc));
-  d.chain = reinterpret_cast<uint32_t*>(take(4 * mc));
-  d.chain_off = reinterpret_cast<uint64_t*>(take(8 * mc));
-  d.nchain = reinterpret_cast<uint32_t*>(take(16));
+  d.place = reinterpret_cast<uint64_t*>(take(8 * mc));
+  d.link_acc = reinterpret_cast<uint64_t*>(take(16));
   const bool wide = bps == 32;
   d.scratch = take((wide ? 8 : 4) * mc * per);
   d.ncand = d_ncand;
@@ -1421,6 +1492,8 @@ int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels,
   else hipLaunchKernelGGL(rpp_flac_frame_kernel<int32_t>, dim3((uint32_t)((mc + 63) / 64)), dim3(64), 0, s, d);
   hipLaunchKernelGGL(rpp_flac_crc_kernel, dim3((uint32_t)(mc < 4096 ? mc : 4096)), dim3(64), 0, s, d.in, d.cand_pos,
                      d.cand_len, (uint32_t)mc, nullptr, d.cand_ok, d.ncand);
+  if (hipMemsetAsync(d.link_acc, 0, 16, s) != hipSuccess) return RPP_HIP_ERROR;
+  hipLaunchKernelGGL(rpp_flac_link_kernel, dim3((uint32_t)((mc + 255) / 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(rpp_flac_chain_kernel, dim3(1), dim3(1), 0, s, d);
   if (wide) hipLaunchKernelGGL(rpp_flac_place_kernel<int64_t>, dim3((uint32_t)mc), dim3(256), 0, s, d);
   else hipLaunchKernelGGL(rpp_flac_place_kernel<int32_t>, dim3((uint32_t)mc), dim3(256), 0, s, d);
