@@ -185,6 +185,8 @@ struct EncShared {
   uint32_t kpar[4][1u << kMaxPo];  // Rice parameters per source and partition
   unsigned long long psum[1u << kMaxPo];
   unsigned long long pbits[kMaxPo + 1][1u << kMaxPo];
+  uint32_t kt[2u << kMaxPo];  // Rice parameter of partition p of order po at [2^po - 1 + p]
+  uint32_t ures[kFlacBlock];  // the planned source's folded residuals
 };
 
 // source sample i: 0 / 1 = staged channel, 2 = side (L - R), 3 = mid ((L + R) >> 1)
@@ -248,12 +250,21 @@ __device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint3
   uint64_t sabs[5] = {0, 0, 0, 0, 0};
   uint32_t bad = 0;
   for (uint32_t i = lane; i < bs; i += kWave) {
+    // the five orders' residuals from x(i-4..i), read once: order o's is the
+    // o-th backward difference
+    int64_t r[5];
+#pragma unroll
+    for (uint32_t j = 0; j <= 4; ++j) r[j] = i >= j ? src_sample(sh, src, i - j) >> wasted : 0;
+#pragma unroll
+    for (uint32_t o = 1; o <= 4; ++o)
+#pragma unroll
+      for (uint32_t j = 4; j >= o; --j) r[j] = r[j - 1] - r[j];
+    // (r[o] now holds the o-th difference at i)
 #pragma unroll
     for (uint32_t o = 0; o <= 4; ++o) {
       if (i < o) continue;
-      const int64_t r = fixed_res(sh, src, i, o, wasted);
-      if (r < INT32_MIN || r > INT32_MAX) bad |= 1u << o;
-      sabs[o] += (uint64_t)(r < 0 ? -r : r);
+      if (r[o] < INT32_MIN || r[o] > INT32_MAX) bad |= 1u << o;
+      sabs[o] += (uint64_t)(r[o] < 0 ? -r[o] : r[o]);
     }
   }
   bad = wave_or(bad);
@@ -276,40 +287,64 @@ __device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint3
   uint32_t pomax = 0;
   while (pomax < kMaxPo && bs % (2u << pomax) == 0 && (bs >> (pomax + 1)) > order) ++pomax;
   const uint32_t psz = bs >> pomax;  // samples per finest partition
-  for (uint32_t i = lane; i < bs; i += kWave)
-    if (i >= order) atomicAdd(&sh.psum[i / psz], (unsigned long long)fold(fixed_res(sh, src, i, order, wasted)));
+  // (a lane's samples run through the partitions in order: its sums go to LDS
+  // once per partition, not once per sample)
+  {
+    uint32_t cur = ~0u;
+    uint64_t acc = 0;
+    for (uint32_t i = lane; i < bs; i += kWave) {
+      if (i < order) continue;
+      const uint32_t q = i / psz;
+      if (q != cur) {
+        if (acc) atomicAdd(&sh.psum[cur], (unsigned long long)acc);
+        cur = q;
+        acc = 0;
+      }
+      const uint64_t u = fold(fixed_res(sh, src, i, order, wasted));
+      sh.ures[i] = (uint32_t)u;  // (residuals fit 32 bits: u < 2^32)
+      acc += u;
+    }
+    if (acc) atomicAdd(&sh.psum[cur], (unsigned long long)acc);
+  }
+  __syncthreads();
+  // k of every partition of every order (kt[2^po - 1 + p])
+  for (uint32_t t = lane; t < (2u << pomax) - 1; t += kWave) {
+    const uint32_t po = 31u - (uint32_t)__builtin_clz(t + 1), p = t + 1 - (1u << po);
+    const uint32_t per = bs >> po, f = 1u << (pomax - po);
+    uint64_t sum = 0;
+    for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
+    const uint32_t cnt = per - (p == 0 ? order : 0u);
+    const uint64_t mean = cnt ? sum / cnt : 0;
+    sh.kt[t] = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
+  }
   __syncthreads();
   for (uint32_t po = 0; po <= pomax; ++po) {
-    const uint32_t np = 1u << po, per = bs >> po;
+    const uint32_t per = bs >> po;
+    const uint32_t* kt = sh.kt + (1u << po) - 1;
+    uint32_t cur = ~0u, k = 0;
+    uint64_t acc = 0;
     for (uint32_t i = lane; i < bs; i += kWave) {
       if (i < order) continue;
       const uint32_t p = i / per;
-      // the partition's sum over the finest ones it covers
-      uint64_t sum = 0;
-      const uint32_t f = 1u << (pomax - po);
-      for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
-      const uint32_t cnt = per - (p == 0 ? order : 0u);
-      const uint64_t mean = cnt ? sum / cnt : 0;
-      const uint32_t k = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
-      const uint64_t u = fold(fixed_res(sh, src, i, order, wasted));
-      atomicAdd(&sh.pbits[po][p], (unsigned long long)((u >> k) + 1 + k));
+      if (p != cur) {
+        if (acc) atomicAdd(&sh.pbits[po][cur], (unsigned long long)acc);
+        cur = p;
+        acc = 0;
+        k = kt[p];
+      }
+      acc += (sh.ures[i] >> k) + 1 + k;
     }
-    (void)np;
+    if (acc) atomicAdd(&sh.pbits[po][cur], (unsigned long long)acc);
   }
   __syncthreads();
   uint64_t rbest = ~0ull;
   uint32_t bpo = 0, bmethod = 0;
   for (uint32_t po = 0; po <= pomax; ++po) {
-    const uint32_t np = 1u << po, per = bs >> po, f = 1u << (pomax - po);
+    const uint32_t np = 1u << po;
     uint64_t tot = 6;
     uint32_t kmaxp = 0;
     for (uint32_t p = 0; p < np; ++p) {
-      uint64_t sum = 0;
-      for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
-      const uint32_t cnt = per - (p == 0 ? order : 0u);
-      const uint64_t mean = cnt ? sum / cnt : 0;
-      const uint32_t k = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
-      kmaxp = max(kmaxp, k);
+      kmaxp = max(kmaxp, sh.kt[np - 1 + p]);
       tot += sh.pbits[po][p];
     }
     const uint32_t method = kmaxp > 14 ? 1u : 0u;
@@ -320,16 +355,7 @@ __device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint3
       bmethod = method;
     }
   }
-  {
-    const uint32_t np = 1u << bpo, per = bs >> bpo, f = 1u << (pomax - bpo);
-    for (uint32_t p = lane; p < np; p += kWave) {
-      uint64_t sum = 0;
-      for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
-      const uint32_t cnt = per - (p == 0 ? order : 0u);
-      const uint64_t mean = cnt ? sum / cnt : 0;
-      sh.kpar[src][p] = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
-    }
-  }
+  for (uint32_t p = lane; p < (1u << bpo); p += kWave) sh.kpar[src][p] = sh.kt[(1u << bpo) - 1 + p];
   __syncthreads();
   const uint64_t fbits = hdr + (uint64_t)order * P.bps + rbest;
   if (fbits < P.bits) {
@@ -470,6 +496,7 @@ __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
     stage(1, 1);
     __syncthreads();
     // the four sources' plans, Rice parameters kept per source (kpar[src])
+#pragma unroll
     for (uint32_t s = 0; s < 4; ++s) plans[s] = plan_subframe(sh, s, bs, s == 2 ? p.bps + 1 : p.bps);
     const uint64_t ind = plans[0].bits + plans[1].bits, ls = plans[0].bits + plans[2].bits,
                    rs = plans[2].bits + plans[1].bits, ms = plans[3].bits + plans[2].bits;
@@ -492,9 +519,11 @@ __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
   if (stereo) {
     const uint32_t s0 = assign == 9 ? 2u : assign == 10 ? 3u : 0u;
     const uint32_t s1 = assign == 1 ? 1u : assign == 9 ? 1u : 2u;
-    pos = emit_subframe(sh, plans[s0], s0, bs, pos, 32 * win_w0);
+    // (plans[] indexed by constants only: a variable index would put it in scratch)
+    auto pick = [&](uint32_t i) { return i == 0 ? plans[0] : i == 1 ? plans[1] : i == 2 ? plans[2] : plans[3]; };
+    pos = emit_subframe(sh, pick(s0), s0, bs, pos, 32 * win_w0);
     flush(sh, slot, win_w0, pos, false);
-    pos = emit_subframe(sh, plans[s1], s1, bs, pos, 32 * win_w0);
+    pos = emit_subframe(sh, pick(s1), s1, bs, pos, 32 * win_w0);
     flush(sh, slot, win_w0, pos, false);
   } else {
     for (uint32_t c = 0; c < C; ++c) {
@@ -1415,6 +1444,9 @@ int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channe
   uint64_t* lens = offs + frames + 1;
   FlacEncParams p{d_samples, nsamples, channels, bps, slots, slot, sizes, (uint32_t)frames};
   const size_t lds = sizeof(EncShared);
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rpp_flac_encode_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return RPP_HIP_ERROR;
   hipLaunchKernelGGL(rpp_flac_encode_kernel, dim3((uint32_t)frames), dim3(64), lds, s, p);
   int st = rpp_exclusive_scan_u64(sizes, frames, offs, s);
   if (st != RPP_OK) return st;
