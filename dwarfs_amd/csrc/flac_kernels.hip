@@ -290,11 +290,11 @@ __device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint3
   // (a lane's samples run through the partitions in order: its sums go to LDS
   // once per partition, not once per sample)
   {
-    uint32_t cur = ~0u;
+    uint32_t cur = ~0u, q = 0, qend = psz;
     uint64_t acc = 0;
     for (uint32_t i = lane; i < bs; i += kWave) {
       if (i < order) continue;
-      const uint32_t q = i / psz;
+      while (i >= qend) ++q, qend += psz;
       if (q != cur) {
         if (acc) atomicAdd(&sh.psum[cur], (unsigned long long)acc);
         cur = q;
@@ -321,11 +321,11 @@ __device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint3
   for (uint32_t po = 0; po <= pomax; ++po) {
     const uint32_t per = bs >> po;
     const uint32_t* kt = sh.kt + (1u << po) - 1;
-    uint32_t cur = ~0u, k = 0;
+    uint32_t cur = ~0u, k = 0, p = 0, pend = per;
     uint64_t acc = 0;
     for (uint32_t i = lane; i < bs; i += kWave) {
       if (i < order) continue;
-      const uint32_t p = i / per;
+      while (i >= pend) ++p, pend += per;
       if (p != cur) {
         if (acc) atomicAdd(&sh.pbits[po][cur], (unsigned long long)acc);
         cur = p;
@@ -400,13 +400,34 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
       if (i < bs) mine += P.bps;
     }
   } else if (P.type == 2) {
+    // a lane's samples are consecutive: the predictor's history slides in
+    // registers (one LDS read per sample) and the folded residuals are kept
+    // in sh.ures for the emission below (same lane, same slots)
+    const uint32_t i0 = lane * kSpl;
+    int64_t h[4];
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) h[t] = i0 >= t + 1 && i0 - t - 1 < bs ? src_sample(sh, src, i0 - t - 1) >> P.wasted : 0;
+    uint32_t p = min(i0, bs) / per, pend = (p + 1) * per;
     for (uint32_t j = 0; j < kSpl; ++j) {
-      const uint32_t i = lane * kSpl + j;
-      if (i >= bs || i < P.order) continue;
-      const uint32_t p = i / per;
+      const uint32_t i = i0 + j;
+      if (i >= bs) break;
+      const int64_t x = src_sample(sh, src, i) >> P.wasted;
+      int64_t r;
+      switch (P.order) {
+        case 0: r = x; break;
+        case 1: r = x - h[0]; break;
+        case 2: r = x - 2 * h[0] + h[1]; break;
+        case 3: r = x - 3 * h[0] + 3 * h[1] - h[2]; break;
+        default: r = x - 4 * h[0] + 6 * h[1] - 4 * h[2] + h[3]; break;
+      }
+      h[3] = h[2], h[2] = h[1], h[1] = h[0], h[0] = x;
+      if (i < P.order) continue;
+      while (i >= pend) ++p, pend += per;
       if (i == (p == 0 ? P.order : p * per)) mine += pbits;
       const uint32_t k = sh.kpar[src][p];
-      mine += (uint32_t)(fold(fixed_res(sh, src, i, P.order, P.wasted)) >> k) + 1 + k;
+      const uint32_t u = (uint32_t)fold(r);
+      sh.ures[i] = u;
+      mine += (u >> k) + 1 + k;
     }
   }
   uint32_t total;
@@ -435,17 +456,19 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
       at += P.bps;
     }
   } else if (P.type == 2) {
+    const uint32_t i0 = lane * kSpl;
+    uint32_t p = min(i0, bs) / per, pend = (p + 1) * per;
     for (uint32_t j = 0; j < kSpl; ++j) {
-      const uint32_t i = lane * kSpl + j;
+      const uint32_t i = i0 + j;
       if (i >= bs) break;
       if (i < P.order) continue;
-      const uint32_t p = i / per;
+      while (i >= pend) ++p, pend += per;
       const uint32_t k = sh.kpar[src][p];
       if (i == (p == 0 ? P.order : p * per)) {
         put(at, k, pbits);
         at += pbits;
       }
-      const uint64_t u = fold(fixed_res(sh, src, i, P.order, P.wasted));
+      const uint64_t u = sh.ures[i];
       at += (uint32_t)(u >> k);  // the unary zeros
       put(at, (1ull << k) | (u & ((1ull << k) - 1)), k + 1);
       at += k + 1;
