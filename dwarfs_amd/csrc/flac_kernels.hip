@@ -390,48 +390,8 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
   uint32_t head = 8 + P.wasted;
   if (P.type == 0) head += P.bps;
   if (P.type == 2) head += P.order * P.bps + 6;
-  // per-lane bits of its samples
   const uint32_t per = P.type == 2 ? bs >> P.po : bs;
   const uint32_t pbits = P.method ? 5u : 4u;
-  uint32_t mine = 0;
-  if (P.type == 1) {
-    for (uint32_t j = 0; j < kSpl; ++j) {
-      const uint32_t i = lane * kSpl + j;
-      if (i < bs) mine += P.bps;
-    }
-  } else if (P.type == 2) {
-    // a lane's samples are consecutive: the predictor's history slides in
-    // registers (one LDS read per sample) and the folded residuals are kept
-    // in sh.ures for the emission below (same lane, same slots)
-    const uint32_t i0 = lane * kSpl;
-    int64_t h[4];
-#pragma unroll
-    for (uint32_t t = 0; t < 4; ++t) h[t] = i0 >= t + 1 && i0 - t - 1 < bs ? src_sample(sh, src, i0 - t - 1) >> P.wasted : 0;
-    uint32_t p = min(i0, bs) / per, pend = (p + 1) * per;
-    for (uint32_t j = 0; j < kSpl; ++j) {
-      const uint32_t i = i0 + j;
-      if (i >= bs) break;
-      const int64_t x = src_sample(sh, src, i) >> P.wasted;
-      int64_t r;
-      switch (P.order) {
-        case 0: r = x; break;
-        case 1: r = x - h[0]; break;
-        case 2: r = x - 2 * h[0] + h[1]; break;
-        case 3: r = x - 3 * h[0] + 3 * h[1] - h[2]; break;
-        default: r = x - 4 * h[0] + 6 * h[1] - 4 * h[2] + h[3]; break;
-      }
-      h[3] = h[2], h[2] = h[1], h[1] = h[0], h[0] = x;
-      if (i < P.order) continue;
-      while (i >= pend) ++p, pend += per;
-      if (i == (p == 0 ? P.order : p * per)) mine += pbits;
-      const uint32_t k = sh.kpar[src][p];
-      const uint32_t u = (uint32_t)fold(r);
-      sh.ures[i] = u;
-      mine += (u >> k) + 1 + k;
-    }
-  }
-  uint32_t total;
-  uint32_t at = pos + head + wave_excl_sum(mine, total);
   if (lane == 0) {
     const uint32_t type6 = P.type == 0 ? 0u : P.type == 1 ? 1u : 8u + P.order;
     put(pos, (type6 << 1) | (P.wasted ? 1u : 0u), 8);
@@ -448,34 +408,40 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
       put(q, (P.method << 4) | P.po, 6);
     }
   }
+  // samples in rows of 64 (lane l: sample 64 j + l, LDS reads without bank
+  // conflicts); a row's codes are placed by one DPP prefix sum
+  uint32_t at = pos + head;
   if (P.type == 1) {
-    for (uint32_t j = 0; j < kSpl; ++j) {
-      const uint32_t i = lane * kSpl + j;
-      if (i >= bs) break;
-      put(at, (uint64_t)(src_sample(sh, src, i) >> P.wasted), P.bps);
-      at += P.bps;
+    for (uint32_t j0 = 0; j0 < bs; j0 += kWave) {
+      const uint32_t i = j0 + lane;
+      if (i < bs) put(at + lane * P.bps, (uint64_t)(src_sample(sh, src, i) >> P.wasted), P.bps);
+      at += min(kWave, bs - j0) * P.bps;
     }
   } else if (P.type == 2) {
-    const uint32_t i0 = lane * kSpl;
-    uint32_t p = min(i0, bs) / per, pend = (p + 1) * per;
-    for (uint32_t j = 0; j < kSpl; ++j) {
-      const uint32_t i = i0 + j;
-      if (i >= bs) break;
-      if (i < P.order) continue;
-      while (i >= pend) ++p, pend += per;
-      const uint32_t k = sh.kpar[src][p];
-      if (i == (p == 0 ? P.order : p * per)) {
-        put(at, k, pbits);
-        at += pbits;
+    uint32_t p = 0, pend = per;
+    for (uint32_t j0 = 0; j0 < bs; j0 += kWave) {
+      const uint32_t i = j0 + lane;
+      uint32_t len = 0, k = 0, hb = 0;
+      uint64_t u = 0;
+      if (i < bs && i >= P.order) {
+        while (i >= pend) ++p, pend += per;
+        k = sh.kpar[src][p];
+        hb = i == (p == 0 ? P.order : p * per) ? pbits : 0u;
+        u = fold(fixed_res(sh, src, i, P.order, P.wasted));
+        len = hb + (uint32_t)(u >> k) + 1 + k;
       }
-      const uint64_t u = sh.ures[i];
-      at += (uint32_t)(u >> k);  // the unary zeros
-      put(at, (1ull << k) | (u & ((1ull << k) - 1)), k + 1);
-      at += k + 1;
+      uint32_t tot;
+      uint32_t a = at + wave_excl_sum(len, tot);
+      if (len) {
+        if (hb) put(a, k, pbits);
+        a += hb + (uint32_t)(u >> k);  // the unary zeros
+        put(a, (1ull << k) | (u & ((1ull << k) - 1)), k + 1);
+      }
+      at += tot;
     }
   }
   __syncthreads();
-  return pos + head + total;
+  return at;
 }
 
 // Moves the window's complete words to the slot (byte order of the stream),
