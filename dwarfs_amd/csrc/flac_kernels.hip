@@ -18,21 +18,25 @@
 // sum of |residual| (orders 0-4, as libFLAC's fixed-order estimate) and the
 // Rice partition order (0-5) and per-partition parameters with the fewest
 // bits, and for two channels the cheapest of the four channel assignments;
-// then every lane writes its samples' codes into an LDS bit window at
-// positions from one wave prefix sum (MSB-first words, byte-swapped on the way
+// then the codes of each row of 64 samples are placed by one wave prefix sum
+// and OR-ed into an LDS bit window (MSB-first words, byte-swapped on the way
 // out).  Frames go to worst-case slots, are packed back to back
 // (rpp_flac_pack_kernel) and get their CRC-16 on the packed bytes
 // (rpp_flac_crc_kernel: per-lane CRCs combined by GF(2) shifts).
 //
 // Decode (rpp_flac_decode): frames are not indexed, so every byte that starts
 // a valid frame header (sync, fields, CRC-8) is a candidate
-// (rpp_flac_scan_kernel); each candidate is decoded by one lane into a
-// scratch slot and its CRC-16 checked (rpp_flac_frame_kernel,
-// rpp_flac_crc_kernel); one lane walks the chain of frames from the first
-// (rpp_flac_chain_kernel) and the chained frames' samples are placed
+// (rpp_flac_scan_kernel); each candidate is decoded by one wave into a
+// scratch slot (rpp_flac_frame_wave_kernel: Rice partitions parsed by all 64
+// lanes at once, see there; rpp_flac_frame_kernel, one lane per candidate,
+// takes what the wave decoder leaves) and its CRC-16 checked
+// (rpp_flac_crc_kernel); the links between valid candidates are checked in
+// parallel against their coded numbers (rpp_flac_link_kernel), one lane walks
+// the chain of frames from the first only when a link fails
+// (rpp_flac_chain_kernel), and the chained frames' samples are placed
 // (rpp_flac_place_kernel).  A false candidate (random bytes passing sync,
-// CRC-8 and CRC-16) can only matter if it lies on the chain, which it cannot:
-// the chain only visits the positions where the previous frame ends.
+// CRC-8 and CRC-16) is never placed: the chain only visits the positions
+// where the previous frame ends.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
