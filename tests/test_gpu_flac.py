@@ -132,3 +132,14 @@ def test_corrupt_frame_is_an_error():
         FL.decompress(bytes(comp))
     with pytest.raises(RuntimeError, match="FLAC"):
         FL.decompress(bytes(comp[: len(comp) - 100]))
+
+
+def test_trailing_bytes_after_the_last_frame():
+    """Bytes after the frame holding the last sample are ignored (the decoder stops at the stream's sample
+    count, as the chain walk does): the parallel link check cannot place the last frame, so the serial walk
+    runs."""
+    x = sines(2, 3 * 4096 + 100, 16)
+    data = pcm_bytes(x, E.Little, S.Signed, Pd.Msb, 2, 16)
+    comp = FL.FlacBlockCompressor().compress(data, meta(E.Little, S.Signed, Pd.Msb, 2, 2, 16))
+    assert FL.decompress(comp + bytes(7)) == data
+    assert FL.decompress(comp + b"\xff\xf8" + bytes(30)) == data
