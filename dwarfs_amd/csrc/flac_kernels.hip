@@ -919,8 +919,9 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d) {
 // parses that meet continue identically), which Rice codes reach within a
 // few codes.  A wave prefix sum over the lanes' code counts then gives each
 // code its sample index.  Residuals, warm-up and verbatim samples go to LDS
-// ([channel][max_bs] int32); afterwards lane ch runs channel ch's predictor
-// (fixed or LPC) over its column, and the wave writes the planar slot.
+// ([channel][max_bs] int32); then fixed predictors run as wave prefix sums,
+// lane ch runs channel ch's LPC predictor over its column, and the wave
+// writes the planar slot.
 // Anything this path does not take (32-bit samples, a block too large for
 // LDS, a code longer than the window's look-ahead, a residual or sample
 // beyond 32 bits) is marked in cand_redo and left to the lane decoder.
@@ -1190,27 +1191,43 @@ __device__ int wave_subframe(FWin& f, uint64_t& pos, int32_t* s, uint32_t bs, ui
   return pos > 8 * f.lim ? kSfBad : kSfOk;
 }
 
-// Channel prediction over its LDS column, one lane; false: a sample beyond 32 bits
+// A fixed predictor of order o over one LDS column, all lanes: the residual
+// is the o-th backward difference of the samples, so the samples are o
+// prefix sums of it, level j (o-1 .. 0) starting from D^j x at j taken from
+// the warm-up samples.  Modulo 2^32, as the output is (the lane decoder's
+// int64 values truncated to int32 give the same bits).
+__device__ void fixed_column_scans(int32_t* s, uint32_t bs, uint32_t o) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t x[4] = {0, 0, 0, 0}, c[4];
+  for (uint32_t t = 0; t < o; ++t) x[t] = (uint32_t)s[t];
+  c[0] = x[0];
+  c[1] = x[1] - x[0];
+  c[2] = x[2] - 2 * x[1] + x[0];
+  c[3] = x[3] - 3 * x[2] + 3 * x[1] - x[0];
+  __syncthreads();
+  for (int j = (int)o - 1; j >= 0; --j) {
+    uint32_t carry = 0;
+    for (uint32_t r0 = (uint32_t)j; r0 < bs; r0 += kWave) {
+      const uint32_t i = r0 + lane;
+      int v = i == (uint32_t)j ? (int)c[j] : i < bs ? s[i] : 0;
+      v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+      if (i < bs) s[i] = (int32_t)(carry + (uint32_t)v);
+      carry += (uint32_t)__builtin_amdgcn_readlane(v, kWave - 1);
+    }
+    __syncthreads();
+  }
+}
+
+// LPC prediction over one LDS column, one lane; false: a sample beyond 32 bits
 __device__ bool predict_column(int32_t* s, uint32_t bs, const SubInfo& inf) {
   const uint32_t o = inf.order;
   bool ok = true;
-  if (inf.kind == 1) {
-    int64_t h0 = o > 0 ? s[o - 1] : 0, h1 = o > 1 ? s[o - 2] : 0, h2 = o > 2 ? s[o - 3] : 0, h3 = o > 3 ? s[o - 4] : 0;
-    for (uint32_t i = o; i < bs; ++i) {
-      const int64_t r = s[i];
-      int64_t v;
-      switch (o) {
-        case 0: v = r; break;
-        case 1: v = r + h0; break;
-        case 2: v = r + 2 * h0 - h1; break;
-        case 3: v = r + 3 * h0 - 3 * h1 + h2; break;
-        default: v = r + 4 * h0 - 6 * h1 + 4 * h2 - h3; break;
-      }
-      ok &= v == (int64_t)(int32_t)v;
-      s[i] = (int32_t)v;
-      h3 = h2, h2 = h1, h1 = h0, h0 = v;
-    }
-  } else if (inf.kind == 2) {
+  if (inf.kind == 2) {
     const int32_t sh = inf.shift;
     for (uint32_t i = o; i < bs; ++i) {
       int64_t acc = 0;
@@ -1253,6 +1270,8 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(FlacDecParams d
     if (st != kSfOk) return;
   }
   __syncthreads();
+  for (uint32_t ch = 0; ch < C; ++ch)
+    if (info[ch].kind == 1 && info[ch].order) fixed_column_scans(smp + (uint64_t)ch * mb, bs, info[ch].order);
   if (lane < C && !predict_column(smp + (uint64_t)lane * mb, bs, info[lane])) wide = 1;
   __syncthreads();
   if (wide) {
