@@ -1223,21 +1223,45 @@ __device__ void fixed_column_scans(int32_t* s, uint32_t bs, uint32_t o) {
   }
 }
 
-// LPC prediction over one LDS column, one lane; false: a sample beyond 32 bits
-__device__ bool predict_column(int32_t* s, uint32_t bs, const SubInfo& inf) {
+// LPC prediction over one LDS column, one lane, with N >= order taps held in
+// registers (coefficients zero past the order, history newest first) so that
+// only the newest sample's product is on the per-sample dependency chain;
+// false: a sample beyond 32 bits
+// (64-bit products: a 32-bit accumulation where libFLAC's bound allows it
+// measured no faster, v_mul_lo_u32 issuing at the 64-bit multiply's rate)
+template <uint32_t N>
+__device__ bool lpc_column(int32_t* s, uint32_t bs, const SubInfo& inf) {
   const uint32_t o = inf.order;
+  const int32_t sh = inf.shift;
+  int32_t c[N], h[N];
+#pragma unroll
+  for (uint32_t j = 0; j < N; ++j) {
+    c[j] = j < o ? inf.coef[j] : 0;
+    h[j] = j < o ? s[o - 1 - j] : 0;
+  }
   bool ok = true;
-  if (inf.kind == 2) {
-    const int32_t sh = inf.shift;
-    for (uint32_t i = o; i < bs; ++i) {
-      int64_t acc = 0;
-      for (uint32_t j = 0; j < o; ++j) acc += (int64_t)inf.coef[j] * s[i - 1 - j];
-      const int64_t v = (int64_t)s[i] + (acc >> sh);
-      ok &= v == (int64_t)(int32_t)v;
-      s[i] = (int32_t)v;
-    }
+  int32_t r = o < bs ? s[o] : 0;
+  for (uint32_t i = o; i < bs; ++i) {
+    const int32_t rn = i + 1 < bs ? s[i + 1] : 0;
+    int64_t acc = 0;
+#pragma unroll
+    for (uint32_t j = N - 1; j > 0; --j) acc += (int64_t)c[j] * h[j];
+    acc += (int64_t)c[0] * h[0];
+    const int64_t v = (int64_t)r + (acc >> sh);
+    ok &= v == (int64_t)(int32_t)v;
+    s[i] = (int32_t)v;
+#pragma unroll
+    for (uint32_t j = N - 1; j > 0; --j) h[j] = h[j - 1];
+    h[0] = (int32_t)v;
+    r = rn;
   }
   return ok;
+}
+__device__ bool predict_column(int32_t* s, uint32_t bs, const SubInfo& inf) {
+  if (inf.kind != 2) return true;
+  if (inf.order <= 8) return lpc_column<8>(s, bs, inf);
+  if (inf.order <= 12) return lpc_column<12>(s, bs, inf);
+  return lpc_column<32>(s, bs, inf);
 }
 
 __global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(FlacDecParams d) {

@@ -89,3 +89,36 @@ for channels, nbytes, bits in ((2, 2, 16), (8, 4, 24)):
                       "encode_kernels_MiBps": round(mib / tk_e, 1), "decode_kernels_MiBps": round(mib / tk_d, 1),
                       "cpu_oracle_encode_MiBps_1t": round(mib / tc_e, 1),
                       "cpu_oracle_decode_MiBps_1t": round(mib / tc_d, 1)}), flush=True)
+
+# libFLAC-like streams: every subframe LPC of order 8 (libFLAC level 5 codes up to order 8; its
+# streams are what a DwarFS image made by the reference holds), written by the CPU restatement;
+# the GPU decode kernels alone
+channels, bits = 2, 16
+n = (16 << 20) // (channels * 2)
+rng = np.random.default_rng(1)
+x = (sines(channels, n, bits).astype(np.int64) + rng.integers(-8, 9, n * channels))
+x = np.clip(x, -(1 << (bits - 1)), (1 << (bits - 1)) - 1).astype(np.int32)
+stream = F.encode(x, channels, bits, 4096, F.EncodeOptions(subframe_type="lpc", lpc_order=8, lpc_precision=12))
+info, at = FL.parse_stream(stream)
+L = N.lib()
+body = torch.from_numpy(np.frombuffer(stream, np.uint8)[at:].copy()).to(dev)
+y = torch.empty(n * channels, dtype=torch.int32, device=dev)
+st = torch.zeros(1, dtype=torch.int32, device=dev)
+nc = torch.zeros(1, dtype=torch.int32, device=dev)
+mc = n // 4096 + body.numel() // 4096 + 64
+wdb = int(L.rpp_flac_decode_workspace_bytes(body.numel(), channels, 4096, mc))
+wd = torch.empty(wdb, dtype=torch.uint8, device=dev)
+s = torch.cuda.current_stream()
+args = (C.c_void_p(body.data_ptr()), body.numel(), channels, bits, 4096, n, C.c_void_p(y.data_ptr()),
+        C.c_void_p(st.data_ptr()), mc, C.c_void_p(wd.data_ptr()), wdb, C.c_void_p(nc.data_ptr()), C.c_void_p(s.cuda_stream))
+L.rpp_flac_decode(*args)
+torch.cuda.synchronize()
+assert int(st.item()) == 0 and np.array_equal(y.cpu().numpy(), x)
+t0 = time.perf_counter()
+for _ in range(5):
+    L.rpp_flac_decode(*args)
+torch.cuda.synchronize()
+tk = (time.perf_counter() - t0) / 5
+print(json.dumps({"case": "flac-lpc8-stream", "block_MiB": 16.0, "channels": channels, "bits": bits,
+                  "ratio": round(len(stream) / (n * channels * 2), 4),
+                  "decode_kernels_MiBps": round(16 / tk, 1)}), flush=True)
