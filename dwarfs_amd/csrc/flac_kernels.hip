@@ -46,7 +46,6 @@ namespace {
 
 constexpr uint32_t kFlacBlock = 4096;   // samples per encoded frame
 constexpr uint32_t kWave = 64;
-constexpr uint32_t kSpl = kFlacBlock / kWave;  // samples per lane
 constexpr uint32_t kMaxPo = 5;          // partition orders 0..5 (libFLAC level 5: -r 5)
 constexpr uint32_t kWinWords = 4352;    // LDS bit window: one subframe (4096 x 33 bits) + slack
 constexpr uint32_t kFlacWaveLds = 144 * 1024;  // dynamic LDS cap of the wave decoder
