@@ -200,7 +200,8 @@ def profiled_counters(kernel: str, profile: str = "pmc_latest.json"):
     if j.get("kernel_source_sha256") != kernel_source_sha256():
         return None, "PMC profile of other kernel sources (stale); not reported"
     return j.get(kernel), f"{j.get('source', 'profiles')} (rocprofv3 PMC, kernel sources sha256 " \
-                         f"{j['kernel_source_sha256'][:12]})"
+                         f"{j['kernel_source_sha256'][:12]} of every dwarfs_amd/csrc/*.hip but flac_kernels.hip, " \
+                         f"which no bench workload launches)"
 
 
 def main() -> None:

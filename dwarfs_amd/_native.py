@@ -209,7 +209,7 @@ def lib() -> C.CDLL:
         L.rpp_flac_encode_workspace_bytes.restype = C.c_uint64
         L.rpp_flac_encode.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, P]
         L.rpp_flac_encode.restype = C.c_int
-        L.rpp_flac_decode_workspace_bytes.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.rpp_flac_decode_workspace_bytes.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.rpp_flac_decode_workspace_bytes.restype = C.c_uint64
         L.rpp_flac_decode.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, P, P,
                                       C.c_uint32, P, C.c_uint64, P, P]

@@ -1494,11 +1494,13 @@ int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channe
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 
-uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t max_blocksize,
+uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t bps, uint32_t max_blocksize,
                                          uint32_t max_candidates) {
   const uint64_t mc = max_candidates;
   const uint64_t per = (uint64_t)max_blocksize * channels;
-  return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 8) + 64 + mc * per * 8 + 256;
+  // (the take() layout below, 16-byte aligned pieces; per-candidate scratch
+  // of int32 samples, int64 for 32-bit streams)
+  return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 8) + 7 * 16 + 16 + mc * per * (bps == 32 ? 8 : 4) + 256;
 }
 
 int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
@@ -1509,7 +1511,7 @@ int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels,
     return RPP_UNSUPPORTED_CONFIG;
   if (!d_status || !d_ncand) return RPP_INVALID_ARGUMENT;
   hipStream_t s = (hipStream_t)stream;
-  if (workspace_bytes < rpp_flac_decode_workspace_bytes(nbytes, channels, max_blocksize, max_candidates))
+  if (workspace_bytes < rpp_flac_decode_workspace_bytes(nbytes, channels, bps, max_blocksize, max_candidates))
     return RPP_INVALID_ARGUMENT;
   if ((nbytes && !d_frames) || (nsamples && !d_out) || !d_workspace || max_candidates == 0)
     return RPP_INVALID_ARGUMENT;

@@ -69,7 +69,10 @@ void maybe_fail_launch() {
   for (uint32_t n = g_launch_faults.load(); n;)
     if (g_launch_faults.compare_exchange_weak(n, n - 1)) throw std::runtime_error("ricepp_amd: injected launch failure");
 }
-std::atomic<uint64_t> g_stage_ns{0}, g_device_ns{0}, g_finish_ns{0};
+std::atomic<uint64_t> g_stage_ns{0}, g_device_ns{0}, g_finish_ns{0}, g_device_event_ns{0};
+// set once shutdown_facade() has begun: the context pool makes no more HIP
+// calls (contexts returned afterwards are leaked, new ones refused)
+std::atomic<bool> g_shutdown{false};
 inline uint64_t now_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch())
@@ -122,8 +125,15 @@ class device_ctx {
       if (g_ctx_faults.compare_exchange_weak(n, n - 1)) throw std::runtime_error("hipStreamCreate: injected failure");
     device_guard g{dev_};
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    // the batch's end (polled by the batch_queue)
-    if (hipEventCreateWithFlags(&event_, hipEventDisableTiming) != hipSuccess) {
+    // the batch's start and end on the device's clock; a host thread waiting
+    // for the end blocks (hipEventBlockingSync) instead of spinning on a core
+    // the callers need
+    if (hipEventCreateWithFlags(&start_, hipEventDefault) != hipSuccess) {
+      (void)hipStreamDestroy(stream_);
+      throw std::runtime_error("ricepp_amd: hipEventCreateWithFlags failed");
+    }
+    if (hipEventCreateWithFlags(&event_, hipEventBlockingSync) != hipSuccess) {
+      (void)hipEventDestroy(start_);
       (void)hipStreamDestroy(stream_);
       throw std::runtime_error("ricepp_amd: hipEventCreateWithFlags failed");
     }
@@ -136,6 +146,7 @@ class device_ctx {
   int kind() const { return kind_; }
   hipStream_t stream() const { return stream_; }
   hipEvent_t event() const { return event_; }
+  hipEvent_t start_event() const { return start_; }
   uint8_t* dev(size_t bytes) { return grow_dev(dbuf_, dcap_, bytes); }
   uint8_t* workspace(size_t bytes) { return grow_dev(wbuf_, wcap_, bytes); }
   uint8_t* pin_in(size_t bytes) { return grow_pinned(hin_, hin_cap_, bytes); }
@@ -158,6 +169,7 @@ class device_ctx {
     for (uint8_t* q : {dbuf_, wbuf_})
       if (q) (void)hipFree(q);
     (void)hipEventDestroy(event_);
+    (void)hipEventDestroy(start_);
     (void)hipStreamDestroy(stream_);
     hin_ = hout_ = dbuf_ = wbuf_ = nullptr;
     hin_cap_ = hout_cap_ = dcap_ = wcap_ = 0;
@@ -215,6 +227,7 @@ class device_ctx {
   int kind_;
   hipStream_t stream_ = nullptr;
   hipEvent_t event_ = nullptr;
+  hipEvent_t start_ = nullptr;
   uint8_t* dbuf_ = nullptr;
   size_t dcap_ = 0;
   uint8_t* wbuf_ = nullptr;
@@ -238,6 +251,7 @@ class ctx_pool {
   // handed from one to the other regrew them (hipFree / hipHostFree
   // synchronise the device) -- one pool per kind keeps them grown
   device_ctx* acquire(int dev, int kind) {
+    if (g_shutdown.load(std::memory_order_acquire)) throw std::runtime_error("ricepp_amd: facade shut down");
     {
       std::lock_guard<std::mutex> lk(mu_);
       auto& v = free_[{dev, kind}];
@@ -254,6 +268,7 @@ class ctx_pool {
   // or destroys it when its stream is in error.  Never called with a queue
   // lock held: the drain and the trim may synchronise.
   void release(device_ctx* c) {
+    if (g_shutdown.load(std::memory_order_acquire)) return;  // (no HIP calls once shutting down: leaked)
     try {
       device_guard g{c->device()};
       if (!c->drain()) {
@@ -262,7 +277,9 @@ class ctx_pool {
         return;
       }
       c->trim();
-    } catch (...) {  // (hipSetDevice failed: keep the context out of the pool)
+    } catch (...) {  // (hipSetDevice failed: the context cannot be trusted; freed, errors ignored)
+      c->destroy();
+      delete c;
       return;
     }
     std::lock_guard<std::mutex> lk(mu_);
@@ -299,9 +316,11 @@ class ctx_lease {
 //     on the device (an idle queue launches a lone call at once, a busy one
 //     gathers everything that arrives meanwhile), or when it is full;
 //   * the queue's driver thread launches a closed batch once every caller has
-//     copied in (copies and kernels enqueued, an event recorded), polls the
-//     events of the batches in flight, and publishes each batch's results
-//     with one wake-up of all its callers;
+//     copied in (copies and kernels enqueued between two events);
+//   * the queue's waiter thread blocks on the end event of the oldest batch
+//     in flight (a blocking-sync event: no core spins), then takes every
+//     other batch in flight that has finished too, and publishes each batch's
+//     results with one wake-up of all its callers;
 //   * every caller copies its own result out; the last one returns the
 //     context to the pool.
 // So a call costs one reservation, two copies and one futex wait, and the
@@ -354,6 +373,9 @@ constexpr size_t kBatchOut = size_t{16} << 20;
 // copies instead of one launch each (block_cache.cpp:628-706 issues them
 // from a worker pool).
 constexpr size_t kLargeJoin = 8;
+// ... as long as the batch's staging stays within this (a 1 GiB block,
+// mkdwarfs -S 29, gets a batch of its own: pinned staging of its size only)
+constexpr size_t kLargeJoinBudget = size_t{256} << 20;
 // encode batches whose worst-case output exceeds this go out by a DMA copy of
 // the slots instead of being packed into mapped host memory by a kernel
 // (set_facade_pack_limit changes it for benchmarks; default: always pack)
@@ -371,11 +393,19 @@ class batch_queue {
 
   void run(request& r) {
     std::unique_lock<std::mutex> lk(mu_);
-    if (!driver_started_) {
-      std::thread([this] { drive(); }).detach();  // (lives as long as the queue: forever)
-      driver_started_ = true;
+    if (stopping_) throw std::runtime_error("ricepp_amd: facade shut down");
+    if (!driver_.joinable()) {
+      driver_ = std::thread([this] { drive(); });
+      waiter_ = std::thread([this] { wait_loop(); });
     }
-    batch* b = reserve(lk, r);  // (may throw: nothing holds r yet)
+    ++active_;
+    batch* b = nullptr;
+    try {
+      b = reserve(lk, r);
+    } catch (...) {  // (nothing holds r yet)
+      leave(lk);
+      throw;
+    }
     std::vector<device_ctx*> unused;
     unused.swap(discarded_);
     lk.unlock();
@@ -383,17 +413,38 @@ class batch_queue {
     if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
     lk.lock();
     ++b->staged;
-    if (!b->closed && inflight_ < g_max_active.load(std::memory_order_relaxed)) close(b);
+    if (!b->closed && (stopping_ || inflight_ < g_max_active.load(std::memory_order_relaxed))) close(b);
     else if (b->closed && b->staged == b->reqs.size()) make_ready(b);
     lk.unlock();
     while (!b->done.load(std::memory_order_acquire)) b->done.wait(0, std::memory_order_acquire);
     if (r.status == RPP_OK && r.result_bytes) std::memcpy(r.out, r.pin_out, r.result_bytes);
-    if (b->finished.fetch_add(1, std::memory_order_acq_rel) + 1 == b->reqs.size()) {
-      lk.lock();
-      device_ctx* c = release(b);
-      lk.unlock();
-      ctx_pool::get().release(c);
-    }
+    device_ctx* c = nullptr;
+    const bool last = b->finished.fetch_add(1, std::memory_order_acq_rel) + 1 == b->reqs.size();
+    lk.lock();
+    if (last) c = release(b);
+    lk.unlock();
+    if (c) ctx_pool::get().release(c);
+    lk.lock();
+    leave(lk);
+  }
+
+  // Stops the queue (shutdown_facade): batches in flight complete, batches
+  // not launched fail, later calls throw; joins the queue's threads and
+  // waits (bounded) for the callers inside run() to leave it.
+  void shutdown() {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (stopping_) return;
+    stopping_ = true;
+    // (an open batch whose callers have all copied in goes out now, and
+    // fails; one still being copied into is closed by its last caller)
+    if (open_ && !open_->reqs.empty() && open_->staged == open_->reqs.size()) close(open_);
+    drv_cv_.notify_all();
+    wait_cv_.notify_all();
+    lk.unlock();
+    if (driver_.joinable()) driver_.join();
+    if (waiter_.joinable()) waiter_.join();
+    lk.lock();
+    quiet_cv_.wait_for(lk, std::chrono::seconds(5), [&] { return active_ == 0; });
   }
 
  private:
@@ -442,7 +493,10 @@ class batch_queue {
     auto* b = new batch;
     try {
       c = ctx_pool::get().acquire(dev_, encode_ ? 0 : 1);
-      const size_t join = need_out(r) > kBatchOut / 4 || need_in(r) > kBatchIn / 4 ? kLargeJoin : 1;
+      const size_t big = std::max(need_in(r), need_out(r));
+      const size_t join = need_out(r) > kBatchOut / 4 || need_in(r) > kBatchIn / 4
+                              ? std::clamp<size_t>(kLargeJoinBudget / big, 1, kLargeJoin)
+                              : 1;
       b->in_cap = std::max(kBatchIn, join * need_in(r) + arrays_in(join));
       b->out_cap = std::max(kBatchOut, join * need_out(r) + arrays_out(join));
       device_guard g{dev_};
@@ -487,70 +541,104 @@ class batch_queue {
   }
 
   // (lk held) closed and every input copied in: the driver launches it
+  // (once the queue is stopping, nothing more is launched)
   void make_ready(batch* b) {
+    if (stopping_) {
+      fail(b, "ricepp_amd: facade shut down");
+      return;
+    }
     ready_.push_back(b);
-    if (driver_idle_) drv_cv_.notify_one();
+    drv_cv_.notify_one();
   }
 
-  // The driver thread: launches ready batches, polls the oldest batch in
-  // flight, publishes results.
+  // (lk held) a caller leaves run()
+  void leave(std::unique_lock<std::mutex>&) {
+    if (--active_ == 0 && stopping_) quiet_cv_.notify_all();
+  }
+
+  // The driver thread: launches ready batches (the waiter completes them).
   void drive() {
     (void)hipSetDevice(dev_);
     std::unique_lock<std::mutex> lk(mu_);
-    uint32_t polls = 0;
     for (;;) {
-      while (!ready_.empty()) {
-        batch* b = ready_.front();
-        ready_.pop_front();
-        b->t_launch = now_ns();
-        lk.unlock();
-        std::string err;
-        try {
-          if (encode_) launch_encode(*b);
-          else launch_decode(*b);
-          hip_check(hipEventRecord(b->ctx->event(), b->ctx->stream()), "hipEventRecord");
-        } catch (std::exception const& e) {
-          err = e.what();
-          // part of the batch may be on the stream already (copies, kernels
-          // writing the mapped pinned output): let it finish before the
-          // callers are released and the buffers reused (a stream in error
-          // makes release() destroy the context instead of pooling it)
+      drv_cv_.wait(lk, [&] { return !ready_.empty() || stopping_; });
+      if (stopping_) {
+        while (!ready_.empty()) {
+          batch* b = ready_.front();
+          ready_.pop_front();
+          fail(b, "ricepp_amd: facade shut down");
+        }
+        driver_done_ = true;
+        wait_cv_.notify_all();
+        return;
+      }
+      batch* b = ready_.front();
+      ready_.pop_front();
+      b->t_launch = now_ns();
+      lk.unlock();
+      std::string err;
+      try {
+        hip_check(hipEventRecord(b->ctx->start_event(), b->ctx->stream()), "hipEventRecord");
+        if (encode_) launch_encode(*b);
+        else launch_decode(*b);
+        hip_check(hipEventRecord(b->ctx->event(), b->ctx->stream()), "hipEventRecord");
+      } catch (std::exception const& e) {
+        err = e.what();
+        // part of the batch may be on the stream already (copies, kernels
+        // writing the mapped pinned output): let it finish before the
+        // callers are released and the buffers reused (a stream in error
+        // makes release() destroy the context instead of pooling it)
+        (void)b->ctx->drain();
+      }
+      lk.lock();
+      if (err.empty()) {
+        flight_.push_back(b);
+        wait_cv_.notify_one();
+      } else {
+        fail(b, err);
+      }
+    }
+  }
+
+  // The waiter thread: blocks on the end event of the oldest batch in flight,
+  // then also takes the later ones (other streams) that have finished, and
+  // publishes their results.  Only this thread removes batches from flight_.
+  void wait_loop() {
+    (void)hipSetDevice(dev_);
+    std::unique_lock<std::mutex> lk(mu_);
+    std::vector<batch*> cand;
+    std::vector<std::pair<batch*, hipError_t>> fin;
+    for (;;) {
+      wait_cv_.wait(lk, [&] { return !flight_.empty() || (stopping_ && driver_done_); });
+      if (flight_.empty()) return;  // (stopping, and the driver launches nothing more)
+      cand.assign(flight_.begin(), flight_.end());
+      lk.unlock();
+      fin.clear();
+      for (size_t i = 0; i < cand.size(); ++i) {
+        batch* b = cand[i];
+        // the oldest: wait for it; the others: only if already done
+        const hipError_t e = i == 0 ? hipEventSynchronize(b->ctx->event()) : hipEventQuery(b->ctx->event());
+        if (e == hipErrorNotReady) continue;
+        if (e == hipSuccess) {
+          float ms = 0.f;
+          if (hipEventElapsedTime(&ms, b->ctx->start_event(), b->ctx->event()) == hipSuccess)
+            g_device_event_ns.fetch_add(static_cast<uint64_t>(double(ms) * 1e6), std::memory_order_relaxed);
+        } else {
           (void)b->ctx->drain();
         }
-        lk.lock();
-        if (err.empty()) {
-          flight_.push_back(b);
-        } else {
-          fail(b, err);
-        }
+        fin.emplace_back(b, e);
       }
-      if (flight_.empty()) {
-        driver_idle_ = true;
-        drv_cv_.wait(lk);
-        driver_idle_ = false;
-        continue;
-      }
-      batch* b = flight_.front();
-      lk.unlock();
-      const hipError_t e = hipEventQuery(b->ctx->event());
-      if (e == hipErrorNotReady) {
-        // (yielding the core; after a few ms of one batch the poll backs off)
-        if (++polls < 4096) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(50));
-        lk.lock();
-        continue;
-      }
-      polls = 0;
-      if (e != hipSuccess) (void)b->ctx->drain();
       lk.lock();
-      flight_.pop_front();
-      if (e != hipSuccess) {
-        fail(b, std::string("ricepp_amd: hipEventQuery: ") + hipGetErrorString(e));
-        continue;
+      for (auto [b, e] : fin) {
+        flight_.erase(std::find(flight_.begin(), flight_.end(), b));
+        if (e != hipSuccess) {
+          fail(b, std::string("ricepp_amd: hipEventSynchronize: ") + hipGetErrorString(e));
+          continue;
+        }
+        if (encode_) results_encode(*b);
+        else results_decode(*b);
+        complete(b);
       }
-      if (encode_) results_encode(*b);
-      else results_decode(*b);
-      complete(b);
     }
   }
 
@@ -567,6 +655,7 @@ class batch_queue {
   // device slot may close now
   void complete(batch* b) {
     b->t_done = now_ns();
+    if (!b->t_launch) b->t_launch = b->t_done;  // (failed before its launch)
     --inflight_;
     g_stage_ns.fetch_add(b->t_launch - b->t_close, std::memory_order_relaxed);
     g_device_ns.fetch_add(b->t_done - b->t_launch, std::memory_order_relaxed);
@@ -756,7 +845,9 @@ class batch_queue {
   bool encode_;
   std::mutex mu_;
   std::condition_variable res_cv_;  // callers waiting for a batch with room
-  std::condition_variable drv_cv_;  // the driver, when it has nothing in flight
+  std::condition_variable drv_cv_;  // the driver, waiting for a ready batch
+  std::condition_variable wait_cv_;  // the waiter, waiting for a batch in flight
+  std::condition_variable quiet_cv_;  // shutdown, waiting for callers to leave run()
   batch* open_ = nullptr;           // the batch taking new requests
   std::vector<batch*> spare_;       // opened concurrently, not yet taking requests
   std::deque<batch*> ready_;        // closed and staged, to be launched
@@ -764,16 +855,42 @@ class batch_queue {
   std::vector<device_ctx*> discarded_;  // contexts of discarded batches, to pool unlocked
   int inflight_ = 0;                // closed, not yet completed
   int alive_ = 0;
-  bool driver_started_ = false, driver_idle_ = false;
+  int active_ = 0;                  // callers inside run()
+  bool stopping_ = false, driver_done_ = false;
+  std::thread driver_, waiter_;
 };
 
+// The queues (intentionally never destroyed: their threads are stopped by
+// shutdown_facade(), which std::atexit runs before the HIP runtime's own
+// teardown -- it is registered after the runtime has come up).
+struct queue_registry {
+  std::mutex mu;
+  std::map<std::tuple<int, uint32_t, uint32_t, uint32_t, uint32_t, bool>, batch_queue*> queues;
+};
+queue_registry& registry() {
+  static auto* r = new queue_registry;
+  return *r;
+}
+
+void shutdown_all() {
+  g_shutdown.store(true, std::memory_order_release);
+  std::vector<batch_queue*> qs;
+  {
+    std::lock_guard<std::mutex> lk(registry().mu);
+    for (auto& [k, q] : registry().queues) qs.push_back(q);
+  }
+  for (batch_queue* q : qs) q->shutdown();
+}
+
 batch_queue& queue_for(int dev, rpp_config const& c, bool encode) {
-  static std::mutex mu;
-  static auto* queues = new std::map<std::tuple<int, uint32_t, uint32_t, uint32_t, uint32_t, bool>, batch_queue*>;
-  std::lock_guard<std::mutex> lk(mu);
+  auto& reg = registry();
+  std::lock_guard<std::mutex> lk(reg.mu);
+  if (g_shutdown.load(std::memory_order_acquire)) throw std::runtime_error("ricepp_amd: facade shut down");
+  static const bool registered = [] { return std::atexit(shutdown_all) == 0; }();
+  (void)registered;
   auto key = std::make_tuple(dev, c.block_size, c.component_stream_count, c.big_endian, c.unused_lsb_count, encode);
-  auto it = queues->find(key);
-  if (it == queues->end()) it = queues->emplace(key, new batch_queue(dev, c, encode)).first;
+  auto it = reg.queues.find(key);
+  if (it == reg.queues.end()) it = reg.queues.emplace(key, new batch_queue(dev, c, encode)).first;
   return *it->second;
 }
 
@@ -921,8 +1038,11 @@ void set_facade_pack_limit(size_t bytes) { g_pack_max.store(bytes); }
 
 facade_stats get_facade_stats() {
   return facade_stats{g_enc_launches.load(), g_enc_blocks.load(), g_dec_launches.load(), g_dec_blocks.load(),
-                      g_ctx_created.load(),     g_stage_ns.load(),   g_device_ns.load(),     g_finish_ns.load()};
+                      g_ctx_created.load(),  g_stage_ns.load(),   g_device_ns.load(),    g_finish_ns.load(),
+                      g_device_event_ns.load()};
 }
+
+void shutdown_facade() { shutdown_all(); }
 
 // ---- block_compressor (src/compression/ricepp.cpp:57-182, 272-296) ----
 

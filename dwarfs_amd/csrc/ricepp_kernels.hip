@@ -190,9 +190,9 @@ __device__ __forceinline__ bool enc_split_ok(const EncParams& p) {
 constexpr uint32_t kEncSegChunks = 256;
 constexpr uint32_t kEncSegChunksMin = 16;
 constexpr uint64_t kEncTargetUnits = 2048;
-#ifndef RPP_EPRIO
-#define RPP_EPRIO 1  // wave priority in the pipelined encode (1: plans over emission, 2: the reverse, 0: off)
-#endif
+// wave priority in the pipelined encode: plans (deltas, split walk,
+// positions) at priority 1, the LDS emission at 0 (the reverse and no
+// priority measured slower: DESIGN.md §4 "Wave priority")
 
 // Compile-time shape of an encode launch: SPL samples per lane (8 or 16), a
 // ricepp sub-block owned by an aligned group of G lanes (G = next pow2 of
@@ -675,29 +675,17 @@ __global__ __launch_bounds__(kWave) void rpp_encode_kernel(EncParams p) {
     auto step = [&](EncPlan<SPL>& E, EncPlan<SPL>& F, EncRaw<SPL>& rn, EncGeom& gn) {
       RPP_STAT(0, 1);
       RPP_TSTAMP(1);
-#if RPP_EPRIO == 1
       __builtin_amdgcn_s_setprio(1);
-#endif
       enc_plan_a<SPL, G, CS, SH>(F, st, rn, gn, selbe, be, ulsb, empty_lanes, dpp_prev);
       gn = enc_geom<SPL, CS>(s_lo + (it + 3) * spw + g, j, nsb, N, bs);
       rn = enc_load_vec<SPL, CS>(in, gn, !dpp_prev);
       RPP_TSTAMP(2);
-#if RPP_EPRIO == 1
       __builtin_amdgcn_s_setprio(0);
-#elif RPP_EPRIO == 2
-      __builtin_amdgcn_s_setprio(1);
-#endif
       enc_emit<SPL>(E, st, j, empty_lanes);
-#if RPP_EPRIO == 1
       __builtin_amdgcn_s_setprio(1);
-#elif RPP_EPRIO == 2
-      __builtin_amdgcn_s_setprio(0);
-#endif
       RPP_TSTAMP(3);
       enc_plan_b<SPL, G>(F, st, j);
-#if RPP_EPRIO == 1
       __builtin_amdgcn_s_setprio(0);
-#endif
       RPP_TSTAMP(4);
       enc_flush(st, false);
       RPP_TSTAMP(5);
@@ -1128,9 +1116,6 @@ __device__ __forceinline__ uint32_t jshift(uint32_t x, uint32_t& keep) {
 }
 // wave priority over the fast loop's parse chain (profiles/r02_prio_ab.jsonl)
 constexpr int kParsePrio = 1;
-#ifndef RPP_END_LIST
-#define RPP_END_LIST 1  // the fast loop's sub-block end read back from the list (0: picked by readlane)
-#endif
 
 // fs >= 8: states 0..13 (13 remainder bits still to skip at most).  A state
 // is kept replicated in all four bytes of a dword (a v_perm selector that
@@ -1628,29 +1613,6 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           t[j] = ffbl(tm);
           tm &= tm - 1;
         }
-#if !RPP_END_LIST
-        {
-          // the next sub-block starts after code n-1's remainder: terminator
-          // n-1-excl (< MT) of the first lane whose inclusive count reaches
-          // n (positions <= 23 packed in bytes and picked by one bit-field
-          // extract); lane 63 when no lane ends the sub-block (Pe unused)
-          const uint32_t lz = (uint32_t)__builtin_ctzll(__ballot(incl >= n) | (1ull << 63));
-          const uint32_t r = n - 1 - excl;
-          uint32_t tpk = t[0] | (t[1] << 8) | ((t[2] | (t[3] << 8)) << 16);
-          if constexpr (MT > 4) {
-            const uint32_t tpk1 = t[4] | (t[5] << 8) | ((t[6] | (t[7] << 8)) << 16);
-            tpk = r < 4 ? tpk : tpk1;
-          }
-          if constexpr (MT > 8) {
-            const uint32_t tpk2 = t[8] | (t[9] << 8) | ((t[10] | (t[11] << 8)) << 16);
-            tpk = r < 8 ? tpk : tpk2;
-          }
-          const uint32_t tend = __builtin_amdgcn_ubfe(tpk, 8 * (r & 3u), 8) + SB * lane;
-          Pe = q + k + readlane(tend, (int)lz);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        xln = seg_bits(Pe, xhn);
-#endif
         RPP_TSTAMP(8);
         // pair excl + j for j = MT-1 .. 0, one instruction each (kept apart:
         // a merged ds_write2 would put two j in one instruction): a slot past
@@ -1669,15 +1631,15 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_decode_kernel(DecPara
           list2[base + j] = make_uint2(abase + t[j] - j * k, rem);
           lds_fence();
         }
-#if RPP_END_LIST
         // the next sub-block starts after code n-1's remainder: its entry,
         // read back from the list (one broadcast LDS read after the writes,
         // instead of picking the terminator out of the lane that holds it);
         // unused when the sub-block does not end in the window
+        // (picking it by readlane out of the lane that holds it measured
+        // slower: profiles/r04_decode_ab.jsonl)
         Pe = pe_base + __builtin_amdgcn_readfirstlane(list[2 * (n - 1)]);
         __builtin_amdgcn_s_setprio(0);
         xln = seg_bits(Pe, xhn);
-#endif
         // (the previous sub-block's stores, off the chain)
         mid(rider_incl, tot2 >> 16);
         RPP_TSTAMP(13);
@@ -2067,10 +2029,7 @@ constexpr uint32_t kRowMT = 24;                      // terminators per 24-bit s
 constexpr uint32_t kRowListWords = 4 + 2 * (kRowDump + kRowMT);
 constexpr uint32_t kRowWords = kRowRing + kRowPad + kRowListWords;
 constexpr uint32_t kRowsLdsBytes = kTabBytes + kRowsWaves * 4 * kRowWords * 4;
-#ifndef RPP_ROWS
-#define RPP_ROWS 1  // 0: bs 16 / 32 one wave per stream too (profiles/r03_rows_sweep.jsonl)
-#endif
-constexpr bool kRowsDecode = RPP_ROWS != 0;
+
 
 // exclusive form of a row-local map scan: the map of row lanes 0..i-1
 // (identity on each row's lane 0)
@@ -3457,7 +3416,7 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
               cfg->block_size, cfg->component_stream_count, cfg->big_endian ? 1u : 0u,
               cfg->unused_lsb_count, W, only_fallback ? 1u : 0u, d_units};
   const auto k = kernels[2 * (cfg->component_stream_count - 1) + (cfg->unused_lsb_count ? 1 : 0)];
-  if (kRowsDecode && rows && !only_fallback && !d_units && !waves &&
+  if (rows && !only_fallback && !d_units && !waves &&
       (cfg->block_size == 16 || cfg->block_size == 32)) {
     // bs 16 / 32: four streams per wave, then the fused kernel for the
     // streams it left (status kSegFallback)

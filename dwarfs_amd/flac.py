@@ -207,10 +207,20 @@ class FlacBlockDecompressor:
         L = N.lib()
         min_bs = max(16, int(info.min_blocksize) or 16)
         max_bs = int(info.max_blocksize) or 65535
-        max_cand = n // min_bs + len(body) // 4096 + 64
+        # Frames: at most n // min_bs + 1 (every block but the last holds at
+        # least min_bs samples); spurious sync codes that pass the CRC-8 are
+        # rare and handled by the retry below.  Every candidate gets a scratch
+        # slot of max_bs samples: a STREAMINFO whose block-size range would make
+        # that more than 4x the block's samples (libFLAC writes min == max;
+        # DwarFS's flac compressor uses fixed blocking) is refused rather than
+        # allowed to size the workspace from a crafted header.
+        max_cand = n // min_bs + 65
+        if max_cand * max_bs > 4 * n + 128 * max_bs:
+            raise RuntimeError("[FLAC] failed to process frame: block size range "
+                               f"{int(info.min_blocksize)}..{max_bs} too wide for {n} samples")
         s = torch.cuda.current_stream(dev)
         for _ in range(2):
-            ws_bytes = int(L.rpp_flac_decode_workspace_bytes(len(body), channels, max_bs, max_cand))
+            ws_bytes = int(L.rpp_flac_decode_workspace_bytes(len(body), channels, bits, max_bs, max_cand))
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
             _status(L.rpp_flac_decode(C.c_void_p(d_in.data_ptr()), len(body), channels, bits, max_bs, n,
                                       C.c_void_p(x.data_ptr()), C.c_void_p(status.data_ptr()), max_cand,
@@ -219,6 +229,8 @@ class FlacBlockDecompressor:
             found = int(ncand.item())
             if found <= max_cand:
                 break
+            if found * max_bs > 4 * n + 128 * max_bs:  # (a stream full of false sync codes)
+                raise RuntimeError(f"[FLAC] failed to process frame: {found} frame candidates")
             max_cand = found + 64  # (more sync candidates than estimated: again, with room for all)
         st = int(status.item())
         if st != N.RPP_OK:

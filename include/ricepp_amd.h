@@ -362,7 +362,7 @@ uint64_t rpp_flac_frame_bound(uint32_t channels, uint32_t bps);
 uint64_t rpp_flac_encode_workspace_bytes(uint64_t nsamples, uint32_t channels, uint32_t bps);
 int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint8_t* d_out,
                     uint64_t* d_total, void* d_workspace, uint64_t workspace_bytes, void* stream);
-uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t max_blocksize,
+uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t bps, uint32_t max_blocksize,
                                          uint32_t max_candidates);
 int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
                     uint32_t max_blocksize, uint64_t nsamples, int32_t* d_out, int32_t* d_status,

@@ -183,11 +183,21 @@ struct facade_stats {
   uint64_t encode_launches, encode_blocks, decode_launches, decode_blocks;
   uint64_t contexts_created;
   // summed over batches (ns): callers copying their inputs into the pinned
-  // staging, the device part (copies and kernels, one synchronisation), and
-  // callers copying their results out
+  // staging, the device part as the host sees it (launch to completion
+  // published), and callers copying their results out
   uint64_t stage_ns, device_ns, finish_ns;
+  // summed over batches (ns): the device part by the device's clock (events
+  // recorded before the batch's first copy and after its last operation)
+  uint64_t device_event_ns;
 };
 facade_stats get_facade_stats();
+
+// Stops the facade's queues: batches on the device complete, batches not yet
+// launched fail (std::runtime_error), calls made afterwards fail, and the
+// queue threads are joined.  Registered with std::atexit when the first queue
+// is created, so that no thread of the facade makes a HIP call while the HIP
+// runtime is torn down at process exit; a program may call it earlier.
+void shutdown_facade();
 
 // Test only: the next `n` pooled-context creations fail (as a failed
 // hipStreamCreate would), to exercise the error paths of the batch queue.

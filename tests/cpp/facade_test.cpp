@@ -92,9 +92,11 @@ static void roundtrip(ricepp_amd::codec_config const& c, size_t n, unsigned full
 }
 
 int bench(int argc, char** argv);
+int exit_in_flight();
 
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "--bench") return bench(argc, argv);
+  if (argc > 1 && std::string(argv[1]) == "--exit-in-flight") return exit_in_flight();
   // the batch queue's error paths (round-2 review): the first pooled context
   // fails to come up; the callers of that batch get an exception, none hangs,
   // and the queue and pool work afterwards
@@ -364,6 +366,33 @@ int main(int argc, char** argv) {
     for (auto& th : pool) th.join();
     for (int t = 0; t < 16; ++t) CHECK(bad[t] == 0);
   }
+  // the batch shape of round 4's all-blocks RPP_INVALID_ARGUMENT record
+  // (gpurun_out/r04/f16p.err): 7 concurrent 8 Mi-sample encodes joined into one
+  // segmented launch (whose device-side parameter arrays the stream-ordered
+  // allocator had overwritten), then decoded back
+  {
+    auto c = cfg(128, 1, true, 0);
+    std::vector<std::vector<uint16_t>> xs(7);
+    std::vector<std::vector<uint8_t>> bytes(7);
+    for (int t = 0; t < 7; ++t) xs[t] = make_data(size_t{8} << 20, 0, true, 50, 9100 + t);
+    std::vector<int> bad(7, 0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < 7; ++t)
+      pool.emplace_back([&, t] { bytes[t] = ricepp_amd::create_encoder<uint16_t>(c)->encode(xs[t]); });
+    for (auto& th : pool) th.join();
+    pool.clear();
+    for (int t = 0; t < 7; ++t)
+      pool.emplace_back([&, t] {
+        if (bytes[t] != oracle_encode(c, xs[t])) ++bad[t];
+        std::vector<uint16_t> y(xs[t].size());
+        ricepp_amd::create_decoder<uint16_t>(c)->decode(y, bytes[t]);
+        if (y != xs[t]) ++bad[t];
+      });
+    for (auto& th : pool) th.join();
+    for (int t = 0; t < 7; ++t) CHECK(bad[t] == 0);
+  }
+  // device time by the device's clock is recorded per batch
+  CHECK(ricepp_amd::get_facade_stats().device_event_ns > 0);
   std::printf("facade_test: %s (%d failures)\n", failures ? "FAILED" : "OK", failures);
   return failures ? 1 : 0;
 }
@@ -403,6 +432,7 @@ int bench(int argc, char** argv) {
   std::vector<std::vector<uint8_t>> encbuf(blocks, std::vector<uint8_t>(wc));
   std::vector<std::span<uint8_t>> enc(blocks);
   std::vector<std::vector<uint16_t>> out(blocks, std::vector<uint16_t>(n));
+  std::atomic<bool> failed{false};
   for (int T : threads) {
     auto run = [&](bool encode) {
       std::vector<std::thread> pool;
@@ -411,14 +441,16 @@ int bench(int argc, char** argv) {
         pool.emplace_back([&, t] {
           auto e = ricepp_amd::create_encoder<uint16_t>(c);
           auto d = ricepp_amd::create_decoder<uint16_t>(c);
-          for (size_t b = t; b < blocks; b += T) {
+          for (size_t b = t; b < blocks && !failed.load(); b += T) {
             try {
               if (encode) enc[b] = e->encode(std::span<uint8_t>{encbuf[b]}, in[b]);
               else d->decode(out[b], enc[b]);
             } catch (std::exception const& x) {
+              // (reported and returned from main: never exit() from a worker
+              // while the others are still inside the facade)
               std::fprintf(stderr, "facade bench: %s of block %zu (%zu encoded bytes): %s\n",
                            encode ? "encode" : "decode", b, enc[b].size(), x.what());
-              std::exit(3);
+              failed.store(true);
             }
           }
         });
@@ -433,6 +465,7 @@ int bench(int argc, char** argv) {
     auto s1 = ricepp_amd::get_facade_stats();
     double td = run(false);
     auto s2 = ricepp_amd::get_facade_stats();
+    if (failed.load()) return 3;
     bool ok = true;
     int reported = 0;
     for (size_t b = 0; b < blocks; ++b) {
@@ -459,14 +492,56 @@ int bench(int argc, char** argv) {
     const double ne = double(s1.encode_launches - s0.encode_launches), nd = double(s2.decode_launches - s1.decode_launches);
     std::printf("{\"facade_bench\": true, \"threads\": %d, \"depth\": %d, \"blocks\": %zu, \"block_bytes\": %zu, "
                 "\"encode_GiBps\": %.3f, \"decode_GiBps\": %.3f, \"encode_launches\": %.0f, "
-                "\"decode_launches\": %.0f, \"encode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, \"finish\": %.1f}, "
-                "\"decode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, \"finish\": %.1f}, \"roundtrip_ok\": %s}\n",
+                "\"decode_launches\": %.0f, \"encode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, "
+                "\"device_events\": %.1f, \"finish\": %.1f}, \"decode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, "
+                "\"device_events\": %.1f, \"finish\": %.1f}, \"roundtrip_ok\": %s}\n",
                 T, depth, blocks, n * 2, gib / te, gib / td, ne, nd, (s1.stage_ns - s0.stage_ns) / 1e3 / ne,
-                (s1.device_ns - s0.device_ns) / 1e3 / ne, (s1.finish_ns - s0.finish_ns) / 1e3 / ne,
-                (s2.stage_ns - s1.stage_ns) / 1e3 / nd, (s2.device_ns - s1.device_ns) / 1e3 / nd,
+                (s1.device_ns - s0.device_ns) / 1e3 / ne, (s1.device_event_ns - s0.device_event_ns) / 1e3 / ne,
+                (s1.finish_ns - s0.finish_ns) / 1e3 / ne, (s2.stage_ns - s1.stage_ns) / 1e3 / nd,
+                (s2.device_ns - s1.device_ns) / 1e3 / nd, (s2.device_event_ns - s1.device_event_ns) / 1e3 / nd,
                 (s2.finish_ns - s1.finish_ns) / 1e3 / nd, ok ? "true" : "false");
     std::fflush(stdout);
     if (!ok) return 1;
   }
   return 0;
+}
+
+// ---- process exit while batches are in flight (facade_test --exit-in-flight) ----
+// 8 worker threads encode and decode 64 KiB and 4 MiB blocks in a loop; one of
+// them calls std::exit(0) while the others' batches are queued or on the
+// device.  The facade's atexit hook stops its queues before the HIP runtime
+// is torn down: the exit status must be 0 (no abort, no core dump).  Workers
+// that get "facade shut down" afterwards stop quietly.
+int exit_in_flight() {
+  auto c = cfg(128, 1, true, 0);
+  std::vector<std::thread> pool;
+  std::atomic<int> rounds{0};
+  for (int t = 0; t < 8; ++t) {
+    pool.emplace_back([&, t] {
+      auto x = make_data(t % 2 ? size_t{2} << 20 : 32768, 0, true, 50, 300 + t);
+      try {
+        auto e = ricepp_amd::create_encoder<uint16_t>(c);
+        auto d = ricepp_amd::create_decoder<uint16_t>(c);
+        for (int i = 0;; ++i) {
+          auto bytes = e->encode(x);
+          std::vector<uint16_t> y(x.size());
+          d->decode(y, bytes);
+          if (y != x) {
+            std::fprintf(stderr, "exit-in-flight: round trip mismatch\n");
+            std::_Exit(4);
+          }
+          ++rounds;
+          if (t == 0 && rounds.load() >= 200) {
+            std::printf("exit-in-flight: exiting after %d round trips\n", rounds.load());
+            std::fflush(stdout);
+            std::exit(0);
+          }
+        }
+      } catch (std::exception const&) {  // (the facade was shut down under this thread)
+      }
+    });
+  }
+  for (auto& th : pool) th.join();
+  std::printf("exit-in-flight: workers ended before the exit\n");
+  return 5;
 }

@@ -67,7 +67,7 @@ for channels, nbytes, bits in ((2, 2, 16), (8, 4, 24)):
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     nc = torch.zeros(1, dtype=torch.int32, device=dev)
     mc = n // 4096 + body.numel() // 4096 + 64
-    wdb = int(L.rpp_flac_decode_workspace_bytes(body.numel(), channels, 4096, mc))
+    wdb = int(L.rpp_flac_decode_workspace_bytes(body.numel(), channels, bits, 4096, mc))
     wd = torch.empty(wdb, dtype=torch.uint8, device=dev)
     tk_d = timed(lambda: L.rpp_flac_decode(C.c_void_p(body.data_ptr()), body.numel(), channels, bits, 4096, n,
                                            C.c_void_p(y.data_ptr()), C.c_void_p(st.data_ptr()), mc,
@@ -106,7 +106,7 @@ y = torch.empty(n * channels, dtype=torch.int32, device=dev)
 st = torch.zeros(1, dtype=torch.int32, device=dev)
 nc = torch.zeros(1, dtype=torch.int32, device=dev)
 mc = n // 4096 + body.numel() // 4096 + 64
-wdb = int(L.rpp_flac_decode_workspace_bytes(body.numel(), channels, 4096, mc))
+wdb = int(L.rpp_flac_decode_workspace_bytes(body.numel(), channels, bits, 4096, mc))
 wd = torch.empty(wdb, dtype=torch.uint8, device=dev)
 s = torch.cuda.current_stream()
 args = (C.c_void_p(body.data_ptr()), body.numel(), channels, bits, 4096, n, C.c_void_p(y.data_ptr()),

@@ -23,7 +23,7 @@ for channels, nbytes, bits in ((2, 2, 16), (8, 4, 24)):
     y = torch.empty(n * channels, dtype=torch.int32, device=dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev); nc = torch.zeros(1, dtype=torch.int32, device=dev)
     mc = n // 4096 + nb // 4096 + 64
-    wdb = int(L.rpp_flac_decode_workspace_bytes(nb, channels, 4096, mc))
+    wdb = int(L.rpp_flac_decode_workspace_bytes(nb, channels, bits, 4096, mc))
     wd = torch.zeros(wdb, dtype=torch.uint8, device=dev)
     L.rpp_flac_decode(C.c_void_p(body.data_ptr()), nb, channels, bits, 4096, n, C.c_void_p(y.data_ptr()), C.c_void_p(st.data_ptr()), mc, C.c_void_p(wd.data_ptr()), wdb, C.c_void_p(nc.data_ptr()), C.c_void_p(s.cuda_stream))
     torch.cuda.synchronize()

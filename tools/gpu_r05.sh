@@ -16,6 +16,8 @@
 #   sbl      small-batch decode latency per path (tools/small_batch_latency.py)
 #   paths    bs 16 / 32 decode per path (tools/workloads.py paths)
 #   flac     the FLAC GPU tests, then tools/flac_bench.py
+#   ftests   the facade GPU tests (C++ facade_test incl. exit with batches in flight) and the FLAC GPU tests
+#   f16x5    facade 16 MiB blocks, 16 threads, five consecutive runs (bimodality check)
 #   pmcq     one PMC pass of the bench workload per library (default + VARIANTS): cycles, LDS, VALU, SALU
 #   dtests   the decode parity tests only (tests/test_gpu_parity.py, test_gpu_abi.py)
 set -u
@@ -73,6 +75,10 @@ for step in "$@"; do
           --output-format csv -d gpurun_out/pmcq/$v/p1 -o run -- python3 tools/prof_kernels.py 2
         python3 tools/pmc_summary.py gpurun_out/pmcq/$v > $O/pmcq_$v.txt; echo "== $v"; cat $O/pmcq_$v.txt
       done ;;
+    ftests) run ftests 600 python -u -m pytest tests/test_gpu_block_codec.py tests/test_gpu_flac.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    f16x5)
+      for i in 1 2 3 4 5; do run f16x5_$i 300 ./tests/cpp/build/facade_test --bench 64 --kib=16384 16; done ;;
+    f64k) run f64k 300 ./tests/cpp/build/facade_test --bench 4096 16 64 ;;
     dtests) run dtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_abi.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
