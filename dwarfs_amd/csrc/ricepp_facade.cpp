@@ -1224,4 +1224,239 @@ void pcm_sample_transformer::pack(std::span<uint8_t> dst, std::span<int32_t cons
   ctx->sync();
 }
 
+// ---- FLAC block codec (src/compression/flac.cpp:215-525) ----
+
+namespace {
+
+constexpr uint32_t kFlacBigEndian = 0x80, kFlacSigned = 0x40, kFlacLsbPadding = 0x20, kFlacBytesMask = 0x03;  // :41-44
+
+char const* status_name(int st) {
+  switch (st) {
+    case RPP_OK: return "OK";
+    case RPP_UNSUPPORTED_CONFIG: return "UNSUPPORTED_CONFIG";
+    case RPP_TRUNCATED_INPUT: return "TRUNCATED_INPUT";
+    case RPP_INVALID_ARGUMENT: return "INVALID_ARGUMENT";
+    case RPP_OUTPUT_TOO_SMALL: return "OUTPUT_TOO_SMALL";
+    case RPP_HIP_ERROR: return "HIP_ERROR";
+    case RPP_INTERNAL_ERROR: return "INTERNAL_ERROR";
+    default: return "UNKNOWN";
+  }
+}
+
+rpp_pcm_format flac_pcm_format(uint32_t flags, uint32_t bits) {
+  rpp_pcm_format f{};
+  f.big_endian = flags & kFlacBigEndian ? 1u : 0u;
+  f.is_signed = flags & kFlacSigned ? 1u : 0u;
+  f.lsb_padded = flags & kFlacLsbPadding ? 1u : 0u;
+  f.bytes = (flags & kFlacBytesMask) + 1;
+  f.bits = bits;
+  return f;
+}
+
+}  // namespace
+
+flac_block_compressor::flac_block_compressor(uint32_t level, bool exhaustive) : level_{level}, exhaustive_{exhaustive} {
+  if (level_ > 8) throw std::runtime_error("invalid option(s) for flac: level=" + std::to_string(level_));
+}
+
+std::unique_ptr<flac_block_compressor> flac_block_compressor::create(std::string const& spec) {
+  // option_map over "flac:level=N:exhaustive" (flac.cpp:509-525; options
+  // separated by ':' or ',')
+  std::string name = spec.substr(0, spec.find(':'));
+  if (name != "flac") throw std::runtime_error("unknown compression: " + name);
+  uint32_t level = 5;
+  bool exhaustive = false;
+  if (auto c = spec.find(':'); c != std::string::npos) {
+    std::string opts = spec.substr(c + 1);
+    size_t p = 0;
+    while (p <= opts.size()) {
+      size_t e = opts.find_first_of(",:", p);
+      std::string kv = opts.substr(p, e == std::string::npos ? std::string::npos : e - p);
+      if (!kv.empty()) {
+        auto eq = kv.find('=');
+        std::string k = kv.substr(0, eq);
+        if (k == "level" && eq != std::string::npos) {
+          std::string v = kv.substr(eq + 1);
+          unsigned long lv = 0;
+          auto r = std::from_chars(v.data(), v.data() + v.size(), lv);
+          if (r.ec != std::errc{} || r.ptr != v.data() + v.size() || lv > 8)
+            throw std::runtime_error("invalid option(s) for flac: " + kv);
+          level = static_cast<uint32_t>(lv);
+        } else if (k == "exhaustive" && eq == std::string::npos) {
+          exhaustive = true;
+        } else {
+          throw std::runtime_error("invalid option(s) for flac: " + kv);
+        }
+      }
+      if (e == std::string::npos) break;
+      p = e + 1;
+    }
+  }
+  return std::make_unique<flac_block_compressor>(level, exhaustive);
+}
+
+std::unique_ptr<flac_block_compressor> flac_block_compressor::clone() const {
+  return std::make_unique<flac_block_compressor>(*this);
+}
+
+std::string flac_block_compressor::describe() const {
+  return "flac [level=" + std::to_string(level_) + (exhaustive_ ? ", exhaustive" : "") + "]";
+}
+
+std::string flac_block_compressor::metadata_requirements() const {
+  // flac.cpp:368-379 (nlohmann::json dump: keys sorted)
+  return R"({"bits_per_sample":["range",8,32],"bytes_per_sample":["range",1,4],"endianness":["set",["big","little"]],)"
+         R"("number_of_channels":["range",1,8],"padding":["set",["msb","lsb"]],"signedness":["set",["signed","unsigned"]]})";
+}
+
+size_t flac_block_compressor::compression_granularity(std::string const& metadata) const {
+  auto m = parse_flat_json(metadata);
+  return static_cast<size_t>(json_int(m, "number_of_channels") * json_int(m, "bytes_per_sample"));
+}
+
+std::vector<uint8_t> flac_block_compressor::compress(std::span<uint8_t const> data, std::string const* metadata) const {
+  if (!metadata) throw std::runtime_error("internal error: flac compression requires metadata");  // :229-232
+  auto meta = parse_flat_json(*metadata);
+  const std::string endianness = json_str(meta, "endianness"), signedness = json_str(meta, "signedness"),
+                    padding = json_str(meta, "padding");
+  const int channels = json_int(meta, "number_of_channels"), bits = json_int(meta, "bits_per_sample"),
+            nbytes = json_int(meta, "bytes_per_sample");
+  if (nbytes < 1 || nbytes > 4 || bits < 8 || bits > 32 || channels < 1)  // asserts at :243-245
+    throw std::runtime_error("ricepp_amd: flac metadata out of range");
+  if (data.size() % static_cast<size_t>(channels * nbytes))  // :247-253
+    throw std::runtime_error("unexpected PCM waveform configuration: " + std::to_string(data.size()) +
+                             " bytes to compress, " + std::to_string(channels) + " channels, " +
+                             std::to_string(nbytes) + " bytes per sample");
+  uint32_t flags = static_cast<uint32_t>(nbytes - 1);
+  if (endianness == "big") flags |= kFlacBigEndian;
+  if (signedness == "signed") flags |= kFlacSigned;
+  if (padding == "lsb") flags |= kFlacLsbPadding;
+  const uint64_t n = data.size() / static_cast<size_t>(channels * nbytes);  // samples per channel
+  rpp_flac_frame f{data.size(), static_cast<uint32_t>(channels), static_cast<uint32_t>(bits), flags};
+  std::vector<uint8_t> out(128);
+  size_t hdr = rpp_flac_frame_header(&f, out.data());
+  hdr += rpp_flac_stream_header(f.num_channels, f.bits_per_sample, n, out.data() + hdr);
+  out.resize(hdr);
+  if (n == 0) return out;
+  // libFLAC's encoder init rejects what it cannot code (:313-317)
+  const uint64_t bound = rpp_flac_frame_bound(f.num_channels, f.bits_per_sample);
+  if (channels > 8 || bound == 0) throw std::runtime_error("[FLAC] init: unsupported stream shape");
+  const rpp_pcm_format pf = flac_pcm_format(flags, f.bits_per_sample);
+  const uint64_t nvals = n * static_cast<uint64_t>(channels);
+  const uint64_t frames = (n + 4095) / 4096;
+  const uint64_t ws_bytes = rpp_flac_encode_workspace_bytes(n, f.num_channels, f.bits_per_sample);
+  const size_t off_x = align16(data.size()), off_out = off_x + align16(nvals * 4),
+               off_tot = off_out + align16(frames * bound + 64), off_ws = off_tot + 16;
+  const int dev = current_device();
+  device_guard g{dev};
+  ctx_lease ctx{dev};
+  uint8_t* d = ctx->dev(off_ws + ws_bytes);
+  hipStream_t st = ctx->stream();
+  hip_check(hipMemcpyAsync(d, data.data(), data.size(), hipMemcpyHostToDevice, st), "H2D flac pcm");
+  int rc = rpp_pcm_unpack(&pf, d, reinterpret_cast<int32_t*>(d + off_x), nvals, st);
+  if (rc != RPP_OK) throw std::runtime_error(std::string("[FLAC] failed to process interleaved samples: ") + status_name(rc));
+  rc = rpp_flac_encode(reinterpret_cast<int32_t const*>(d + off_x), n, f.num_channels, f.bits_per_sample, d + off_out,
+                       reinterpret_cast<uint64_t*>(d + off_tot), d + off_ws, ws_bytes, st);
+  if (rc != RPP_OK) throw std::runtime_error(std::string("[FLAC] failed to process interleaved samples: ") + status_name(rc));
+  uint64_t total = 0;
+  hip_check(hipMemcpyAsync(&total, d + off_tot, 8, hipMemcpyDeviceToHost, st), "D2H flac size");
+  ctx->sync();
+  out.resize(hdr + total);
+  hip_check(hipMemcpyAsync(out.data() + hdr, d + off_out, total, hipMemcpyDeviceToHost, st), "D2H flac frames");
+  ctx->sync();
+  return out;
+}
+
+flac_block_decompressor::flac_block_decompressor(std::span<uint8_t const> data) {
+  long h = rpp_flac_parse_frame(data.data(), data.size(), &frame_);
+  if (h < 0) throw std::runtime_error("ricepp_amd: malformed flac block header");
+  auto stream = data.subspan(static_cast<size_t>(h));
+  long at = rpp_flac_parse_stream(stream.data(), stream.size(), &info_);
+  if (at < 0)  // :410-418
+    throw std::runtime_error(std::string("[FLAC] could not initialize decoder: ") + status_name(static_cast<int>(at)));
+  frames_ = stream.subspan(static_cast<size_t>(at));
+}
+
+std::optional<std::string> flac_block_decompressor::metadata() const {
+  // :429-440 (nlohmann::json dump: keys sorted)
+  const uint32_t fl = frame_.flags;
+  return std::string(R"({"bits_per_sample":)") + std::to_string(frame_.bits_per_sample) +
+         R"(,"bytes_per_sample":)" + std::to_string((fl & kFlacBytesMask) + 1) + R"(,"endianness":")" +
+         (fl & kFlacBigEndian ? "big" : "little") + R"(","number_of_channels":)" +
+         std::to_string(frame_.num_channels) + R"(,"padding":")" + (fl & kFlacLsbPadding ? "lsb" : "msb") +
+         R"(","signedness":")" + (fl & kFlacSigned ? "signed" : "unsigned") + "\"}";
+}
+
+void flac_block_decompressor::start_decompression(std::vector<uint8_t>* target) {
+  target_ = target;
+  target_->reserve(frame_.uncompressed_bytes);
+}
+
+bool flac_block_decompressor::decompress_frame(size_t) {
+  if (!target_) throw std::runtime_error("decompression not started");
+  if (done_) return false;
+  const uint32_t channels = info_.channels, bits = info_.bits_per_sample;
+  const uint32_t nbytes = (frame_.flags & kFlacBytesMask) + 1;
+  const uint64_t n = info_.total_samples;
+  auto fail = [](std::string const& why) { return std::runtime_error("[FLAC] failed to process frame: " + why); };
+  if (n * channels * nbytes != frame_.uncompressed_bytes) throw fail("stream length does not match the block");
+  target_->resize(frame_.uncompressed_bytes);
+  done_ = true;
+  if (n == 0) return true;
+  // frames: at most n / min_blocksize + 1; spurious sync codes passing the
+  // CRC-8 are rare and retried with room for all.  A block-size range that
+  // would size the per-candidate scratch beyond 4x the block's samples is
+  // refused (libFLAC and DwarFS's compressor write min == max).
+  const uint64_t min_bs = std::max<uint64_t>(16, info_.min_blocksize ? info_.min_blocksize : 16);
+  const uint64_t max_bs = info_.max_blocksize ? info_.max_blocksize : 65535;
+  uint64_t max_cand = n / min_bs + 65;
+  auto too_wide = [&](uint64_t cand) { return cand * max_bs > 4 * n + 128 * max_bs; };
+  if (too_wide(max_cand)) throw fail("block size range too wide for the block");
+  const rpp_pcm_format pf = flac_pcm_format(frame_.flags, frame_.bits_per_sample);
+  const uint64_t nvals = n * channels;
+  const int dev = current_device();
+  device_guard g{dev};
+  ctx_lease ctx{dev};
+  hipStream_t st = ctx->stream();
+  for (int attempt = 0;; ++attempt) {
+    const uint64_t ws_bytes = rpp_flac_decode_workspace_bytes(frames_.size(), channels, bits,
+                                                              static_cast<uint32_t>(max_bs),
+                                                              static_cast<uint32_t>(max_cand));
+    const size_t off_x = align16(frames_.size()), off_pcm = off_x + align16(nvals * 4),
+                 off_st = off_pcm + align16(frame_.uncompressed_bytes), off_ws = off_st + 16;
+    uint8_t* d = ctx->dev(off_ws + ws_bytes);
+    auto* dst = reinterpret_cast<int32_t*>(d + off_st);
+    hip_check(hipMemcpyAsync(d, frames_.data(), frames_.size(), hipMemcpyHostToDevice, st), "H2D flac frames");
+    hip_check(hipMemsetAsync(dst, 0, 8, st), "hipMemsetAsync");
+    int rc = rpp_flac_decode(d, frames_.size(), channels, bits, static_cast<uint32_t>(max_bs), n,
+                             reinterpret_cast<int32_t*>(d + off_x), dst, static_cast<uint32_t>(max_cand), d + off_ws,
+                             ws_bytes, reinterpret_cast<uint32_t*>(dst + 1), st);
+    if (rc != RPP_OK) throw fail(status_name(rc));
+    int32_t res[2] = {0, 0};  // status, candidates found
+    hip_check(hipMemcpyAsync(res, dst, 8, hipMemcpyDeviceToHost, st), "D2H flac status");
+    ctx->sync();
+    const uint64_t found = static_cast<uint32_t>(res[1]);
+    if (found > max_cand) {
+      if (attempt > 0 || too_wide(found)) throw fail(std::to_string(found) + " frame candidates");
+      max_cand = found + 64;
+      continue;
+    }
+    if (res[0] != RPP_OK) throw fail(status_name(res[0]));
+    rc = rpp_pcm_pack(&pf, reinterpret_cast<int32_t const*>(d + off_x), d + off_pcm, nvals, st);
+    if (rc != RPP_OK) throw fail(status_name(rc));
+    hip_check(hipMemcpyAsync(target_->data(), d + off_pcm, frame_.uncompressed_bytes, hipMemcpyDeviceToHost, st),
+              "D2H flac pcm");
+    ctx->sync();
+    return true;
+  }
+}
+
+std::vector<uint8_t> flac_block_decompressor::decompress(std::span<uint8_t const> data) {
+  flac_block_decompressor d{data};
+  std::vector<uint8_t> out;
+  d.start_decompression(&out);
+  d.decompress_frame(d.uncompressed_size());
+  return out;
+}
+
 }  // namespace ricepp_amd

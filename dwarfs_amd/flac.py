@@ -36,6 +36,11 @@ COMPRESSION_TYPE_FLAC = 6  # include/dwarfs/compression.h:41
 FLAG_BIG_ENDIAN, FLAG_SIGNED, FLAG_LSB_PADDING, BYTES_PER_SAMPLE_MASK = 0x80, 0x40, 0x20, 0x03  # flac.cpp:41-44
 
 
+def _dump(obj) -> str:
+    """nlohmann::json::dump() of an object: keys sorted, no spaces."""
+    return json.dumps(obj, sort_keys=True, separators=(",", ":"))
+
+
 def _status(st: int, what: str) -> None:
     if st != N.RPP_OK:
         raise RuntimeError(f"[FLAC] {what}: {N.STATUS_NAMES.get(st, st)}")
@@ -91,8 +96,8 @@ class FlacBlockCompressor:
     def describe(self) -> str:  # :363-366
         return f"flac [level={self.level}{', exhaustive' if self.exhaustive else ''}]"
 
-    def metadata_requirements(self) -> str:  # :368-379
-        return json.dumps({
+    def metadata_requirements(self) -> str:  # :368-379 (nlohmann::json dump: keys sorted, compact)
+        return _dump({
             "endianness": ["set", ["big", "little"]],
             "signedness": ["set", ["signed", "unsigned"]],
             "padding": ["set", ["msb", "lsb"]],
@@ -166,9 +171,9 @@ class FlacBlockDecompressor:
     def uncompressed_size(self) -> int:
         return int(self.frame.uncompressed_bytes)
 
-    def metadata(self) -> str:  # :429-440
+    def metadata(self) -> str:  # :429-440 (nlohmann::json dump: keys sorted, compact)
         fl = int(self.frame.flags)
-        return json.dumps({
+        return _dump({
             "endianness": "big" if fl & FLAG_BIG_ENDIAN else "little",
             "signedness": "signed" if fl & FLAG_SIGNED else "unsigned",
             "padding": "lsb" if fl & FLAG_LSB_PADDING else "msb",

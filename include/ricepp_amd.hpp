@@ -148,6 +148,66 @@ class block_decompressor {
   std::vector<uint8_t>* target_ = nullptr;
 };
 
+// ---- DwarFS FLAC block codec (src/compression/flac.cpp) ----
+//
+// flac_block_compressor / flac_block_decompressor: the plugin's framing
+// (varint + thrift-compact flac_block_header + a FLAC stream), metadata JSON,
+// describe(), constraints and error messages (flac.cpp:215-489), with the PCM
+// bytes unpacked, encoded, decoded and packed on the GPU (rpp_pcm_unpack,
+// rpp_flac_encode, rpp_flac_decode, rpp_pcm_pack) through a pooled device
+// context.  Parity unpinned: the reference codes the stream with libFLAC
+// (absent here); this encoder writes valid FLAC (RFC 9639) with fixed
+// predictors, 4096-sample frames and stereo decorrelation, so its bytes differ
+// from libFLAC's.  `level` and `exhaustive` are accepted, validated (level
+// 0..8) and reported by describe() as the reference does; they do not change
+// the output (no LPC search).  The decoder reads every RFC 9639 frame kind,
+// LPC included.
+
+// compression_type::FLAC (include/dwarfs/compression.h, FLAC = 6)
+inline constexpr int compression_type_flac = 6;
+
+class flac_block_compressor {
+ public:
+  explicit flac_block_compressor(uint32_t level = 5, bool exhaustive = false);
+  // "flac", "flac:level=N", "flac:exhaustive", "flac:level=N:exhaustive"
+  // (flac_compressor_factory, flac.cpp:509-525: options level=[0..8],
+  // exhaustive)
+  static std::unique_ptr<flac_block_compressor> create(std::string const& spec);
+
+  std::unique_ptr<flac_block_compressor> clone() const;
+  std::vector<uint8_t> compress(std::span<uint8_t const> data, std::string const* metadata) const;
+  int type() const { return compression_type_flac; }
+  std::string describe() const;                                       // flac.cpp:363-366
+  std::string metadata_requirements() const;                          // :368-379
+  size_t compression_granularity(std::string const& metadata) const;  // :381-393
+  size_t estimate_memory_usage(size_t data_size) const { return data_size; }  // :395-398
+
+ private:
+  uint32_t level_;
+  bool exhaustive_;
+};
+
+class flac_block_decompressor {
+ public:
+  // throws "[FLAC] could not initialize decoder: ..." for a stream whose
+  // metadata does not parse (flac.cpp:410-418)
+  explicit flac_block_decompressor(std::span<uint8_t const> data);
+
+  int type() const { return compression_type_flac; }
+  std::optional<std::string> metadata() const;  // :429-440
+  size_t uncompressed_size() const { return frame_.uncompressed_bytes; }
+  void start_decompression(std::vector<uint8_t>* target);
+  bool decompress_frame(size_t frame_size = 0);  // decodes everything on the first call
+  static std::vector<uint8_t> decompress(std::span<uint8_t const> data);
+
+ private:
+  rpp_flac_frame frame_{};
+  rpp_flac_stream_info info_{};
+  std::span<uint8_t const> frames_;  // the stream's frames (after its metadata blocks)
+  std::vector<uint8_t>* target_ = nullptr;
+  bool done_ = false;
+};
+
 // ---- PCM sample transformer (include/dwarfs/pcm_sample_transformer.h:36-71) ----
 //
 // pcm_sample_transformer<int32_t>: (end, sig, pad, bytes, bits) -> unpack / pack

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cmath>
 #include <random>
 #include <span>
 #include <stdexcept>
@@ -24,6 +25,15 @@ struct rpo_config {
 size_t rpo_worst_case_bytes(const rpo_config*, size_t);
 int rpo_encode(const rpo_config*, const uint16_t*, size_t, uint8_t*, size_t, size_t*);
 size_t rpo_frame_header(uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, uint32_t);
+// FLAC restatement (oracle/flac_oracle.c), an independent encoder / decoder
+typedef struct {
+  int subframe_type, fixed_order, lpc_order, lpc_precision, stereo, max_partition_order, rice2, escape,
+      padding_block, wasted, variable_blocking, max_lpc_order;
+} fo_opts;
+size_t fo_encode(const int32_t* x, uint64_t nsamples, uint32_t channels, uint32_t bps, uint32_t blocksize,
+                 const fo_opts* opts, uint8_t* out, size_t cap);
+int fo_decode(const uint8_t* in, size_t len, int32_t* out, uint64_t cap, uint32_t* channels_out, uint32_t* bps_out,
+              uint64_t* nsamples_out);
 }
 
 static int failures = 0;
@@ -93,6 +103,7 @@ static void roundtrip(ricepp_amd::codec_config const& c, size_t n, unsigned full
 
 int bench(int argc, char** argv);
 int exit_in_flight();
+void flac_tests();
 
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "--bench") return bench(argc, argv);
@@ -393,6 +404,7 @@ int main(int argc, char** argv) {
   }
   // device time by the device's clock is recorded per batch
   CHECK(ricepp_amd::get_facade_stats().device_event_ns > 0);
+  flac_tests();
   std::printf("facade_test: %s (%d failures)\n", failures ? "FAILED" : "OK", failures);
   return failures ? 1 : 0;
 }
@@ -544,4 +556,104 @@ int exit_in_flight() {
   for (auto& th : pool) th.join();
   std::printf("exit-in-flight: workers ended before the exit\n");
   return 5;
+}
+
+// ---- FLAC block codec (src/compression/flac.cpp; test/flac_compressor_test.cpp:97-205) ----
+// Parity unpinned (libFLAC is absent): the C++ compressor's stream is decoded
+// by the independent restatement, and the restatement's streams (LPC order 8,
+// as libFLAC level 5 writes) by the C++ decompressor.
+static std::vector<int32_t> flac_signal(size_t frames, uint32_t channels, uint32_t bits, uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  std::vector<int32_t> x(frames * channels);
+  const double amp = double((int64_t(1) << (bits - 1)) - 1) * 0.6;
+  for (size_t i = 0; i < frames; ++i)
+    for (uint32_t c = 0; c < channels; ++c)
+      x[i * channels + c] = int32_t(amp * std::sin(0.001 * double(i) * (1.0 + c)) + double(int(rng() % 17) - 8));
+  return x;
+}
+
+void flac_tests() {
+  using ricepp_amd::flac_block_compressor;
+  using ricepp_amd::flac_block_decompressor;
+  const std::string meta16 = R"({"bits_per_sample":16,"bytes_per_sample":2,"endianness":"little",)"
+                             R"("number_of_channels":2,"padding":"msb","signedness":"signed"})";
+  // factory, describe, requirements, constraints (flac.cpp:363-393, 509-525)
+  CHECK(flac_block_compressor::create("flac")->describe() == "flac [level=5]");
+  CHECK(flac_block_compressor::create("flac:level=8:exhaustive")->describe() == "flac [level=8, exhaustive]");
+  CHECK(flac_block_compressor::create("flac:level=0")->describe() == "flac [level=0]");
+  CHECK(throws<std::runtime_error>([] { flac_block_compressor::create("flac:level=9"); }));
+  CHECK(throws<std::runtime_error>([] { flac_block_compressor::create("flac:speed=3"); }));
+  flac_block_compressor comp;
+  CHECK(comp.type() == 6);
+  CHECK(comp.metadata_requirements() ==
+        R"({"bits_per_sample":["range",8,32],"bytes_per_sample":["range",1,4],"endianness":["set",["big","little"]],)"
+        R"("number_of_channels":["range",1,8],"padding":["set",["msb","lsb"]],"signedness":["set",["signed","unsigned"]]})");
+  CHECK(comp.compression_granularity(meta16) == 4);
+  // error contract (:229-232, :247-253)
+  {
+    std::vector<uint8_t> odd(7);
+    CHECK(throws<std::runtime_error>([&] { comp.compress(odd, nullptr); },
+                                     "internal error: flac compression requires metadata"));
+    CHECK(throws<std::runtime_error>(
+        [&] { comp.compress(odd, &meta16); },
+        "unexpected PCM waveform configuration: 7 bytes to compress, 2 channels, 2 bytes per sample"));
+  }
+  // round trip, 16-bit stereo little endian signed; stream checked by the restatement
+  {
+    const size_t frames = 3 * 4096 + 1234;
+    auto x = flac_signal(frames, 2, 16, 1);
+    std::vector<uint8_t> pcm(x.size() * 2);
+    for (size_t i = 0; i < x.size(); ++i) {
+      pcm[2 * i] = uint8_t(x[i]);
+      pcm[2 * i + 1] = uint8_t(uint32_t(x[i]) >> 8);
+    }
+    auto block = comp.compress(pcm, &meta16);
+    CHECK(block.size() < pcm.size() / 2);  // flac_compressor_test.cpp: the output is below half the input
+    // framing: varint + flac_block_header + "fLaC" + STREAMINFO
+    rpp_flac_frame f{};
+    long h = rpp_flac_parse_frame(block.data(), block.size(), &f);
+    CHECK(h > 0 && f.uncompressed_bytes == pcm.size() && f.num_channels == 2 && f.bits_per_sample == 16 &&
+          f.flags == 0x41);
+    std::vector<int32_t> y(x.size());
+    uint32_t ch = 0, bps = 0;
+    uint64_t ns = 0;
+    CHECK(fo_decode(block.data() + h, block.size() - (size_t)h, y.data(), y.size(), &ch, &bps, &ns) == 0);
+    CHECK(ch == 2 && bps == 16 && ns == frames && y == x);
+    flac_block_decompressor d{block};
+    CHECK(d.uncompressed_size() == pcm.size());
+    CHECK(*d.metadata() == meta16);
+    std::vector<uint8_t> out;
+    d.start_decompression(&out);
+    CHECK(d.decompress_frame(pcm.size()));
+    CHECK(!d.decompress_frame(pcm.size()));
+    CHECK(out == pcm);
+  }
+  // the restatement's LPC streams (orders up to 8, as libFLAC level 5),
+  // 24-bit in 3 bytes, big endian, 3 channels -> the C++ decompressor
+  {
+    const size_t frames = 2 * 4096 + 77;
+    auto x = flac_signal(frames, 3, 24, 2);
+    fo_opts o{};
+    o.stereo = -1;
+    o.max_partition_order = 6;
+    o.max_lpc_order = 8;
+    std::vector<uint8_t> stream(frames * 3 * 4 + 65536);
+    size_t len = fo_encode(x.data(), frames, 3, 24, 4096, &o, stream.data(), stream.size());
+    CHECK(len > 0);
+    stream.resize(len);
+    rpp_flac_frame f{frames * 3 * 3, 3, 24, 0x80 | 0x40 | 2};
+    std::vector<uint8_t> block(64);
+    block.resize(rpp_flac_frame_header(&f, block.data()));
+    block.insert(block.end(), stream.begin(), stream.end());
+    std::vector<uint8_t> want(frames * 3 * 3);
+    for (size_t i = 0; i < x.size(); ++i) {
+      const uint32_t v = uint32_t(x[i]);
+      want[3 * i] = uint8_t(v >> 16), want[3 * i + 1] = uint8_t(v >> 8), want[3 * i + 2] = uint8_t(v);
+    }
+    CHECK(flac_block_decompressor::decompress(block) == want);
+    // a stream whose metadata does not parse
+    std::vector<uint8_t> bad(block.begin(), block.begin() + 12);
+    bad.resize(40, 0);
+    CHECK(throws<std::runtime_error>([&] { flac_block_decompressor d{bad}; }));
+  }
 }

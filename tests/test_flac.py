@@ -162,3 +162,12 @@ def test_flac_factory_options_and_description():
     assert req["number_of_channels"] == ["range", 1, 8] and req["bits_per_sample"] == ["range", 8, 32]
     with pytest.raises(RuntimeError, match="requires metadata"):
         FL.FlacBlockCompressor().compress(b"\0\0", None)
+
+
+def test_flac_metadata_json_is_nlohmann_dump():
+    # flac.cpp:368-379 / :429-440 build nlohmann::json objects, whose dump() sorts the keys and writes no
+    # spaces; the C++ facade (ricepp_facade.cpp) writes the same string
+    from dwarfs_amd import flac as FL
+    assert FL.FlacBlockCompressor().metadata_requirements() == (
+        '{"bits_per_sample":["range",8,32],"bytes_per_sample":["range",1,4],"endianness":["set",["big","little"]],'
+        '"number_of_channels":["range",1,8],"padding":["set",["msb","lsb"]],"signedness":["set",["signed","unsigned"]]}')
