@@ -666,7 +666,7 @@ struct SegArgs {
 };
 
 __device__ __forceinline__ bool seg_stream_ok(uint64_t n, uint64_t nb, uint32_t cs) {
-  return n % cs == 0 && n < rpp_internal::kSegMaxSamples && nb < (UINT64_C(1) << 29);
+  return rpp_internal::seg_stream_fits(n, nb, cs);
 }
 
 // unit -> stream, and the list capacity of each unit of a split stream: one

@@ -22,11 +22,20 @@ namespace rpp_internal {
 // (rerun passes, then one serial pass): the result is the serial parse's,
 // whatever the guesses were.
 // ---------------------------------------------------------------------------
-// Streams the segmented decode (and the four-streams-per-wave kernel) take:
-// their unit and sub-block position lists are 32-bit bit positions.  Longer
-// streams (up to RPP_MAX_STREAM_SAMPLES) are decoded one wave each by the
-// fused kernel, which rebases its positions as it goes.
+// The one-wave encode of a whole stream and the four-streams-per-wave decode
+// keep 32-bit bit positions for any data: streams below 2^27 samples (longer
+// ones are encoded in segments, decoded by the other kernels).
 constexpr uint64_t kSegMaxSamples = UINT64_C(1) << 27;
+// The segmented decode's unit, overshoot and sub-block positions are 32-bit
+// bit positions from the stream's 4-aligned base: it takes streams of any
+// sample count whose bytes stay below 2^29 minus room for a window's reads
+// past the end (round 5; before, streams below 2^27 samples only).  Longer
+// streams (compressed past 512 MiB) are decoded one wave each by the fused
+// kernel, which rebases its positions as it goes.
+constexpr uint64_t kSegMaxBytes = (UINT64_C(1) << 29) - (UINT64_C(1) << 16);
+__host__ __device__ inline bool seg_stream_fits(uint64_t n, uint64_t nb, uint32_t cs) {
+  return n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES && nb < kSegMaxBytes;
+}
 constexpr uint32_t kSegOvr = 16;             // headers recorded past a unit's region
 constexpr uint32_t kSegNone = 0xFFFFFFFFu;   // no position
 constexpr uint32_t kSpecSteps = 12;          // sub-blocks a candidate first header must chain through

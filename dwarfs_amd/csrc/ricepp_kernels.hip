@@ -2685,7 +2685,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       const uint64_t n64 = p.n_samples[b];
       const uint64_t ioff = p.in_off[b];
       const uint64_t nb64 = p.in_bytes[b];
-      if (n64 % CS != 0 || n64 >= rpp_internal::kSegMaxSamples || nb64 >= (UINT64_C(1) << 29)) {
+      if (!rpp_internal::seg_stream_fits(n64, nb64, CS)) {
         status = RPP_INVALID_ARGUMENT;
       } else {
         N = (uint32_t)n64;
@@ -3235,7 +3235,7 @@ __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(Parse
   const uint32_t ju = u - u0;
   if (nunits <= 1 || ju == 0) return;
   const uint64_t n64 = p.n_samples[b], ioff = p.in_off[b], nb64 = p.in_bytes[b];
-  if (n64 % CS != 0 || n64 >= rpp_internal::kSegMaxSamples || nb64 >= (UINT64_C(1) << 29)) return;
+  if (!rpp_internal::seg_stream_fits(n64, nb64, CS)) return;
   {
     copy_tables(dsm);
   }

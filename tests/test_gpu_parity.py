@@ -33,8 +33,8 @@ FUSED = codec.DecodeOptions(path="fused")
 
 def run_batch(cfg, blocks, in_align=8, dec=None):
     """Encodes the list of stored-sample arrays on the GPU, checks every
-    stream against the oracle, decodes on the GPU (decode options `dec`) and
-    checks the samples."""
+    stream against the oracle, decodes on the GPU (decode options `dec`, or
+    each of a list of them) and checks the samples."""
     oc = ocfg(cfg)
     offs, pos = [], 0
     for b in blocks:
@@ -58,14 +58,17 @@ def run_batch(cfg, blocks, in_align=8, dec=None):
         if got != w:
             diff = next((k for k in range(min(len(got), len(w))) if got[k] != w[k]), None)
             raise AssertionError(f"block {i} (n={ns[i]}): GPU {len(got)} B vs oracle {len(w)} B, first diff at {diff}")
-    out, dst = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns, options=dec)
-    torch.cuda.synchronize()
-    assert (dst.cpu().numpy() == 0).all(), dst
-    outn = out.cpu().numpy().view(np.uint16)
-    pos = 0
-    for i, b in enumerate(blocks):
-        assert np.array_equal(outn[pos:pos + len(b)], b), f"decode mismatch block {i}"
-        pos += len(b)
+    del data
+    for opt in dec if isinstance(dec, list) else [dec]:
+        out, dst = codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns, options=opt)
+        torch.cuda.synchronize()
+        assert (dst.cpu().numpy() == 0).all(), (opt, dst)
+        outn = out.cpu().numpy().view(np.uint16)
+        del out
+        pos = 0
+        for i, b in enumerate(blocks):
+            assert np.array_equal(outn[pos:pos + len(b)], b), f"decode mismatch block {i} ({opt})"
+            pos += len(b)
     return wants
 
 
@@ -549,16 +552,38 @@ def test_segmented_decode_of_a_64mib_stream():
 @pytest.mark.parametrize("cs", [1, 2])
 def test_stream_longer_than_2_27_samples(cs):
     """One stream of 2**27 + 5 samples (cs 1; 2**27 + 6 for cs 2) with short blocks beside it: past the
-    segmented encode's and decode's 2**27-sample unit range and, with the generator's ~14 bits per sample, past
-    2**30 bits, where the fused decode rebases its bit positions. Encoded on the GPU byte for byte as the oracle
-    (ricepp/ricepp_cpu.cpp encode), decoded back to the input (the default mode and the fused kernel)."""
+    one-wave encode's 2**27-sample range and, with the generator's ~14 bits per sample, past 2**30 bits, where
+    the fused decode rebases its bit positions. Encoded on the GPU byte for byte as the oracle
+    (ricepp/ricepp_cpu.cpp encode), decoded back to the input by the default mode, the segmented decode
+    (since round 5 it takes any stream compressed below 2**29 bytes: here it does, by units) and the fused
+    kernel."""
     rng = np.random.default_rng(2727 + cs)
     n = (1 << 27) + (5 if cs == 1 else 6)
     big = datagen.benchmark_data(rng, n) if cs == 1 else datagen.poisson_data(rng, n, lam=3000.0)
     blocks = [datagen.poisson_data(rng, 4096 * cs), big, datagen.poisson_data(rng, 777 * cs)]
     cfg = codec.CodecConfig(128, cs, "big", 0)
-    run_batch(cfg, blocks)
-    run_batch(cfg, blocks[1:2], dec=FUSED)
+    codec.segmented_decode_stats(reset=True)
+    run_batch(cfg, blocks, dec=[None, seg(), FUSED])
+    st = codec.segmented_decode_stats(reset=True)
+    assert st["met"] > 0 and st["fallback"] == 0, st
+
+
+def _chunked(gen, rng, n, parts=16, **kw):
+    step = (n + parts - 1) // parts
+    return np.concatenate([gen(rng, min(step, n - i), **kw) for i in range(0, n, step)])
+
+
+def test_stream_of_2_29_samples_past_2_32_bits():
+    """one stream of 2**29 + 3 samples of the benchmark generator (~14 bits per sample, 7.5e9
+    bits: past 2**32, with the segmented encode's 64-bit unit offsets near their largest and the fused
+    decode rebasing its 32-bit positions seven times; past the segmented decode's 2**29-byte range, so decoded
+    by the fused kernel), encoded byte for byte as the oracle and decoded back."""
+    rng = np.random.default_rng(2929)
+    n = (1 << 29) + 3
+    big = _chunked(datagen.benchmark_data, rng, n)
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    wants = run_batch(cfg, [big])
+    assert 8 * len(wants[0]) > (1 << 32)
 
 
 @pytest.mark.parametrize("bs", [17, 99, 200, 256, 512])

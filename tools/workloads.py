@@ -245,7 +245,29 @@ def case_e2e():
            transfer_bytes_note="encode D2H copies the worst-case-strided image (raw size + framing)")
 
 
-CASES = {"gen": case_gen, "fits": case_fits, "frames": case_frames, "mix": case_mix, "sweep": case_sweep,
+def case_giant():
+    """Streams of 2^27 samples and more (DwarFS -S 28..30 blocks): one stream each, decode by the default
+    path (segmented when the stream compresses below 2^29 bytes) against the fused kernel."""
+    cfg = codec.CodecConfig(128, 1, "big", 0)
+    for label, n, make in (("2^27+5 generator (~14 bits/sample)", (1 << 27) + 5, lambda n: gen_benchmark(n, 7)),
+                           ("2^28 Poisson(1000) (~7.7 bits/sample)", 1 << 28, lambda n: poisson_scaled(n, 1000.0, 0, 8)),
+                           ("2^29 Poisson(1000) (~7.7 bits/sample)", 1 << 29, lambda n: poisson_scaled(n, 1000.0, 0, 9))):
+        x = make(n)
+        p = pipe_for(cfg, x, [n])
+        raw = n * 2
+        te, td = timed(p.encode, iters=3), timed(p.decode, iters=3)
+        seg = codec.segmented_decode_stats(reset=True)
+        pf = pipe_for(cfg, x, [n], dec=codec.DecodeOptions(path="fused"))
+        tf = timed(pf.decode, iters=1, warm_s=0.0)
+        report("giant", layout=label, raw_MiB=raw / 2**20, ratio=round(int(p.sizes.sum()) / raw, 4),
+               encode_GiBps=round(raw / te / GIB, 2), decode_GiBps=round(raw / td / GIB, 2),
+               decode_fused_GiBps=round(raw / tf / GIB, 3), encode_ms=round(te * 1e3, 2), decode_ms=round(td * 1e3, 2),
+               decode_fused_ms=round(tf * 1e3, 1), segmented_stats=seg)
+        del p, pf, x
+        torch.cuda.empty_cache()
+
+
+CASES = {"gen": case_gen, "giant": case_giant, "fits": case_fits, "frames": case_frames, "mix": case_mix, "sweep": case_sweep,
          "e2e": case_e2e, "paths": case_paths}
 
 if __name__ == "__main__":
