@@ -402,8 +402,12 @@ class batch_queue {
     batch* b = nullptr;
     try {
       b = reserve(lk, r);
-    } catch (...) {  // (nothing holds r yet)
+    } catch (...) {  // (nothing holds r yet; contexts parked by discard() are pooled all the same)
+      std::vector<device_ctx*> parked;
+      parked.swap(discarded_);
       leave(lk);
+      lk.unlock();
+      for (device_ctx* c : parked) ctx_pool::get().release(c);
       throw;
     }
     std::vector<device_ctx*> unused;

@@ -1,4 +1,4 @@
-// Compile-only check (tests/test_native_abi.py) that DwarFS's ricepp plugin
+// Compile-only check (tests/test_native_abi.py) that DwarFS's ricepp and FLAC plugins
 // compiles against the facade with only its #include lines and the namespace
 // changed.  The function bodies restate the plugin's call expressions
 // (src/compression/ricepp.cpp:95-102 create_encoder with designated
@@ -81,3 +81,43 @@ static_assert(std::is_same_v<ricepp::encoder_interface<uint16_t>::pixel_type, ui
 static_assert(std::is_same_v<decltype(std::declval<ricepp::codec_config>().byteorder), std::endian>);
 
 }  // namespace plugin_shape
+
+// The FLAC plugin's classes forwarding to the facade (INTEGRATION.md §4 "The
+// FLAC codec"): src/compression/flac.cpp:215-393 (compressor: compress,
+// describe, metadata_requirements, get_compression_constraints) and
+// :405-489 (decompressor: metadata, decompress_frame, uncompressed_size).
+namespace flac_plugin_shape {
+
+class flac_block_compressor {
+ public:
+  flac_block_compressor(uint32_t level, bool exhaustive) : gpu_{level, exhaustive} {}
+  std::vector<uint8_t> compress(std::vector<uint8_t> const& data, std::string const* metadata) const {
+    return gpu_.compress(std::span<uint8_t const>{data}, metadata);
+  }
+  std::string describe() const { return gpu_.describe(); }
+  std::string metadata_requirements() const { return gpu_.metadata_requirements(); }
+  size_t granularity(std::string const& metadata) const { return gpu_.compression_granularity(metadata); }
+  size_t estimate_memory_usage(size_t data_size) const { return gpu_.estimate_memory_usage(data_size); }
+  std::unique_ptr<ricepp::flac_block_compressor> clone() const { return gpu_.clone(); }
+
+ private:
+  ricepp::flac_block_compressor gpu_;
+};
+
+class flac_block_decompressor {
+ public:
+  explicit flac_block_decompressor(std::span<uint8_t const> data) : gpu_{data} {}
+  std::optional<std::string> metadata() const { return gpu_.metadata(); }
+  size_t uncompressed_size() const { return gpu_.uncompressed_size(); }
+  void start_decompression(std::vector<uint8_t>* target) { gpu_.start_decompression(target); }
+  bool decompress_frame(size_t frame_size) { return gpu_.decompress_frame(frame_size); }
+
+ private:
+  ricepp::flac_block_decompressor gpu_;
+};
+
+inline std::unique_ptr<ricepp::flac_block_compressor> factory(std::string const& spec) {
+  return ricepp::flac_block_compressor::create(spec);  // "flac:level=8:exhaustive"
+}
+
+}  // namespace flac_plugin_shape
