@@ -43,10 +43,16 @@
 namespace {
 
 constexpr uint32_t kTile = 256;          // sub-blocks (lanes) per tile
-// 64 KiB of the stream per tile in LDS: a tile's 256 sub-blocks at bs 128
-// take up to 16 bits per sample; with 36 KiB, generator data (14 bits per
-// sample) left 40 % of each tile's lanes unstaged, on the general path
+// The stream's words of a tile in LDS.  64 KiB: a tile's 256 sub-blocks at
+// bs 128 take up to 16 bits per sample (with 36 KiB, generator data -- 14
+// bits per sample -- left 40 % of each tile's lanes unstaged, on global
+// reads), two workgroups per CU.  48 KiB: three workgroups per CU (<= 168
+// VGPRs), tiles up to ~12 bits per sample staged whole -- for batches of many
+// tiles, where throughput, not one tile's latency, is the time: configs[3]
+// mix decode 50.8 -> 47.3 ms, a lone 16 MiB generator stream 0.95 -> 1.03 ms
+// (profiles/r05_extract_stage_ab.jsonl)
 constexpr uint32_t kStageWords = 16384;
+constexpr uint32_t kStageWordsMany = 12288;
 // slack after the staged words: a lane whose codes run past their window
 // (then decoded again by the general path) reads at most 128 * 45 bits on
 constexpr uint32_t kStagePad = 192;
@@ -348,9 +354,9 @@ __device__ __forceinline__ uint32_t px_write2(uint32_t v, uint32_t sel, uint32_t
 
 // BS: the block size of the fast lanes' unrolled decode (16..128); BS = 0 is
 // any other block size (the run-time p.bs), decoded by general lanes only.
-template <uint32_t CS, uint32_t BS, bool SH>
-__global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) {
-  __shared__ __attribute__((aligned(16))) uint32_t stage[kStageWords + kStagePad];
+template <uint32_t CS, uint32_t BS, bool SH, uint32_t STAGE>
+__global__ __launch_bounds__(kTile, STAGE == kStageWords ? 2 : 3) void rpp_extract_kernel(ExtractParams p) {
+  __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE + kStagePad];
   __shared__ uint32_t scan_buf[kTile];
   __shared__ uint32_t sh_tile, sh_carry[2], sh_min;
   __shared__ uint32_t wtot[kTile / 64][2];
@@ -413,7 +419,7 @@ __global__ __launch_bounds__(kTile, 2) void rpp_extract_kernel(ExtractParams p) 
     //      the last byte) ----
     const uint32_t w0 = pos_tab[k0] >> 5;
     const uint32_t wend = (pos_tab[k0 + kcount] >> 5) + 2;
-    const uint32_t nst = min(wend - w0, kStageWords);
+    const uint32_t nst = min(wend - w0, STAGE);
     {
       const uint32_t l = tid & 63u, wv = tid >> 6;
       for (uint32_t c = wv; 64 * c < nst; c += kTile / 64) {
@@ -973,15 +979,24 @@ __global__ void rpp_seg_tail_kernel(SegArgs a) {
 
 using ExtractKernel = void (*)(ExtractParams);
 
-template <uint32_t CS, bool SH>
+template <uint32_t CS, bool SH, uint32_t STAGE>
 ExtractKernel extract_kernel_for(uint32_t bs) {
   switch (bs) {
-    case 16: return rpp_extract_kernel<CS, 16, SH>;
-    case 32: return rpp_extract_kernel<CS, 32, SH>;
-    case 64: return rpp_extract_kernel<CS, 64, SH>;
-    case 128: return rpp_extract_kernel<CS, 128, SH>;
-    default: return rpp_extract_kernel<CS, 0, SH>;  // (general lanes: bs 256 / 512 / not a power of two)
+    case 16: return rpp_extract_kernel<CS, 16, SH, STAGE>;
+    case 32: return rpp_extract_kernel<CS, 32, SH, STAGE>;
+    case 64: return rpp_extract_kernel<CS, 64, SH, STAGE>;
+    case 128: return rpp_extract_kernel<CS, 128, SH, STAGE>;
+    default: return rpp_extract_kernel<CS, 0, SH, STAGE>;  // (general lanes: bs 256 / 512 / not a power of two)
   }
+}
+template <uint32_t STAGE>
+ExtractKernel extract_kernel(const rpp_config* cfg) {
+  const bool sh = cfg->unused_lsb_count != 0;
+  return cfg->component_stream_count == 1
+             ? (sh ? extract_kernel_for<1, true, STAGE>(cfg->block_size)
+                   : extract_kernel_for<1, false, STAGE>(cfg->block_size))
+             : (sh ? extract_kernel_for<2, true, STAGE>(cfg->block_size)
+                   : extract_kernel_for<2, false, STAGE>(cfg->block_size));
 }
 
 // The segmented decode forks the fused launch of a batch's one-unit streams
@@ -1352,12 +1367,10 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
   if ((st = rpp_exclusive_scan_u64(w.cnt2, U + 1, w.off2, s)) != RPP_OK) return st;
   hipLaunchKernelGGL(rpp_seg_write_kernel, dim3((uint32_t)U), dim3(kSegThreads), 0, s, a);
   hipLaunchKernelGGL(rpp_seg_tail_kernel, dim3(g256), dim3(256), 0, s, a);
-  const bool sh = cfg->unused_lsb_count != 0;
-  const ExtractKernel k = cfg->component_stream_count == 1
-                              ? (sh ? extract_kernel_for<1, true>(cfg->block_size)
-                                    : extract_kernel_for<1, false>(cfg->block_size))
-                              : (sh ? extract_kernel_for<2, true>(cfg->block_size)
-                                    : extract_kernel_for<2, false>(cfg->block_size));
+  // (a batch of more tiles than the grid holds: the smaller stage, three
+  // workgroups per CU)
+  const ExtractKernel k = w.max_tiles >= kMaxExtractGrid ? extract_kernel<kStageWordsMany>(cfg)
+                                                         : extract_kernel<kStageWords>(cfg);
   ExtractParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_out, d_out_offsets, d_status, w.sb_pos, w.sb_base,
                   w.tile_base, w.tile_map, w.tile_lt, w.lvl_base + w.levels, w.tile_state, w.counter, nblocks,
                   cfg->block_size, cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count, test};
