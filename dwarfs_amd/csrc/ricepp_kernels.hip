@@ -786,17 +786,6 @@ __global__ __launch_bounds__(256) void rpp_enc_concat_kernel(EncParams p, const 
   const uint64_t o_n = o_k + L_k;  // next segment's offset
   uint8_t* out8 = p.out + p.out_off[b];
   uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
-  // bits [x, x + 32) of this segment (zero past its end)
-  auto seg_bits32 = [&](uint32_t x) -> uint32_t {
-    if (x >= L_k) return 0u;
-    const uint32_t i = x >> 5, sh = x & 31u;
-    const uint32_t lo = src[i];
-    const uint32_t hi = (32 * (i + 1) < L_k) ? src[i + 1] : 0u;
-    uint32_t v = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
-    const uint32_t have = L_k - x;
-    if (have < 32) v &= (1u << have) - 1u;
-    return v;
-  };
   auto put = [&](uint32_t w, uint32_t v) {
     if (4ull * w + 4 <= total_bytes) {
       out32[w] = v;
@@ -804,12 +793,33 @@ __global__ __launch_bounds__(256) void rpp_enc_concat_kernel(EncParams p, const 
       for (uint32_t c = 0; 4ull * w + c < total_bytes; ++c) out8[4ull * w + c] = (uint8_t)(v >> (8 * c));
     }
   };
-  // words whose first bit lies in this segment
+  // words whose first bit lies in this segment, four per thread (one 16-byte
+  // store for a group inside the segment and the stream): word w holds
+  // segment bits [32 (w - w_begin) + sh0, + 32), i.e. a funnel shift of
+  // slot words w - w_begin and w - w_begin + 1 by the segment's constant sh0
   const uint32_t w_begin = (uint32_t)((o_k + 31) >> 5), w_end = (uint32_t)((o_n + 31) >> 5);
-  for (uint32_t w = w_begin + threadIdx.x; w < w_end; w += blockDim.x) {
-    uint32_t v = seg_bits32((uint32_t)(32ull * w - o_k));
-    if (!last && 32ull * w + 32 > o_n) v |= nxt[0] << (uint32_t)(o_n - 32ull * w);  // (the next segment is >= 1024 bits)
-    put(w, v);
+  const uint32_t sh0 = (uint32_t)(32ull * w_begin - o_k);
+  const uint32_t nsrc = (L_k + 31) >> 5;  // (the slot's last word is zero-padded past L_k)
+  const uint32_t first_next = last ? 0u : nxt[0];  // (the next segment is >= 1024 bits)
+  for (uint32_t g = (w_begin >> 2) + threadIdx.x; g < (w_end + 3) >> 2; g += blockDim.x) {
+    const int64_t i0 = 4 * (int64_t)g - w_begin;  // slot word of output word 4 g
+    uint32_t sw[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) sw[j] = i0 + j >= 0 && i0 + j < (int64_t)nsrc ? src[i0 + j] : 0u;
+    uint32_t v[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t w = 4 * g + j;
+      v[j] = __builtin_amdgcn_alignbit(sw[j + 1], sw[j], sh0);
+      if (!last && 32ull * w + 32 > o_n && 32ull * w < o_n) v[j] |= first_next << (uint32_t)(o_n - 32ull * w);
+    }
+    if (4 * g >= w_begin && 4 * g + 4 <= w_end && 16ull * g + 16 <= total_bytes) {
+      *reinterpret_cast<uint4*>(out32 + 4 * (size_t)g) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j)
+        if (4 * g + j >= w_begin && 4 * g + j < w_end) put(4 * g + j, v[j]);
+    }
   }
   // the word holding o_1: segment 0's bits below it, segment 1's above
   if (k == 1 && (o_k & 31u) && threadIdx.x == 0) {
