@@ -2037,9 +2037,7 @@ constexpr uint32_t kRowChunk = 64;                   // refill unit: 16 lanes x 
 constexpr uint32_t kRowDump = 40;                    // first list pair of lanes past the sub-block
 constexpr uint32_t kRowMT = 24;                      // terminators per 24-bit segment at most (fs 0: 1-bit codes)
 constexpr uint32_t kRowListWords = 4 + 2 * (kRowDump + kRowMT);
-// two lists per row: the parse of sub-block s+1 fills one while the values of
-// sub-block s are read from the other (the step loop is software-pipelined)
-constexpr uint32_t kRowWords = kRowRing + kRowPad + 2 * kRowListWords;
+constexpr uint32_t kRowWords = kRowRing + kRowPad + kRowListWords;
 constexpr uint32_t kRowsLdsBytes = kTabBytes + kRowsWaves * 4 * kRowWords * 4;
 
 
@@ -2073,9 +2071,8 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
   __syncthreads();
   const uint4* tab = dsm;
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + kTabBytes / 4 + (wv * 4 + row) * kRowWords;
-  uint32_t* const listA = ring + kRowRing + kRowPad + 4;
-  uint32_t* const listB = listA + kRowListWords;
-  if (ri < 4) listA[(int)ri - 4] = listB[(int)ri - 4] = 0u;  // pair -1 = (0, 0): a_(-1) of the deltas
+  uint32_t* list = ring + kRowRing + kRowPad + 4;
+  if (ri < 4) list[(int)ri - 4] = 0u;  // pair -1 = (0, 0): a_(-1) of the deltas
   const uint32_t be = p.be, ulsb = p.ulsb;
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;
   const uint32_t selpack = be ? 0x04050001u : 0x05040100u;
@@ -2156,38 +2153,13 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
     }
     if (votes >= 5) active = false;
   }
-  uint32_t s = 0;  // sub-blocks the row has parsed
+  uint32_t s = 0;  // the row's sub-block
   ScanRegs sreg;
-  // The values of a parsed sub-block (row-uniform), decoded one iteration
-  // after its parse: an iteration parses sub-block s+1 and decodes the values
-  // of sub-block s, in one basic block, so that the value work (list reads,
-  // deltas, the delta scan, stores) fills the latency gaps of the parse chain
-  // (ring read -> table reads -> map scan -> counts -> end lane -> next
-  // header) -- with one wave per SIMD nothing else can
-  struct Pend {
-    uint32_t fs, n, comp, cbase;
-    bool zero, ok;
-  };
-  Pend z{1u, 0u, 0u, 0u, true, false};  // (nothing pending)
-  uint32_t cur = 0;                     // the list the next parse fills
+  uint2* const list2 = reinterpret_cast<uint2*>(list);
+  const uint4* const list4 = reinterpret_cast<const uint4*>(list);
 
-  // parse one sub-block of every active row into list `cur` (MT: terminators a
-  // segment can hold) and decode the values of the pending one from the other
-  auto iter = [&]<uint32_t MT>() {
-    uint32_t* const wl = cur ? listB : listA;
-    const uint32_t* const rl = cur ? listA : listB;
-    // ---- values of the pending sub-block: its list pairs ----
-    uint4 tt4;
-    uint2 tt2;
-    uint32_t aprev;
-    if constexpr (TWO) {
-      tt4 = reinterpret_cast<const uint4*>(rl)[ri];
-      aprev = rl[4 * ri - 2];
-    } else {
-      tt2 = reinterpret_cast<const uint2*>(rl)[ri];
-      aprev = rl[2 * ri - 2];
-    }
-    // ---- parse: maps, row scan, entry states, terminators, counts ----
+  // one sub-block of every active row; MT: terminators a segment can hold
+  auto step = [&]<uint32_t MT>() {
     const uint32_t q = P;
     const uint32_t* w = word_at(q >> 5);
     const uint32_t h = __builtin_amdgcn_alignbit(w[1], w[0], q & 31u) & 15u;
@@ -2200,6 +2172,7 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
     const uint32_t k = fs + 1;
     const uint32_t comp = s % CS, cbase = (s / CS) * chunk_len;
     const uint32_t n = active ? min(N - cbase, chunk_len) / CS : BS;
+    // ---- parse: maps, row scan, entry states, terminators, counts ----
     const uint4* tb = tab + 256u * fs;
     const uint4 e0 = tb[xl & 0xFFu], e1 = tb[__builtin_amdgcn_ubfe(xl, 8, 8)], e2 = tb[__builtin_amdgcn_ubfe(xl, 16, 8)];
     const Map8 M01 = comp8(Map8{e1.x, e1.y}, Map8{e0.x, e0.y});
@@ -2249,64 +2222,58 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
     const uint32_t tend = (uint32_t)__shfl((int)tsel, (int)((lane & 48u) | (lz & 15u)));
     const uint32_t Pe = zero ? q + 4 : q + kSegBits * lz + tend + k;
     const bool ok = active && (zero || (rice && mrow != 0)) && Pe <= lim;
-
-    // ---- values of the pending sub-block: codes -> zig-zag deltas ->
-    //      values -> stores ----
-    {
-      uint32_t d0 = 0, d1 = 0, dsum = 0;
-      if constexpr (TWO) {
-        const uint32_t df0 = lshl_or(tt4.x - aprev, z.fs, tt4.y), df1 = lshl_or(tt4.z - tt4.x, z.fs, tt4.w);
-        d0 = (df0 >> 1) ^ neg_lsb(df0);
-        d1 = (df1 >> 1) ^ neg_lsb(df1);
-        if (z.zero || 2 * ri >= z.n) d0 = 0;
-        if (z.zero || 2 * ri + 1 >= z.n) d1 = 0;
-        dsum = d0 + d1;
-      } else {
-        const uint32_t df = lshl_or(tt2.x - aprev, z.fs, tt2.y);
-        d1 = (df >> 1) ^ neg_lsb(df);
-        if (z.zero || ri >= z.n) d1 = 0;
-        dsum = d1;
-      }
-      const uint32_t inc = row_incl_sum(dsum);
-      const uint32_t lastc = z.comp ? last1 : last0;
-      const uint32_t v1 = lastc + inc;  // value of the lane's last code (mod 2^16)
-      uint16_t* dst = out + z.cbase + z.comp;
-      if (z.ok) {
-        if constexpr (TWO) {
-          const uint32_t v0 = v1 - d1;
-          if (CS == 1 && 2 * ri + 1 < z.n && ((((uintptr_t)dst) & 3u) == 0)) {
-            const uint32_t o2 = SH ? px_write2(__builtin_amdgcn_perm(v1, v0, 0x05040100u), selbe, ulsb)
-                                   : __builtin_amdgcn_perm(v1, v0, selpack);
-            *reinterpret_cast<uint32_t*>(dst + 2 * ri) = o2;
-          } else {
-            if (2 * ri < z.n) dst[CS * 2 * ri] = (uint16_t)px_write(v0 & 0xFFFFu, be, ulsb);
-            if (2 * ri + 1 < z.n) dst[CS * (2 * ri + 1)] = (uint16_t)px_write(v1 & 0xFFFFu, be, ulsb);
-          }
-        } else {
-          if (ri < z.n) dst[CS * ri] = (uint16_t)px_write(v1 & 0xFFFFu, be, ulsb);
-        }
-      }
-      const uint32_t tot = (uint32_t)__shfl((int)inc, (int)(lane | 15u));
-      if (z.ok) {
-        const uint32_t lnew = (lastc + tot) & 0xFFFFu;
-        if (z.comp) last1 = lnew;
-        else last0 = lnew;
-      }
-    }
-
     // ---- terminators -> (a_i, remainder) list pairs (as the fused loop) ----
     const uint32_t base = ok && !zero && cnt != 0 && excl < n ? excl : kRowDump;
     const uint32_t abase = lane24 - 4u - base * k;
     const uint32_t xr = xl >> 1;
-    uint2* const wl2 = reinterpret_cast<uint2*>(wl);
 #pragma unroll
     for (int j = (int)MT - 1; j >= 0; --j) {
-      wl2[base + j] = make_uint2(abase + t[j] - (uint32_t)j * k, __builtin_amdgcn_ubfe(xr, t[j], fs));
+      list2[base + j] = make_uint2(abase + t[j] - (uint32_t)j * k, __builtin_amdgcn_ubfe(xr, t[j], fs));
       lds_fence();
     }
-    z = Pend{fs, n, comp, cbase, zero, ok};
-    cur ^= 1u;
+    // ---- codes -> zig-zag deltas -> values -> stores ----
+    uint32_t d0 = 0, d1 = 0, dsum = 0;
+    if constexpr (TWO) {
+      const uint4 tt = list4[ri];
+      const uint32_t aprev = list[4 * ri - 2];
+      const uint32_t df0 = lshl_or(tt.x - aprev, fs, tt.y), df1 = lshl_or(tt.z - tt.x, fs, tt.w);
+      d0 = (df0 >> 1) ^ neg_lsb(df0);
+      d1 = (df1 >> 1) ^ neg_lsb(df1);
+      if (zero || 2 * ri >= n) d0 = 0;
+      if (zero || 2 * ri + 1 >= n) d1 = 0;
+      dsum = d0 + d1;
+    } else {
+      const uint2 tt = list2[ri];
+      const uint32_t aprev = list[2 * ri - 2];
+      const uint32_t df = lshl_or(tt.x - aprev, fs, tt.y);
+      d1 = (df >> 1) ^ neg_lsb(df);
+      if (zero || ri >= n) d1 = 0;
+      dsum = d1;
+    }
+    const uint32_t inc = row_incl_sum(dsum);
+    const uint32_t lastc = comp ? last1 : last0;
+    const uint32_t v1 = lastc + inc;  // value of the lane's last code (mod 2^16)
+    uint16_t* dst = out + cbase + comp;
     if (ok) {
+      if constexpr (TWO) {
+        const uint32_t v0 = v1 - d1;
+        if (CS == 1 && 2 * ri + 1 < n && ((((uintptr_t)dst) & 3u) == 0)) {
+          const uint32_t o2 = SH ? px_write2(__builtin_amdgcn_perm(v1, v0, 0x05040100u), selbe, ulsb)
+                                 : __builtin_amdgcn_perm(v1, v0, selpack);
+          *reinterpret_cast<uint32_t*>(dst + 2 * ri) = o2;
+        } else {
+          if (2 * ri < n) dst[CS * 2 * ri] = (uint16_t)px_write(v0 & 0xFFFFu, be, ulsb);
+          if (2 * ri + 1 < n) dst[CS * (2 * ri + 1)] = (uint16_t)px_write(v1 & 0xFFFFu, be, ulsb);
+        }
+      } else {
+        if (ri < n) dst[CS * ri] = (uint16_t)px_write(v1 & 0xFFFFu, be, ulsb);
+      }
+    }
+    const uint32_t tot = (uint32_t)__shfl((int)inc, (int)(lane | 15u));
+    if (ok) {
+      const uint32_t lnew = (lastc + tot) & 0xFFFFu;
+      if (comp) last1 = lnew;
+      else last0 = lnew;
       P = Pe;
       if (++s == nsb) {
         active = false;
@@ -2323,10 +2290,10 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
     // fs 2..4 (codes of >= 3 bits), else 4
     const uint32_t* w = word_at(P >> 5);
     const uint32_t h = __builtin_amdgcn_alignbit(w[1], w[0], P & 31u) & 15u;
-    if (__any(active && h == 1u)) iter.template operator()<kRowMT>();
-    else if (__any(active && h == 2u)) iter.template operator()<12>();
-    else if (__any(active && h - 3u <= 2u)) iter.template operator()<8>();
-    else iter.template operator()<4>();
+    if (__any(active && h == 1u)) step.template operator()<kRowMT>();
+    else if (__any(active && h == 2u)) step.template operator()<12>();
+    else if (__any(active && h - 3u <= 2u)) step.template operator()<8>();
+    else step.template operator()<4>();
     // ---- ring: once a row's look-ahead drops below 40 words, every row with
     //      room takes its prefetched chunk and prefetches the next ----
     if (__any(active && fill_w < (P >> 5) + 40u)) {
@@ -2339,9 +2306,6 @@ __global__ __launch_bounds__(kWave* kRowsWaves) void rpp_decode_rows_kernel(DecP
       lds_fence();
     }
   }
-  // the last parsed sub-block's values (an iteration with no active row
-  // parses nothing: every row's ok is false)
-  if (__any(z.ok)) iter.template operator()<4>();
   if (ri == 0 && b < p.nblocks) p.status[b] = status;
 }
 
