@@ -217,6 +217,16 @@ __device__ __forceinline__ uint32_t gsum(uint32_t v) {
   return v;
 }
 
+// Wave-uniform "any active lane has c", branched on through a VCC written by
+// the scalar unit.  __any() compiles to v_cmp -> s_cbranch_vccz; at the
+// emission fast-path test that branch measured to go the wrong way now and
+// then on gfx950 with several waves per SIMD (bs 128 cs 2 high-entropy
+// batches: most 64 KiB streams wrong, run to run different; through the
+// scalar unit: none).  DESIGN.md section 4 "Uniform branches".
+__device__ __forceinline__ bool wave_any_salu(bool c) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(__builtin_amdgcn_ballot_w64(c) != 0)) != 0u;
+}
+
 // Per-lane sub-block geometry of one encode iteration.
 struct EncGeom {
   uint32_t n;        // samples in this lane's sub-block (0: no sub-block)
@@ -453,7 +463,7 @@ __device__ __forceinline__ void enc_plan_b(EncPlan<SPL>& P, EncState& st, uint32
   walk_step(P.walking && P.cand > 0 && P.cand < 14);
   for (;;) {
     const bool act = P.walking && P.cand > 0 && P.cand < 14;
-    if (!__any(act)) break;
+    if (!wave_any_salu(act)) break;
     walk_step(act);
   }
   // encode.h:127-156: 0 = all-zero, 1 = Rice, 2 = raw
@@ -498,7 +508,7 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
     // the pair (2h, 2h+1) spans k + q_(2h+1) + k bits from code 2h's '1':
     // when that fits 32 bits for every pair of the wave (fs <= 13 and unary
     // runs short: Poisson data), one 64-bit shift and two ds_or_b32 per pair
-    if (!__any(2u * k + (as_u32(qmax) >> 16) > 32u)) {
+    if (!wave_any_salu(2u * k + (as_u32(qmax) >> 16) > 32u)) {
 #pragma unroll
       for (uint32_t h = 0; h < SPL / 2; ++h) {
         const uint32_t qq = as_u32(qv[h]);

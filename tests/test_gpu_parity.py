@@ -318,6 +318,13 @@ def test_full_size_4096x64k_benchmark_generator_bit_exact():
     _full_size("benchmark")
 
 
+def test_full_size_4096x64k_generator_two_streams_bit_exact():
+    """Two component streams (bs 128 cs 2) on high-entropy data: the launch that runs several encode waves per SIMD
+    and takes the emission slow path in almost every group (the fast/slow test once branched on a v_cmp-written
+    VCC and went the wrong way in most streams here; DESIGN.md section 4 "Uniform branches")."""
+    _full_size("benchmark", cs=2)
+
+
 @pytest.mark.parametrize("mib", [1, 4, 16])
 def test_large_blocks(mib):
     rng = np.random.default_rng(mib)
@@ -546,6 +553,22 @@ def test_segmented_decode_of_a_64mib_stream():
     x = datagen.poisson_data(rng, 32 << 20, lam=700.0, ulsb=1, big_endian=False)
     codec.segmented_decode_stats(reset=True)
     run_batch(codec.CodecConfig(128, 2, "little", 1), [x])
+    assert codec.segmented_decode_stats(reset=True)["met"] > 0
+
+
+@pytest.mark.parametrize("cs", [1, 2])
+def test_segmented_decode_many_tiles(cs):
+    """A batch of >= 2048 extraction tiles (8 x 16 MiB streams at bs 128: 2048 tiles of 256 sub-blocks) takes
+    the extraction kernel with the 48 KiB stage (three workgroups per CU): Poisson streams of three densities
+    (one tile per window) and a generator stream (14 bits per sample: lanes past the stage read the stream
+    from memory), with 1 MiB blocks between them -- encoded byte for byte as the oracle and decoded back."""
+    rng = np.random.default_rng(4848 + cs)
+    n16 = (8 << 20) // cs * cs
+    blocks = [datagen.poisson_data(rng, n16, lam=float(lam)) for lam in (300, 1000, 3000, 1000, 300, 3000, 1000)]
+    blocks.insert(3, datagen.benchmark_data(rng, n16))
+    blocks += [datagen.poisson_data(rng, (1 << 19) // cs * cs) for _ in range(3)]
+    codec.segmented_decode_stats(reset=True)
+    run_batch(codec.CodecConfig(128, cs, "big", 0), blocks)
     assert codec.segmented_decode_stats(reset=True)["met"] > 0
 
 
