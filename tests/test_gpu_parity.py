@@ -281,13 +281,16 @@ def test_corrupt_streams_match_oracle(bs, cs, dec=None):
             assert np.array_equal(outn[i * n:(i + 1) * n], want), i
 
 
-def _full_size(kind, nblocks=4096, n=32768, bs=128, cs=1, nthreads=8, dec=None):
+def _full_size(kind, nblocks=4096, n=32768, bs=128, cs=1, nthreads=8, dec=None, byteorder="big", ulsb=0):
     rng = np.random.default_rng(42)
     if kind == "poisson":
         x = datagen.poisson_data(rng, nblocks * n)
     else:
         x = datagen.benchmark_data(rng, nblocks * n)
-    cfg = codec.CodecConfig(bs, cs, "big", 0)
+    if ulsb:  # unused low bits are zero in the pixel values (ricepp_cpuspecific_traits.h:63-67), else no round trip
+        keep = np.uint16((0xFFFF << ulsb) & 0xFFFF)
+        x = x & (keep.byteswap() if byteorder == "big" else keep)
+    cfg = codec.CodecConfig(bs, cs, byteorder, ulsb)
     oc = ocfg(cfg)
     offs = np.arange(nblocks, dtype=np.int64) * n
     d = torch.from_numpy(x.view(np.int16)).to(DEV)
@@ -323,6 +326,21 @@ def test_full_size_4096x64k_generator_two_streams_bit_exact():
     and takes the emission slow path in almost every group (the fast/slow test once branched on a v_cmp-written
     VCC and went the wrong way in most streams here; DESIGN.md section 4 "Uniform branches")."""
     _full_size("benchmark", cs=2)
+
+
+@pytest.mark.parametrize("kind", ["poisson", "benchmark"])
+@pytest.mark.parametrize("cs", [1, 2])
+@pytest.mark.parametrize("bs", [16, 32, 64, 256, 512])
+def test_at_scale_block_sizes(bs, cs, kind):
+    """2048 x 64 KiB blocks (eight encode waves per CU, the occupancy at which the bs 128 cs 2 emission branch once
+    went wrong) for every other block size, both component counts, low and high entropy: bit-exact encode against the
+    oracle and decode round trip."""
+    _full_size(kind, nblocks=2048, bs=bs, cs=cs)
+
+
+@pytest.mark.parametrize("bs,cs,byteorder,ulsb", [(128, 2, "little", 0), (128, 2, "big", 3), (64, 2, "little", 2)])
+def test_at_scale_byteorder_lsb(bs, cs, byteorder, ulsb):
+    _full_size("benchmark", nblocks=2048, bs=bs, cs=cs, byteorder=byteorder, ulsb=ulsb)
 
 
 @pytest.mark.parametrize("mib", [1, 4, 16])
