@@ -7,17 +7,23 @@
 // fixture.  The decoder accepts every frame kind RFC 9639 defines (constant,
 // verbatim, fixed and LPC subframes, wasted bits, both Rice methods, escape
 // partitions, the four channel assignments, any block size code), so it reads
-// libFLAC's streams; the encoder writes a subset (fixed predictors), so its
-// streams differ from libFLAC's but are valid FLAC.  Checked against the CPU
-// restatement in oracle/flac_oracle.c both ways (tests/test_gpu_flac.py).
+// libFLAC's streams; the encoder writes constant, verbatim, fixed and LPC
+// subframes (no escape partitions), so its streams differ from libFLAC's but
+// are valid FLAC.  Checked against the CPU restatement in oracle/flac_oracle.c
+// both ways (tests/test_gpu_flac.py).
 //
 // Encode (rpp_flac_encode): one wave per 4096-sample frame (libFLAC's level-5
 // block size; flac.cpp:311-313 sets level 5 by default, :516).  The frame's
 // channels are staged in LDS; per subframe source the wave finds the wasted
 // low bits, the constant case, the fixed predictor order with the smallest
-// sum of |residual| (orders 0-4, as libFLAC's fixed-order estimate) and the
-// Rice partition order (0-5) and per-partition parameters with the fewest
-// bits, and for two channels the cheapest of the four channel assignments;
+// sum of |residual| (orders 0-4, as libFLAC's fixed-order estimate), an LPC
+// predictor (levels 3-8: libFLAC's presets' maximum order 6 / 8 / 12;
+// tukey(0.5)-windowed autocorrelation, Levinson-Durbin, the order by the
+// expected-bits estimate or, exhaustive, every order coded; coefficients
+// quantized to libFLAC's automatic precision with error feedback), the Rice
+// partition order and per-partition parameters with the fewest bits for each,
+// the cheapest subframe, and for two channels the cheapest of the four
+// channel assignments;
 // then the codes of each row of 64 samples are placed by one wave prefix sum
 // and OR-ed into an LDS bit window (MSB-first words, byte-swapped on the way
 // out).  Frames go to worst-case slots, are packed back to back
@@ -173,12 +179,18 @@ struct FlacEncParams {
   uint64_t slot_bytes;
   uint64_t* sizes;      // [frames] frame bytes (CRC-16 included)
   uint32_t frames;
+  uint32_t max_lpc;     // LPC orders 1..max_lpc (0: fixed predictors only)
+  uint32_t exhaustive;  // code every LPC order (else the expected-bits estimate picks one)
+  uint32_t max_po;      // Rice partition orders 0..max_po (<= kMaxPo)
 };
 
+constexpr uint32_t kMaxLpc = 12;  // libFLAC's presets: -l 6 (level 3), 8 (4-6), 12 (7-8)
+
 struct SubPlan {
-  uint32_t type;     // 0 constant, 1 verbatim, 2 fixed
+  uint32_t type;     // 0 constant, 1 verbatim, 2 fixed, 3 LPC
   uint32_t order, wasted, bps;  // bps: of the coded samples (after wasted bits)
   uint32_t po, method;
+  uint32_t prec, shift;  // LPC: coefficient precision and shift (coefficients in EncShared::lpcq[src])
   uint64_t bits;
 };
 
@@ -189,7 +201,12 @@ struct EncShared {
   unsigned long long psum[1u << kMaxPo];
   unsigned long long pbits[kMaxPo + 1][1u << kMaxPo];
   uint32_t kt[2u << kMaxPo];  // Rice parameter of partition p of order po at [2^po - 1 + p]
-  uint32_t ures[kFlacBlock];  // the planned source's folded residuals
+  uint32_t ures[kFlacBlock];  // the planned source's folded residuals (LPC analysis: the windowed samples)
+  int32_t lpcq[4][kMaxLpc];   // quantized LPC coefficients of the chosen plan per source
+  int32_t lpct[kMaxLpc];      // ... of the LPC order being tried
+  double ac[kMaxLpc + 1];     // autocorrelation of the windowed source
+  double lerr[kMaxLpc + 1];   // Levinson residual energy per order
+  uint32_t bad;               // a residual of the plan being tried does not fit 32 bits
 };
 
 // source sample i: 0 / 1 = staged channel, 2 = side (L - R), 3 = mid ((L + R) >> 1)
@@ -216,9 +233,163 @@ __device__ __forceinline__ int64_t fixed_res(const EncShared& sh, uint32_t src, 
   }
 }
 
+__device__ __forceinline__ int64_t lpc_res(const EncShared& sh, const int32_t* q, uint32_t src, uint32_t i,
+                                           uint32_t order, uint32_t shift, uint32_t wasted) {
+  int64_t pred = 0;
+  for (uint32_t j = 0; j < order; ++j) pred += (int64_t)q[j] * (src_sample(sh, src, i - 1 - j) >> wasted);
+  return (src_sample(sh, src, i) >> wasted) - (pred >> shift);
+}
+
+// Rice partition plan of the residuals res(i), i in [order, bs): partition
+// orders 0..po_cap that divide bs with a first partition longer than the
+// predictor order, per partition k = floor(log2(mean u)); the cheapest order
+// and method in bpo / bmethod, its parameters in sh.kt[2^bpo - 1 + p].
+// Returns the residual's bits (its 6-bit header included), or ~0 when a
+// residual does not fit 32 bits.
+template <class Res>
+__device__ uint64_t rice_plan(EncShared& sh, uint32_t bs, uint32_t order, uint32_t po_cap, Res&& res,
+                              uint32_t& bpo, uint32_t& bmethod) {
+  const uint32_t lane = lane_id();
+  for (uint32_t p = lane; p < (1u << kMaxPo); p += kWave) sh.psum[p] = 0;
+  for (uint32_t p = lane; p < (kMaxPo + 1) * (1u << kMaxPo); p += kWave) (&sh.pbits[0][0])[p] = 0;
+  if (lane == 0) sh.bad = 0;
+  __syncthreads();
+  uint32_t pomax = 0;
+  while (pomax < po_cap && bs % (2u << pomax) == 0 && (bs >> (pomax + 1)) > order) ++pomax;
+  const uint32_t psz = bs >> pomax;  // samples per finest partition
+  // (a lane's samples run through the partitions in order: its sums go to LDS
+  // once per partition, not once per sample)
+  {
+    uint32_t cur = ~0u, q = 0, qend = psz, bad = 0;
+    uint64_t acc = 0;
+    for (uint32_t i = lane; i < bs; i += kWave) {
+      if (i < order) continue;
+      while (i >= qend) ++q, qend += psz;
+      if (q != cur) {
+        if (acc) atomicAdd(&sh.psum[cur], (unsigned long long)acc);
+        cur = q;
+        acc = 0;
+      }
+      const uint64_t u = fold(res(i));
+      bad |= u >> 32 ? 1u : 0u;
+      sh.ures[i] = (uint32_t)u;
+      acc += u;
+    }
+    if (acc) atomicAdd(&sh.psum[cur], (unsigned long long)acc);
+    if (wave_or(bad) && lane == 0) sh.bad = 1;
+  }
+  __syncthreads();
+  if (sh.bad) return ~0ull;
+  // k of every partition of every order (kt[2^po - 1 + p])
+  for (uint32_t t = lane; t < (2u << pomax) - 1; t += kWave) {
+    const uint32_t po = 31u - (uint32_t)__builtin_clz(t + 1), p = t + 1 - (1u << po);
+    const uint32_t per = bs >> po, f = 1u << (pomax - po);
+    uint64_t sum = 0;
+    for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
+    const uint32_t cnt = per - (p == 0 ? order : 0u);
+    const uint64_t mean = cnt ? sum / cnt : 0;
+    sh.kt[t] = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t po = 0; po <= pomax; ++po) {
+    const uint32_t per = bs >> po;
+    const uint32_t* kt = sh.kt + (1u << po) - 1;
+    uint32_t cur = ~0u, k = 0, p = 0, pend = per;
+    uint64_t acc = 0;
+    for (uint32_t i = lane; i < bs; i += kWave) {
+      if (i < order) continue;
+      while (i >= pend) ++p, pend += per;
+      if (p != cur) {
+        if (acc) atomicAdd(&sh.pbits[po][cur], (unsigned long long)acc);
+        cur = p;
+        acc = 0;
+        k = kt[p];
+      }
+      acc += (sh.ures[i] >> k) + 1 + k;
+    }
+    if (acc) atomicAdd(&sh.pbits[po][cur], (unsigned long long)acc);
+  }
+  __syncthreads();
+  uint64_t rbest = ~0ull;
+  bpo = 0;
+  bmethod = 0;
+  for (uint32_t po = 0; po <= pomax; ++po) {
+    const uint32_t np = 1u << po;
+    uint64_t tot = 6;
+    uint32_t kmaxp = 0;
+    for (uint32_t p = 0; p < np; ++p) {
+      kmaxp = max(kmaxp, sh.kt[np - 1 + p]);
+      tot += sh.pbits[po][p];
+    }
+    const uint32_t method = kmaxp > 14 ? 1u : 0u;
+    tot += (uint64_t)np * (method ? 5 : 4);
+    if (tot < rbest) {
+      rbest = tot;
+      bpo = po;
+      bmethod = method;
+    }
+  }
+  return rbest;
+}
+
+// libFLAC's automatic quantized-coefficient precision (qlp_coeff_precision 0)
+__device__ __forceinline__ uint32_t lpc_precision(uint32_t bps, uint32_t bs) {
+  if (bps < 16) return max(5u, 2u + bps / 2);
+  if (bps == 16) return bs <= 192 ? 7u : bs <= 384 ? 8u : bs <= 576 ? 9u : bs <= 1152 ? 10u : bs <= 2304 ? 11u
+                                                                                        : bs <= 4608 ? 12u : 13u;
+  return bs <= 384 ? 13u : bs <= 1152 ? 14u : 15u;
+}
+
+// Levinson-Durbin recursion over the autocorrelation ac[0..order] (in
+// double, every lane alike; lane 0 writes): the residual energy of each order
+// to err[1..order] (if err), and the predictor of `order` (x[i] ~ sum lp[j]
+// x[i-1-j]) quantized to `prec`-bit coefficients with error feedback to q
+// (if q).  Returns the quantization shift (0..15), or -1 when the
+// coefficients are all zero or need a negative shift.  Out of line: its
+// double arrays would otherwise stay live across the planner's LDS loops.
+__device__ __noinline__ int lpc_coefs(const double* ac, uint32_t order, uint32_t prec, int32_t* q, double* err) {
+  const bool w = lane_id() == 0;
+  double a[kMaxLpc];
+  double e = ac[0];
+  for (uint32_t i = 0; i < order; ++i) {
+    double r = -ac[i + 1];
+    for (uint32_t j = 0; j < i; ++j) r -= a[j] * ac[i - j];
+    r = e != 0.0 ? r / e : 0.0;
+    a[i] = r;
+    for (uint32_t j = 0; j < i / 2; ++j) {
+      const double t = a[j];
+      a[j] += r * a[i - 1 - j];
+      a[i - 1 - j] += r * t;
+    }
+    if (i & 1) a[i / 2] += a[i / 2] * r;
+    e *= 1.0 - r * r;
+    if (err && w) err[i + 1] = e;
+  }
+  if (!q) return 0;
+  double cmax = 0.0;
+  for (uint32_t j = 0; j < order; ++j) cmax = fmax(cmax, fabs(a[j]));
+  if (!(cmax > 0.0)) return -1;
+  int e2;
+  (void)frexp(cmax, &e2);
+  int shift = (int)prec - 1 - (e2 - 1) - 1;
+  if (shift > 15) shift = 15;
+  if (shift < 0) return -1;
+  const int32_t qmax = (1 << (prec - 1)) - 1, qmin = -(1 << (prec - 1));
+  double carry = 0.0;
+  for (uint32_t j = 0; j < order; ++j) {
+    carry += -a[j] * (double)(1 << shift);  // (the predictor is the negated error filter)
+    int32_t v = (int32_t)lround(carry);
+    v = min(max(v, qmin), qmax);
+    carry -= v;
+    if (w) q[j] = v;
+  }
+  return shift;
+}
+
 // The cheapest subframe of source `src` (samples [0, bs), sbps bits each);
-// its Rice parameters go to sh.kpar[src]
-__device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint32_t sbps) {
+// its Rice parameters go to sh.kpar[src] (LPC coefficients: sh.lpcq[src])
+__device__ SubPlan plan_subframe(EncShared& sh, const FlacEncParams& prm, uint32_t src, uint32_t bs,
+                                 uint32_t sbps) {
   const uint32_t lane = lane_id();
   SubPlan P{};
   // wasted bits and the constant case
@@ -249,6 +420,10 @@ __device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint3
   }
   P.type = 1;
   P.bits = hdr + (uint64_t)P.bps * bs;
+  auto take_kpar = [&](uint32_t bpo) {
+    for (uint32_t p = lane; p < (1u << bpo); p += kWave) sh.kpar[src][p] = sh.kt[(1u << bpo) - 1 + p];
+    __syncthreads();
+  };
   // fixed predictor order: the smallest sum of |residual| (residuals must fit 32 bits)
   uint64_t sabs[5] = {0, 0, 0, 0, 0};
   uint32_t bad = 0;
@@ -281,92 +456,88 @@ __device__ SubPlan plan_subframe(EncShared& sh, uint32_t src, uint32_t bs, uint3
       order = o;
     }
   }
-  if (order == 0xFFFFFFFFu) return P;  // verbatim
-  // Rice partitions: orders 0..kMaxPo that divide bs with a first partition
-  // longer than the predictor order; per partition k = floor(log2(mean u))
-  for (uint32_t p = lane; p < (1u << kMaxPo); p += kWave) sh.psum[p] = 0;
-  for (uint32_t p = lane; p < (kMaxPo + 1) * (1u << kMaxPo); p += kWave) (&sh.pbits[0][0])[p] = 0;
+  if (order != 0xFFFFFFFFu) {
+    uint32_t bpo, bmethod;
+    const uint64_t rb = rice_plan(sh, bs, order, prm.max_po, [&](uint32_t i) { return fixed_res(sh, src, i, order, wasted); },
+                                  bpo, bmethod);
+    const uint64_t fbits = rb == ~0ull ? ~0ull : hdr + (uint64_t)order * P.bps + rb;
+    if (fbits < P.bits) {
+      take_kpar(bpo);
+      P.type = 2;
+      P.order = order;
+      P.po = bpo;
+      P.method = bmethod;
+      P.bits = fbits;
+    }
+  }
+  // LPC (RFC 9639 9.2.6): orders 1..max_lpc below the block size
+  const uint32_t maxo = min(prm.max_lpc, bs > 1 ? bs - 1 : 0u);
+  if (maxo == 0) return P;
+  // tukey(0.5)-windowed samples (libFLAC's default apodization) in the
+  // residual scratch, their autocorrelation in double
+  float* xw = reinterpret_cast<float*>(sh.ures);
+  const uint32_t np = bs / 4 > 1 ? bs / 4 - 1 : 0u;  // taper length - 1 (p / 2 * bs - 1)
+  for (uint32_t i = lane; i < bs; i += kWave) {
+    float w = 1.f;
+    if (np) {
+      if (i <= np) w = 0.5f - 0.5f * cosf(3.14159265358979f * (float)i / (float)np);
+      else if (i >= bs - np - 1) w = 0.5f - 0.5f * cosf(3.14159265358979f * (float)(bs - i - 1) / (float)np);
+    }
+    xw[i] = (float)(src_sample(sh, src, i) >> wasted) * w;
+  }
   __syncthreads();
-  uint32_t pomax = 0;
-  while (pomax < kMaxPo && bs % (2u << pomax) == 0 && (bs >> (pomax + 1)) > order) ++pomax;
-  const uint32_t psz = bs >> pomax;  // samples per finest partition
-  // (a lane's samples run through the partitions in order: its sums go to LDS
-  // once per partition, not once per sample)
-  {
-    uint32_t cur = ~0u, q = 0, qend = psz;
-    uint64_t acc = 0;
-    for (uint32_t i = lane; i < bs; i += kWave) {
-      if (i < order) continue;
-      while (i >= qend) ++q, qend += psz;
-      if (q != cur) {
-        if (acc) atomicAdd(&sh.psum[cur], (unsigned long long)acc);
-        cur = q;
-        acc = 0;
+  for (uint32_t lag = 0; lag <= maxo; ++lag) {
+    double a = 0.0;
+    for (uint32_t i = lane + lag; i < bs; i += kWave) a += (double)xw[i] * (double)xw[i - lag];
+    a = wave_sum(a);
+    if (lane == 0) sh.ac[lag] = a;
+  }
+  __syncthreads();
+  if (!(sh.ac[0] > 0.0)) return P;
+  const uint32_t prec = min(lpc_precision(P.bps, bs), 15u);
+  // orders to code: every one (exhaustive) or the one with the fewest
+  // expected bits (libFLAC's estimate: 0.5 log2(error / 2n) bits per residual
+  // plus the warm-up samples and coefficients)
+  uint32_t olo = 1, ohi = maxo;
+  if (!prm.exhaustive) {
+    (void)lpc_coefs(sh.ac, maxo, prec, nullptr, sh.lerr);
+    __syncthreads();
+    double bestb = 1e300;
+    uint32_t bo = 1;
+    for (uint32_t o = 1; o <= maxo; ++o) {
+      const double n = (double)(bs - o);
+      const double e = sh.lerr[o];
+      double bpr = e > 0.0 ? 0.5 * log2(0.5 * e / n) : 0.0;
+      if (bpr < 0.0) bpr = 0.0;
+      const double b = bpr * n + (double)o * (P.bps + prec);
+      if (b < bestb) {
+        bestb = b;
+        bo = o;
       }
-      const uint64_t u = fold(fixed_res(sh, src, i, order, wasted));
-      sh.ures[i] = (uint32_t)u;  // (residuals fit 32 bits: u < 2^32)
-      acc += u;
     }
-    if (acc) atomicAdd(&sh.psum[cur], (unsigned long long)acc);
+    olo = ohi = bo;
   }
-  __syncthreads();
-  // k of every partition of every order (kt[2^po - 1 + p])
-  for (uint32_t t = lane; t < (2u << pomax) - 1; t += kWave) {
-    const uint32_t po = 31u - (uint32_t)__builtin_clz(t + 1), p = t + 1 - (1u << po);
-    const uint32_t per = bs >> po, f = 1u << (pomax - po);
-    uint64_t sum = 0;
-    for (uint32_t q = p * f; q < (p + 1) * f; ++q) sum += sh.psum[q];
-    const uint32_t cnt = per - (p == 0 ? order : 0u);
-    const uint64_t mean = cnt ? sum / cnt : 0;
-    sh.kt[t] = mean ? min(63u - (uint32_t)__builtin_clzll(mean), 30u) : 0u;
-  }
-  __syncthreads();
-  for (uint32_t po = 0; po <= pomax; ++po) {
-    const uint32_t per = bs >> po;
-    const uint32_t* kt = sh.kt + (1u << po) - 1;
-    uint32_t cur = ~0u, k = 0, p = 0, pend = per;
-    uint64_t acc = 0;
-    for (uint32_t i = lane; i < bs; i += kWave) {
-      if (i < order) continue;
-      while (i >= pend) ++p, pend += per;
-      if (p != cur) {
-        if (acc) atomicAdd(&sh.pbits[po][cur], (unsigned long long)acc);
-        cur = p;
-        acc = 0;
-        k = kt[p];
-      }
-      acc += (sh.ures[i] >> k) + 1 + k;
+  for (uint32_t o = olo; o <= ohi; ++o) {
+    const int shift = __builtin_amdgcn_readfirstlane(lpc_coefs(sh.ac, o, prec, sh.lpct, nullptr));
+    __syncthreads();
+    if (shift < 0) continue;
+    uint32_t bpo, bmethod;
+    const uint64_t rb = rice_plan(sh, bs, o, prm.max_po,
+                                  [&](uint32_t i) { return lpc_res(sh, sh.lpct, src, i, o, (uint32_t)shift, wasted); },
+                                  bpo, bmethod);
+    const uint64_t lbits = rb == ~0ull ? ~0ull : hdr + (uint64_t)o * P.bps + 4 + 5 + (uint64_t)o * prec + rb;
+    if (lbits < P.bits) {
+      take_kpar(bpo);
+      if (lane < o) sh.lpcq[src][lane] = sh.lpct[lane];
+      __syncthreads();
+      P.type = 3;
+      P.order = o;
+      P.po = bpo;
+      P.method = bmethod;
+      P.prec = prec;
+      P.shift = (uint32_t)shift;
+      P.bits = lbits;
     }
-    if (acc) atomicAdd(&sh.pbits[po][cur], (unsigned long long)acc);
-  }
-  __syncthreads();
-  uint64_t rbest = ~0ull;
-  uint32_t bpo = 0, bmethod = 0;
-  for (uint32_t po = 0; po <= pomax; ++po) {
-    const uint32_t np = 1u << po;
-    uint64_t tot = 6;
-    uint32_t kmaxp = 0;
-    for (uint32_t p = 0; p < np; ++p) {
-      kmaxp = max(kmaxp, sh.kt[np - 1 + p]);
-      tot += sh.pbits[po][p];
-    }
-    const uint32_t method = kmaxp > 14 ? 1u : 0u;
-    tot += (uint64_t)np * (method ? 5 : 4);
-    if (tot < rbest) {
-      rbest = tot;
-      bpo = po;
-      bmethod = method;
-    }
-  }
-  for (uint32_t p = lane; p < (1u << bpo); p += kWave) sh.kpar[src][p] = sh.kt[(1u << bpo) - 1 + p];
-  __syncthreads();
-  const uint64_t fbits = hdr + (uint64_t)order * P.bps + rbest;
-  if (fbits < P.bits) {
-    P.type = 2;
-    P.order = order;
-    P.po = bpo;
-    P.method = bmethod;
-    P.bits = fbits;
   }
   return P;
 }
@@ -393,10 +564,11 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
   uint32_t head = 8 + P.wasted;
   if (P.type == 0) head += P.bps;
   if (P.type == 2) head += P.order * P.bps + 6;
-  const uint32_t per = P.type == 2 ? bs >> P.po : bs;
+  if (P.type == 3) head += P.order * P.bps + 4 + 5 + P.order * P.prec + 6;
+  const uint32_t per = P.type >= 2 ? bs >> P.po : bs;
   const uint32_t pbits = P.method ? 5u : 4u;
   if (lane == 0) {
-    const uint32_t type6 = P.type == 0 ? 0u : P.type == 1 ? 1u : 8u + P.order;
+    const uint32_t type6 = P.type == 0 ? 0u : P.type == 1 ? 1u : P.type == 2 ? 8u + P.order : 31u + P.order;
     put(pos, (type6 << 1) | (P.wasted ? 1u : 0u), 8);
     uint32_t q = pos + 8;
     if (P.wasted) {
@@ -405,9 +577,15 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
     }
     if (P.type == 0) {
       put(q, (uint64_t)(src_sample(sh, src, 0) >> P.wasted), P.bps);
-    } else if (P.type == 2) {
+    } else if (P.type >= 2) {
       for (uint32_t i = 0; i < P.order; ++i, q += P.bps)
         put(q, (uint64_t)(src_sample(sh, src, i) >> P.wasted), P.bps);
+      if (P.type == 3) {  // precision - 1, shift, coefficients (two's complement)
+        put(q, P.prec - 1, 4);
+        put(q + 4, P.shift, 5);
+        q += 9;
+        for (uint32_t j = 0; j < P.order; ++j, q += P.prec) put(q, (uint64_t)(uint32_t)sh.lpcq[src][j], P.prec);
+      }
       put(q, (P.method << 4) | P.po, 6);
     }
   }
@@ -420,7 +598,7 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
       if (i < bs) put(at + lane * P.bps, (uint64_t)(src_sample(sh, src, i) >> P.wasted), P.bps);
       at += min(kWave, bs - j0) * P.bps;
     }
-  } else if (P.type == 2) {
+  } else if (P.type >= 2) {
     uint32_t p = 0, pend = per;
     for (uint32_t j0 = 0; j0 < bs; j0 += kWave) {
       const uint32_t i = j0 + lane;
@@ -430,7 +608,8 @@ __device__ uint32_t emit_subframe(EncShared& sh, const SubPlan& P, uint32_t src,
         while (i >= pend) ++p, pend += per;
         k = sh.kpar[src][p];
         hb = i == (p == 0 ? P.order : p * per) ? pbits : 0u;
-        u = fold(fixed_res(sh, src, i, P.order, P.wasted));
+        u = fold(P.type == 2 ? fixed_res(sh, src, i, P.order, P.wasted)
+                             : lpc_res(sh, sh.lpcq[src], src, i, P.order, P.shift, P.wasted));
         len = hb + (uint32_t)(u >> k) + 1 + k;
       }
       uint32_t tot;
@@ -489,7 +668,7 @@ __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
     __syncthreads();
     // the four sources' plans, Rice parameters kept per source (kpar[src])
 #pragma unroll
-    for (uint32_t s = 0; s < 4; ++s) plans[s] = plan_subframe(sh, s, bs, s == 2 ? p.bps + 1 : p.bps);
+    for (uint32_t s = 0; s < 4; ++s) plans[s] = plan_subframe(sh, p, s, bs, s == 2 ? p.bps + 1 : p.bps);
     const uint64_t ind = plans[0].bits + plans[1].bits, ls = plans[0].bits + plans[2].bits,
                    rs = plans[2].bits + plans[1].bits, ms = plans[3].bits + plans[2].bits;
     uint64_t best = ind;
@@ -521,7 +700,7 @@ __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
     for (uint32_t c = 0; c < C; ++c) {
       stage(0, c);
       __syncthreads();
-      const SubPlan P = plan_subframe(sh, 0, bs, p.bps);
+      const SubPlan P = plan_subframe(sh, p, 0, bs, p.bps);
       pos = emit_subframe(sh, P, 0, bs, pos, 32 * win_w0);
       flush(sh, slot, win_w0, pos, false);
     }
@@ -1463,7 +1642,15 @@ uint64_t rpp_flac_encode_workspace_bytes(uint64_t nsamples, uint32_t channels, u
 
 int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint8_t* d_out,
                     uint64_t* d_total, void* d_workspace, uint64_t workspace_bytes, void* stream) {
+  return rpp_flac_encode_ex(d_samples, nsamples, channels, bps, 5, 0, d_out, d_total, d_workspace, workspace_bytes,
+                            stream);
+}
+
+int rpp_flac_encode_ex(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint32_t level,
+                       uint32_t exhaustive, uint8_t* d_out, uint64_t* d_total, void* d_workspace,
+                       uint64_t workspace_bytes, void* stream) {
   if (channels < 1 || channels > 8 || bps < 4 || bps > 32) return RPP_UNSUPPORTED_CONFIG;
+  if (level > 8) return RPP_INVALID_ARGUMENT;
   if (!d_total) return RPP_INVALID_ARGUMENT;
   hipStream_t s = (hipStream_t)stream;
   if (nsamples == 0) return hipMemsetAsync(d_total, 0, 8, s) == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
@@ -1477,7 +1664,12 @@ int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channe
   uint64_t* sizes = reinterpret_cast<uint64_t*>(ws + frames * slot);
   uint64_t* offs = sizes + frames + 1;
   uint64_t* lens = offs + frames + 1;
-  FlacEncParams p{d_samples, nsamples, channels, bps, slots, slot, sizes, (uint32_t)frames};
+  // libFLAC's level presets (-l max LPC order, -r max partition order; the
+  // block size stays 4096 and all four stereo assignments are tried)
+  const uint32_t max_lpc = level <= 2 ? 0u : level == 3 ? 6u : level <= 6 ? 8u : kMaxLpc;
+  const uint32_t max_po = min(level <= 2 ? 3u : level <= 4 ? 4u : 6u, kMaxPo);
+  FlacEncParams p{d_samples, nsamples, channels, bps, slots, slot, sizes, (uint32_t)frames,
+                  max_lpc, exhaustive ? 1u : 0u, max_po};
   const size_t lds = sizeof(EncShared);
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rpp_flac_encode_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -1359,8 +1359,9 @@ std::vector<uint8_t> flac_block_compressor::compress(std::span<uint8_t const> da
   hip_check(hipMemcpyAsync(d, data.data(), data.size(), hipMemcpyHostToDevice, st), "H2D flac pcm");
   int rc = rpp_pcm_unpack(&pf, d, reinterpret_cast<int32_t*>(d + off_x), nvals, st);
   if (rc != RPP_OK) throw std::runtime_error(std::string("[FLAC] failed to process interleaved samples: ") + status_name(rc));
-  rc = rpp_flac_encode(reinterpret_cast<int32_t const*>(d + off_x), n, f.num_channels, f.bits_per_sample, d + off_out,
-                       reinterpret_cast<uint64_t*>(d + off_tot), d + off_ws, ws_bytes, st);
+  rc = rpp_flac_encode_ex(reinterpret_cast<int32_t const*>(d + off_x), n, f.num_channels, f.bits_per_sample, level_,
+                          exhaustive_ ? 1u : 0u, d + off_out, reinterpret_cast<uint64_t*>(d + off_tot), d + off_ws,
+                          ws_bytes, st);
   if (rc != RPP_OK) throw std::runtime_error(std::string("[FLAC] failed to process interleaved samples: ") + status_name(rc));
   uint64_t total = 0;
   hip_check(hipMemcpyAsync(&total, d + off_tot, 8, hipMemcpyDeviceToHost, st), "D2H flac size");

@@ -14,10 +14,13 @@ flac.cpp:322-334) and 4096-sample FLAC frames (rpp_flac_encode); decoding runs
 the other way (rpp_flac_decode, rpp_pcm_pack).
 
 Parity unpinned: the reference uses libFLAC (absent here), whose model search
-(LPC orders, precision) decides its bytes; this encoder writes valid FLAC
-with fixed predictors, so its streams differ from libFLAC's.  The decoder
-reads every frame kind RFC 9639 defines.  ``level`` and ``exhaustive`` are
-accepted and described as the reference does, and do not change the output.
+(LPC orders, precision, apodization) decides its bytes; this encoder writes
+valid FLAC with fixed and LPC predictors chosen by its own search, so its
+streams differ from libFLAC's.  The decoder reads every frame kind RFC 9639
+defines.  ``level`` selects libFLAC's preset limits (levels 0-2 fixed
+predictors only, 3 LPC up to order 6, 4-6 up to 8, 7-8 up to 12) and
+``exhaustive`` codes every LPC order instead of the estimated best
+(rpp_flac_encode_ex; flac.cpp:312-313).
 """
 
 from __future__ import annotations
@@ -146,9 +149,9 @@ class FlacBlockCompressor:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         total = torch.zeros(1, dtype=torch.int64, device=dev)
         s = torch.cuda.current_stream(dev)
-        _status(L.rpp_flac_encode(C.c_void_p(x.data_ptr()), n, channels, bits, C.c_void_p(out.data_ptr()),
-                                  C.c_void_p(total.data_ptr()), C.c_void_p(ws.data_ptr()), ws_bytes,
-                                  C.c_void_p(s.cuda_stream)), "encode")
+        _status(L.rpp_flac_encode_ex(C.c_void_p(x.data_ptr()), n, channels, bits, self.level, int(self.exhaustive),
+                                     C.c_void_p(out.data_ptr()), C.c_void_p(total.data_ptr()),
+                                     C.c_void_p(ws.data_ptr()), ws_bytes, C.c_void_p(s.cuda_stream)), "encode")
         size = int(total.item())
         return head + stream_head + out[:size].cpu().numpy().tobytes()
 

@@ -345,8 +345,8 @@ long rpp_flac_parse_stream(const uint8_t* in, size_t len, rpp_flac_stream_info* 
  *
  * rpp_flac_encode: nsamples interleaved frames of `channels` int32 samples
  * of `bps` significant bits (8..32; channels 1..8, flac.cpp:243-245) ->
- * FLAC frames of 4096 samples (fixed predictors, stereo decorrelation,
- * partitioned Rice codes, CRC-8 / CRC-16) back to back at d_out
+ * FLAC frames of 4096 samples (fixed and LPC predictors, stereo
+ * decorrelation, partitioned Rice codes, CRC-8 / CRC-16) back to back at d_out
  * (rpp_flac_frame_bound bytes per frame at most); *d_total = their size.
  * Workspace: rpp_flac_encode_workspace_bytes.
  *
@@ -362,6 +362,15 @@ uint64_t rpp_flac_frame_bound(uint32_t channels, uint32_t bps);
 uint64_t rpp_flac_encode_workspace_bytes(uint64_t nsamples, uint32_t channels, uint32_t bps);
 int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint8_t* d_out,
                     uint64_t* d_total, void* d_workspace, uint64_t workspace_bytes, void* stream);
+/* rpp_flac_encode at a libFLAC compression level (0..8: levels 0-2 fixed
+ * predictors only, 3 LPC up to order 6, 4-6 up to 8, 7-8 up to 12; Rice
+ * partition orders up to 3 / 4 / 5) and with `exhaustive` (every LPC order
+ * coded, the cheapest kept; else libFLAC's expected-bits estimate picks the
+ * order) -- FLAC__stream_encoder_set_compression_level / _set_do_exhaustive_
+ * model_search as flac.cpp:312-313 calls them.  rpp_flac_encode is level 5. */
+int rpp_flac_encode_ex(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint32_t level,
+                       uint32_t exhaustive, uint8_t* d_out, uint64_t* d_total, void* d_workspace,
+                       uint64_t workspace_bytes, void* stream);
 uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t bps, uint32_t max_blocksize,
                                          uint32_t max_candidates);
 int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,

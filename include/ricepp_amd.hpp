@@ -156,12 +156,12 @@ class block_decompressor {
 // bytes unpacked, encoded, decoded and packed on the GPU (rpp_pcm_unpack,
 // rpp_flac_encode, rpp_flac_decode, rpp_pcm_pack) through a pooled device
 // context.  Parity unpinned: the reference codes the stream with libFLAC
-// (absent here); this encoder writes valid FLAC (RFC 9639) with fixed
+// (absent here); this encoder writes valid FLAC (RFC 9639) with fixed and LPC
 // predictors, 4096-sample frames and stereo decorrelation, so its bytes differ
-// from libFLAC's.  `level` and `exhaustive` are accepted, validated (level
-// 0..8) and reported by describe() as the reference does; they do not change
-// the output (no LPC search).  The decoder reads every RFC 9639 frame kind,
-// LPC included.
+// from libFLAC's.  `level` (0..8) and `exhaustive` are validated, reported by
+// describe() as the reference does, and select libFLAC's preset limits (LPC
+// order 0 / 6 / 8 / 12) and the exhaustive model search (rpp_flac_encode_ex).
+// The decoder reads every RFC 9639 frame kind.
 
 // compression_type::FLAC (include/dwarfs/compression.h, FLAC = 6)
 inline constexpr int compression_type_flac = 6;

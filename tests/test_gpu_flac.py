@@ -118,6 +118,45 @@ def test_gpu_encoder_kinds():
                              f"want {x[bad[:8]].tolist()}\n{trace[:3000]}")
 
 
+def ar_audio(channels, n, bits, seed=9):
+    """Band-limited 'audio' a linear predictor models well and fixed predictors do not: white noise through a
+    sixth-order all-pole resonator (poles at radius 0.97), per channel, scaled to `bits`."""
+    from scipy.signal import lfilter
+    rng = np.random.default_rng(seed)
+    poles = [0.97 * np.exp(1j * w) for w in (0.07, 0.31, 0.9)]
+    a = np.real(np.poly(poles + [np.conj(p) for p in poles]))
+    out = np.empty((n, channels), np.int64)
+    lim = (1 << (bits - 1)) - 1
+    for c in range(channels):
+        y = lfilter([1.0], a, rng.standard_normal(n))
+        out[:, c] = np.clip(np.round(y / np.abs(y).max() * 0.8 * lim), -lim, lim)
+    return out.reshape(-1).astype(np.int32)
+
+
+@pytest.mark.parametrize("channels,bits", [(1, 16), (2, 16), (2, 24), (3, 12)])
+def test_gpu_lpc_levels(channels, bits):
+    """LPC subframes (rpp_flac_encode_ex): every level and the exhaustive search round-trip through the GPU decoder
+    and the restatement's decoder; on all-pole audio LPC (level 5) codes smaller than level 2's fixed predictors,
+    and the exhaustive search (every order coded) is never larger than the estimated order."""
+    n = 5 * 4096 + 123
+    x = ar_audio(channels, n, bits)
+    nbytes = (bits + 7) // 8
+    data = pcm_bytes(x, E.Little, S.Signed, Pd.Msb, nbytes, bits)
+    m = meta(E.Little, S.Signed, Pd.Msb, channels, nbytes, bits)
+    sizes = {}
+    for level, exh in [(0, False), (2, False), (3, False), (5, False), (5, True), (8, False), (8, True)]:
+        comp = FL.FlacBlockCompressor(level, exh).compress(data, m)
+        d = FL.FlacBlockDecompressor(comp)
+        assert d.decompress() == data, (level, exh)
+        st, y, ch, b = F.decode(d.stream, x.size)
+        assert st == F.OK and (ch, b) == (channels, bits), (level, exh)
+        assert np.array_equal(y, x), (level, exh)
+        sizes[(level, exh)] = len(comp)
+    assert sizes[(5, False)] < 0.97 * sizes[(2, False)], sizes
+    assert sizes[(5, True)] <= sizes[(5, False)], sizes
+    assert sizes[(8, True)] <= sizes[(8, False)], sizes
+
+
 def test_empty_block():
     comp = FL.FlacBlockCompressor().compress(b"", meta(E.Big, S.Signed, Pd.Msb, 2, 2, 16))
     assert FL.decompress(comp) == b""
