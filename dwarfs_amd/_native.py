@@ -68,6 +68,8 @@ EXPORTED_SYMBOLS = (
     "rpp_flac_encode_workspace_bytes",
     "rpp_flac_encode",
     "rpp_flac_encode_ex",
+    "rpp_flac_encode_batch_workspace_bytes",
+    "rpp_flac_encode_batch",
     "rpp_flac_decode_workspace_bytes",
     "rpp_flac_decode",
 )
@@ -213,6 +215,10 @@ def lib() -> C.CDLL:
         L.rpp_flac_encode_ex.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P,
                                          C.c_uint64, P]
         L.rpp_flac_encode_ex.restype = C.c_int
+        L.rpp_flac_encode_batch_workspace_bytes.argtypes = [C.c_uint32, P, P, P]
+        L.rpp_flac_encode_batch_workspace_bytes.restype = C.c_uint64
+        L.rpp_flac_encode_batch.argtypes = [P, C.c_uint32, P, P, P, P, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, P]
+        L.rpp_flac_encode_batch.restype = C.c_int
         L.rpp_flac_decode_workspace_bytes.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.rpp_flac_decode_workspace_bytes.restype = C.c_uint64
         L.rpp_flac_decode.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, P, P,

@@ -46,6 +46,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "ricepp_amd.h"
 
 namespace {
@@ -182,6 +185,14 @@ struct FlacEncParams {
   uint32_t max_lpc;     // LPC orders 1..max_lpc (0: fixed predictors only)
   uint32_t exhaustive;  // code every LPC order (else the expected-bits estimate picks one)
   uint32_t max_po;      // Rice partition orders 0..max_po (<= kMaxPo)
+  // batch launches (rpp_flac_encode_batch): slot g codes frame fdesc[g] =
+  // (block, frame number) of block b's samples x + in_off[b] (nsamples[b],
+  // chan[b], bpsb[b]); null: one block of the fields above
+  const uint2* fdesc;
+  const uint64_t* in_off;
+  const uint64_t* bnsamples;
+  const uint32_t* chan;
+  const uint32_t* bpsb;
 };
 
 constexpr uint32_t kMaxLpc = 12;  // libFLAC's presets: -l 6 (level 3), 8 (4-6), 12 (7-8)
@@ -648,18 +659,29 @@ __device__ void flush(EncShared& sh, uint8_t* slot, uint32_t& win_w0, uint32_t p
 __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   EncShared& sh = *reinterpret_cast<EncShared*>(smem);
-  const uint32_t fn = blockIdx.x, lane = lane_id();
-  if (fn >= p.frames) return;
+  const uint32_t g = blockIdx.x, lane = lane_id();
+  if (g >= p.frames) return;
+  // this slot's block and frame number
+  uint32_t fn = g, C = p.channels, BPS = p.bps;
+  uint64_t NS = p.nsamples;
+  const int32_t* X = p.x;
+  if (p.fdesc) {
+    const uint2 d = p.fdesc[g];
+    fn = d.y;
+    C = p.chan[d.x];
+    BPS = p.bpsb[d.x];
+    NS = p.bnsamples[d.x];
+    X = p.x + p.in_off[d.x];
+  }
   const uint64_t f0 = (uint64_t)fn * kFlacBlock;
-  const uint32_t bs = (uint32_t)min((uint64_t)kFlacBlock, p.nsamples - f0);
-  const uint32_t C = p.channels;
-  uint8_t* slot = p.slots + (uint64_t)fn * p.slot_bytes;
+  const uint32_t bs = (uint32_t)min((uint64_t)kFlacBlock, NS - f0);
+  uint8_t* slot = p.slots + (uint64_t)g * p.slot_bytes;
   for (uint32_t w = lane; w < kWinWords; w += kWave) sh.win[w] = 0;
   uint32_t win_w0 = 0;
   auto stage = [&](uint32_t slotc, uint32_t c) {
-    for (uint32_t i = lane; i < bs; i += kWave) sh.smp[slotc][i] = p.x[(f0 + i) * C + c];
+    for (uint32_t i = lane; i < bs; i += kWave) sh.smp[slotc][i] = X[(f0 + i) * C + c];
   };
-  const bool stereo = C == 2 && p.bps < 32;
+  const bool stereo = C == 2 && BPS < 32;
   SubPlan plans[4];
   uint32_t assign = C - 1;
   if (stereo) {
@@ -668,7 +690,7 @@ __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
     __syncthreads();
     // the four sources' plans, Rice parameters kept per source (kpar[src])
 #pragma unroll
-    for (uint32_t s = 0; s < 4; ++s) plans[s] = plan_subframe(sh, p, s, bs, s == 2 ? p.bps + 1 : p.bps);
+    for (uint32_t s = 0; s < 4; ++s) plans[s] = plan_subframe(sh, p, s, bs, s == 2 ? BPS + 1 : BPS);
     const uint64_t ind = plans[0].bits + plans[1].bits, ls = plans[0].bits + plans[2].bits,
                    rs = plans[2].bits + plans[1].bits, ms = plans[3].bits + plans[2].bits;
     uint64_t best = ind;
@@ -679,7 +701,7 @@ __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
   }
   // header (byte-aligned at the slot start) and its CRC-8
   uint8_t hdr[20];
-  const uint32_t hlen = build_header(hdr, fn, bs, assign, p.bps);
+  const uint32_t hlen = build_header(hdr, fn, bs, assign, BPS);
   uint8_t c8 = 0;
   for (uint32_t i = 0; i < hlen; ++i) c8 = crc8_byte(c8, hdr[i]);
   hdr[hlen] = c8;
@@ -700,14 +722,14 @@ __global__ __launch_bounds__(64) void rpp_flac_encode_kernel(FlacEncParams p) {
     for (uint32_t c = 0; c < C; ++c) {
       stage(0, c);
       __syncthreads();
-      const SubPlan P = plan_subframe(sh, p, 0, bs, p.bps);
+      const SubPlan P = plan_subframe(sh, p, 0, bs, BPS);
       pos = emit_subframe(sh, P, 0, bs, pos, 32 * win_w0);
       flush(sh, slot, win_w0, pos, false);
     }
   }
   pos = (pos + 7) & ~7u;  // zero padding to a byte
   flush(sh, slot, win_w0, pos, true);
-  if (lane == 0) p.sizes[fn] = pos / 8 + 2;  // + CRC-16 (rpp_flac_crc_kernel)
+  if (lane == 0) p.sizes[g] = pos / 8 + 2;  // + CRC-16 (rpp_flac_crc_kernel)
 }
 
 // ---- pack: frames back to back ----
@@ -728,6 +750,15 @@ __global__ void rpp_flac_lens_kernel(const uint64_t* sizes, const uint64_t* offs
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < frames) lens[i] = sizes[i] - 2;
   if (i == frames - 1) *total = offs[i] + sizes[i];
+}
+
+// block b's frames start at the exclusive scan's entry of its first frame
+// (blocks without frames after the last frame, and entry nblocks: the total)
+__global__ void rpp_flac_block_off_kernel(const uint64_t* sizes, const uint64_t* offs, uint64_t frames,
+                                          const uint32_t* fstart, uint32_t nblocks, uint64_t* out_off) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = frames ? offs[frames - 1] + sizes[frames - 1] : 0;
+  if (b <= nblocks) out_off[b] = fstart[b] < frames ? offs[fstart[b]] : total;
 }
 
 // ---- CRC-16 of frames: per-lane chunks combined by GF(2) shifts ----
@@ -1624,6 +1655,30 @@ __global__ __launch_bounds__(256) void rpp_flac_place_kernel(FlacDecParams d) {
   }
 }
 
+// libFLAC's level presets (-l max LPC order, -r max partition order; the
+// block size stays 4096 and all four stereo assignments are tried)
+uint32_t level_max_lpc(uint32_t level) { return level <= 2 ? 0u : level == 3 ? 6u : level <= 6 ? 8u : kMaxLpc; }
+uint32_t level_max_po(uint32_t level) { return min(level <= 2 ? 3u : level <= 4 ? 4u : 6u, kMaxPo); }
+
+// the batch's frame table and per-block arrays, laid out in its workspace
+struct BatchLayout {
+  uint64_t frames = 0, slot = 0, slots_bytes = 0, head_bytes = 0;
+};
+BatchLayout batch_layout(uint32_t nblocks, const uint64_t* nsamples, const uint32_t* channels, const uint32_t* bps) {
+  BatchLayout L;
+  uint64_t bound = 0;
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    L.frames += (nsamples[b] + kFlacBlock - 1) / kFlacBlock;
+    bound = std::max<uint64_t>(bound, rpp_flac_frame_bound(channels[b], bps[b]));
+  }
+  L.slot = (bound + 15) & ~15ull;
+  L.slots_bytes = L.frames * L.slot;
+  // frame table (8 B per frame) + in_off, nsamples (8 B per block), channels,
+  // bps, first frames (4 B per block, + 1)
+  L.head_bytes = ((8 * L.frames + 16 * nblocks + 12 * (uint64_t)nblocks + 4 + 15) & ~15ull);
+  return L;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1664,12 +1719,9 @@ int rpp_flac_encode_ex(const int32_t* d_samples, uint64_t nsamples, uint32_t cha
   uint64_t* sizes = reinterpret_cast<uint64_t*>(ws + frames * slot);
   uint64_t* offs = sizes + frames + 1;
   uint64_t* lens = offs + frames + 1;
-  // libFLAC's level presets (-l max LPC order, -r max partition order; the
-  // block size stays 4096 and all four stereo assignments are tried)
-  const uint32_t max_lpc = level <= 2 ? 0u : level == 3 ? 6u : level <= 6 ? 8u : kMaxLpc;
-  const uint32_t max_po = min(level <= 2 ? 3u : level <= 4 ? 4u : 6u, kMaxPo);
   FlacEncParams p{d_samples, nsamples, channels, bps, slots, slot, sizes, (uint32_t)frames,
-                  max_lpc, exhaustive ? 1u : 0u, max_po};
+                  level_max_lpc(level), exhaustive ? 1u : 0u, level_max_po(level),
+                  nullptr, nullptr, nullptr, nullptr, nullptr};
   const size_t lds = sizeof(EncShared);
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rpp_flac_encode_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1683,6 +1735,84 @@ int rpp_flac_encode_ex(const int32_t* d_samples, uint64_t nsamples, uint32_t cha
                      d_total);
   hipLaunchKernelGGL(rpp_flac_crc_kernel, dim3((uint32_t)(frames < 4096 ? frames : 4096)), dim3(64), 0, s, d_out, offs,
                      lens, (uint32_t)frames, d_out, nullptr, nullptr);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
+uint64_t rpp_flac_encode_batch_workspace_bytes(uint32_t nblocks, const uint64_t* h_nsamples, const uint32_t* h_channels,
+                                               const uint32_t* h_bps) {
+  if (!nblocks || !h_nsamples || !h_channels || !h_bps) return 256;
+  const BatchLayout L = batch_layout(nblocks, h_nsamples, h_channels, h_bps);
+  return L.slots_bytes + 3 * 8 * (L.frames + 1) + L.head_bytes + 256;
+}
+
+int rpp_flac_encode_batch(const int32_t* d_samples, uint32_t nblocks, const uint64_t* h_in_off,
+                          const uint64_t* h_nsamples, const uint32_t* h_channels, const uint32_t* h_bps,
+                          uint32_t level, uint32_t exhaustive, uint8_t* d_out, uint64_t* d_out_off, void* d_workspace,
+                          uint64_t workspace_bytes, void* stream) {
+  if (level > 8) return RPP_INVALID_ARGUMENT;
+  if (nblocks == 0) return RPP_OK;
+  if (!h_in_off || !h_nsamples || !h_channels || !h_bps || !d_out_off || !d_workspace) return RPP_INVALID_ARGUMENT;
+  for (uint32_t b = 0; b < nblocks; ++b)
+    if (h_channels[b] < 1 || h_channels[b] > 8 || h_bps[b] < 4 || h_bps[b] > 32) return RPP_UNSUPPORTED_CONFIG;
+  if (workspace_bytes < rpp_flac_encode_batch_workspace_bytes(nblocks, h_nsamples, h_channels, h_bps))
+    return RPP_INVALID_ARGUMENT;
+  const BatchLayout L = batch_layout(nblocks, h_nsamples, h_channels, h_bps);
+  if (L.frames > 0x7FFFFFFFu) return RPP_INVALID_ARGUMENT;
+  if (L.frames && (!d_samples || !d_out)) return RPP_INVALID_ARGUMENT;
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t* ws = static_cast<uint8_t*>(d_workspace);
+  uint8_t* slots = ws;
+  uint64_t* sizes = reinterpret_cast<uint64_t*>(ws + L.slots_bytes);
+  uint64_t* offs = sizes + L.frames + 1;
+  uint64_t* lens = offs + L.frames + 1;
+  uint8_t* head = reinterpret_cast<uint8_t*>(lens + L.frames + 1);
+  // the frame table and per-block arrays, staged on the host and copied once
+  std::vector<uint8_t> h(L.head_bytes, 0);
+  auto* fdesc = reinterpret_cast<uint2*>(h.data());
+  auto* in_off = reinterpret_cast<uint64_t*>(h.data() + 8 * L.frames);
+  auto* ns = in_off + nblocks;
+  auto* ch = reinterpret_cast<uint32_t*>(ns + nblocks);
+  auto* bp = ch + nblocks;
+  auto* fstart = bp + nblocks;  // [nblocks + 1]
+  uint64_t g = 0;
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    in_off[b] = h_in_off[b];
+    ns[b] = h_nsamples[b];
+    ch[b] = h_channels[b];
+    bp[b] = h_bps[b];
+    fstart[b] = (uint32_t)g;
+    const uint64_t nf = (h_nsamples[b] + kFlacBlock - 1) / kFlacBlock;
+    for (uint64_t f = 0; f < nf; ++f, ++g) fdesc[g] = make_uint2(b, (uint32_t)f);
+  }
+  fstart[nblocks] = (uint32_t)g;
+  if (hipMemcpyAsync(head, h.data(), h.size(), hipMemcpyHostToDevice, s) != hipSuccess) return RPP_HIP_ERROR;
+  const uint8_t* dh = head;
+  FlacEncParams p{d_samples, 0, 1, 16, slots, L.slot, sizes, (uint32_t)L.frames,
+                  level_max_lpc(level), exhaustive ? 1u : 0u, level_max_po(level),
+                  reinterpret_cast<const uint2*>(dh), reinterpret_cast<const uint64_t*>(dh + 8 * L.frames),
+                  reinterpret_cast<const uint64_t*>(dh + 8 * L.frames) + nblocks,
+                  reinterpret_cast<const uint32_t*>(dh + 8 * L.frames + 16 * (uint64_t)nblocks),
+                  reinterpret_cast<const uint32_t*>(dh + 8 * L.frames + 16 * (uint64_t)nblocks) + nblocks};
+  const uint32_t* d_fstart = reinterpret_cast<const uint32_t*>(dh + 8 * L.frames + 16 * (uint64_t)nblocks) + 2 * nblocks;
+  if (L.frames) {
+    const size_t lds = sizeof(EncShared);
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rpp_flac_encode_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return RPP_HIP_ERROR;
+    hipLaunchKernelGGL(rpp_flac_encode_kernel, dim3((uint32_t)L.frames), dim3(64), lds, s, p);
+  }
+  int st = rpp_exclusive_scan_u64(sizes, L.frames, offs, s);
+  if (st != RPP_OK) return st;
+  if (L.frames) {
+    hipLaunchKernelGGL(rpp_flac_pack_kernel, dim3((uint32_t)L.frames), dim3(256), 0, s, slots, L.slot, sizes, offs,
+                       d_out, (uint32_t)L.frames);
+    hipLaunchKernelGGL(rpp_flac_lens_kernel, dim3((uint32_t)((L.frames + 255) / 256)), dim3(256), 0, s, sizes, offs,
+                       lens, L.frames, d_out_off + nblocks);  // (the total; rpp_flac_block_off_kernel writes it too)
+    hipLaunchKernelGGL(rpp_flac_crc_kernel, dim3((uint32_t)(L.frames < 4096 ? L.frames : 4096)), dim3(64), 0, s, d_out,
+                       offs, lens, (uint32_t)L.frames, d_out, nullptr, nullptr);
+  }
+  hipLaunchKernelGGL(rpp_flac_block_off_kernel, dim3((nblocks + 256) / 256), dim3(256), 0, s, sizes, offs, L.frames,
+                     d_fstart, nblocks, d_out_off);
   return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
 }
 

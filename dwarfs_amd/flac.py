@@ -116,7 +116,9 @@ class FlacBlockCompressor:
     def estimate_memory_usage(self, data_size: int) -> int:  # :395-398
         return int(data_size)
 
-    def compress(self, data: bytes, metadata: Optional[str]) -> bytes:
+    @staticmethod
+    def _prepare(data: bytes, metadata: Optional[str]):
+        """The block's framing (varint + flac_block_header + fLaC/STREAMINFO) and PCM shape (flac.cpp:284-304)."""
         if metadata is None:
             raise RuntimeError("internal error: flac compression requires metadata")
         m = json.loads(metadata)
@@ -135,9 +137,12 @@ class FlacBlockCompressor:
         n = len(data) // (channels * nbytes)  # samples per channel
         sh = (C.c_uint8 * 64)()
         sl = N.lib().rpp_flac_stream_header(channels, bits, n, sh)
-        stream_head = bytes(sh[:sl])
+        return head + bytes(sh[:sl]), n, channels, bits, flags
+
+    def compress(self, data: bytes, metadata: Optional[str]) -> bytes:
+        prefix, n, channels, bits, flags = self._prepare(data, metadata)
         if n == 0:
-            return head + stream_head
+            return prefix
         dev = self.device
         raw = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
         x = torch.empty(n * channels, dtype=torch.int32, device=dev)
@@ -153,7 +158,44 @@ class FlacBlockCompressor:
                                      C.c_void_p(out.data_ptr()), C.c_void_p(total.data_ptr()),
                                      C.c_void_p(ws.data_ptr()), ws_bytes, C.c_void_p(s.cuda_stream)), "encode")
         size = int(total.item())
-        return head + stream_head + out[:size].cpu().numpy().tobytes()
+        return prefix + out[:size].cpu().numpy().tobytes()
+
+    def compress_many(self, items) -> list:
+        """compress() of every (data, metadata) pair, all blocks' frames in one launch (rpp_flac_encode_batch);
+        the result is byte-identical to calling compress() per block."""
+        items = list(items)
+        if not items:
+            return []
+        preps = [self._prepare(d, m) for d, m in items]
+        dev = self.device
+        nb = len(items)
+        n = np.array([p[1] for p in preps], np.uint64)
+        ch = np.array([p[2] for p in preps], np.uint32)
+        bp = np.array([p[3] for p in preps], np.uint32)
+        vals = n * ch
+        in_off = np.zeros(nb, np.uint64)
+        if nb > 1:
+            in_off[1:] = np.cumsum(vals)[:-1]
+        x = torch.empty(max(int(vals.sum()), 1), dtype=torch.int32, device=dev)
+        for b, ((data, _), p) in enumerate(zip(items, preps)):
+            if p[1]:
+                raw = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
+                _transformer(p[4], p[3]).unpack(x[int(in_off[b]):int(in_off[b] + vals[b])], raw)
+        L = N.lib()
+        P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        frames = int(sum((int(v) + 4095) // 4096 for v in n))
+        bound = max(int(L.rpp_flac_frame_bound(int(c), int(b))) for c, b in zip(ch, bp))
+        out = torch.empty(frames * bound + 64, dtype=torch.uint8, device=dev)
+        offs = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+        ws_bytes = int(L.rpp_flac_encode_batch_workspace_bytes(nb, P(n), P(ch), P(bp)))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        s = torch.cuda.current_stream(dev)
+        _status(L.rpp_flac_encode_batch(C.c_void_p(x.data_ptr()), nb, P(in_off), P(n), P(ch), P(bp), self.level,
+                                        int(self.exhaustive), C.c_void_p(out.data_ptr()), C.c_void_p(offs.data_ptr()),
+                                        C.c_void_p(ws.data_ptr()), ws_bytes, C.c_void_p(s.cuda_stream)), "encode")
+        o = offs.cpu().numpy()
+        host = out[: int(o[-1])].cpu().numpy().tobytes()
+        return [p[0] + host[int(o[b]):int(o[b + 1])] for b, p in enumerate(preps)]
 
 
 class FlacBlockDecompressor:

@@ -371,6 +371,20 @@ int rpp_flac_encode(const int32_t* d_samples, uint64_t nsamples, uint32_t channe
 int rpp_flac_encode_ex(const int32_t* d_samples, uint64_t nsamples, uint32_t channels, uint32_t bps, uint32_t level,
                        uint32_t exhaustive, uint8_t* d_out, uint64_t* d_total, void* d_workspace,
                        uint64_t workspace_bytes, void* stream);
+/* Several blocks in one launch (DwarFS compresses one block per call,
+ * flac.cpp:284-349; a batching caller, as the ricepp facade does for ricepp,
+ * joins them): block b is h_nsamples[b] interleaved frames of h_channels[b]
+ * int32 samples of h_bps[b] bits at d_samples + h_in_off[b] (host arrays: the
+ * launch needs the frame count).  Its FLAC frames (numbered from 0) are
+ * written to d_out[d_out_off[b], d_out_off[b + 1]) (d_out_off: device,
+ * nblocks + 1 entries), byte-identical to rpp_flac_encode_ex of that block
+ * alone.  Workspace: rpp_flac_encode_batch_workspace_bytes. */
+uint64_t rpp_flac_encode_batch_workspace_bytes(uint32_t nblocks, const uint64_t* h_nsamples, const uint32_t* h_channels,
+                                               const uint32_t* h_bps);
+int rpp_flac_encode_batch(const int32_t* d_samples, uint32_t nblocks, const uint64_t* h_in_off,
+                          const uint64_t* h_nsamples, const uint32_t* h_channels, const uint32_t* h_bps,
+                          uint32_t level, uint32_t exhaustive, uint8_t* d_out, uint64_t* d_out_off, void* d_workspace,
+                          uint64_t workspace_bytes, void* stream);
 uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uint32_t bps, uint32_t max_blocksize,
                                          uint32_t max_candidates);
 int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
