@@ -109,6 +109,23 @@ def _dev_u64(values, device) -> torch.Tensor:
     return torch.as_tensor(np.asarray(values, dtype=np.int64), device=device)
 
 
+def _dev_u64_many(device, *arrays):
+    """Several host int64 arrays in one host-to-device copy (a small batch's call is latency-bound: one copy
+    instead of one per array); returns device views, one per array (a device tensor passes through)."""
+    host = [a for a in arrays if not isinstance(a, torch.Tensor)]
+    flat = np.concatenate([np.asarray(a, dtype=np.int64).reshape(-1) for a in host]) if host else np.zeros(0, np.int64)
+    d = torch.as_tensor(flat, device=device)
+    out, at = [], 0
+    for a in arrays:
+        if isinstance(a, torch.Tensor):
+            out.append(a)
+            continue
+        n = np.asarray(a).size
+        out.append(d[at:at + n])
+        at += n
+    return out
+
+
 def _as_u16_tensor(samples, device) -> torch.Tensor:
     if isinstance(samples, torch.Tensor):
         if samples.element_size() != 2:
@@ -163,7 +180,9 @@ def encode_batch(
     n_samples = np.asarray(n_samples, dtype=np.int64)
     nb = len(n_samples)
     if out_offsets is None:
-        caps = np.array([N.lib().rpp_worst_case_bytes(C.byref(c), int(n)) for n in n_samples], np.int64)
+        # (one rpp_worst_case_bytes call per distinct length)
+        uniq, inv = np.unique(n_samples, return_inverse=True)
+        caps = np.array([N.lib().rpp_worst_case_bytes(C.byref(c), int(n)) for n in uniq], np.int64)[inv]
         caps = (caps + 15) // 16 * 16
         out_offsets = np.zeros(nb, np.int64)
         if nb:
@@ -173,9 +192,7 @@ def encode_batch(
         total = None
     if out is None:
         out = torch.empty(max(total or 0, 16), dtype=torch.uint8, device=dev)
-    d_in_off = _dev_u64(in_offsets, dev)
-    d_n = _dev_u64(n_samples, dev)
-    d_out_off = _dev_u64(out_offsets, dev)
+    d_in_off, d_n, d_out_off = _dev_u64_many(dev, in_offsets, n_samples, out_offsets)
     sizes = torch.empty(nb, dtype=torch.int64, device=dev)
     status = torch.empty(nb, dtype=torch.int32, device=dev)
     total_samples = int(n_samples.sum()) if nb else 0
@@ -252,10 +269,7 @@ def decode_batch(
     if out is None:
         total = int((out_offsets + n_samples).max()) if nb else 0
         out = torch.empty(max(total, 8), dtype=torch.int16, device=dev)
-    d_in_off = in_offsets if isinstance(in_offsets, torch.Tensor) else _dev_u64(in_offsets, dev)
-    d_in_bytes = in_bytes if isinstance(in_bytes, torch.Tensor) else _dev_u64(in_bytes, dev)
-    d_n = _dev_u64(n_samples, dev)
-    d_out_off = _dev_u64(out_offsets, dev)
+    d_in_off, d_in_bytes, d_n, d_out_off = _dev_u64_many(dev, in_offsets, in_bytes, n_samples, out_offsets)
     status = torch.empty(nb, dtype=torch.int32, device=dev)
     total = int(n_samples.sum()) if nb else 0
     longest = int(n_samples.max()) if nb else 0
