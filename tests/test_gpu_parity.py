@@ -338,6 +338,21 @@ def test_at_scale_block_sizes(bs, cs, kind):
     _full_size(kind, nblocks=2048, bs=bs, cs=cs)
 
 
+@pytest.mark.parametrize("kind", ["poisson", "benchmark"])
+@pytest.mark.parametrize("cs", [1, 2])
+@pytest.mark.parametrize("bs", [16, 64, 256])
+def test_at_scale_long_streams(bs, cs, kind):
+    """64 x 1 MiB blocks (bs 256: 16 x 4 MiB, the length from which it splits streams): long streams, so the
+    segmented encode (units of chunks, concat) and the segmented decode (guess, unit parse, stitch, extraction) run
+    at several block sizes and both component counts; the decode is checked to have taken the segmented path."""
+    codec.segmented_decode_stats(reset=True)
+    if bs > 128:
+        _full_size(kind, nblocks=16, n=1 << 21, bs=bs, cs=cs)
+    else:
+        _full_size(kind, nblocks=64, n=1 << 19, bs=bs, cs=cs)
+    assert codec.segmented_decode_stats(reset=True)["met"] > 0
+
+
 @pytest.mark.parametrize("bs,cs,byteorder,ulsb", [(128, 2, "little", 0), (128, 2, "big", 3), (64, 2, "little", 2)])
 def test_at_scale_byteorder_lsb(bs, cs, byteorder, ulsb):
     _full_size("benchmark", nblocks=2048, bs=bs, cs=cs, byteorder=byteorder, ulsb=ulsb)
