@@ -1,5 +1,5 @@
 # Round-5 GPU session steps (run through gpurun; outputs under gpurun_out/r05/).
-# usage: bash tools/gpu_r04.sh step [step ...]
+# usage: bash tools/gpu_r05.sh step [step ...]
 #   isa      instruction-rate microbenchmark (tools/isa_rate)
 #   occ      fused-decode time vs waves per SIMD (tools/occupancy_sweep.py)
 #   bench    bench line, the driver's short command and the default one (no CPU baseline)
