@@ -238,10 +238,15 @@ def case_e2e():
     torch.cuda.synchronize()
     assert torch.equal(h_out, h_in)
     tk_e, tk_d = timed(p.encode), timed(p.decode)
+    # the copies alone, the same buffers
+    t_h2d = timed(lambda: p.samples.copy_(h_in, non_blocking=True), 3)
+    t_d2h = timed(lambda: h_out.copy_(p.decoded[: nb * n], non_blocking=True), 3)
     report("e2e", workload="4096 x 64 KiB Poisson(1000), pinned host buffers", raw_MiB=raw / 2**20,
            encode_e2e_GiBps=round(raw / te / GIB, 2), decode_e2e_GiBps=round(raw / td / GIB, 2),
            roundtrip_e2e_GiBps=round(raw / (te + td) / GIB, 2),
            encode_kernel_GiBps=round(raw / tk_e / GIB, 2), decode_kernel_GiBps=round(raw / tk_d / GIB, 2),
+           h2d_GiBps=round(raw / t_h2d / GIB, 2), d2h_GiBps=round(raw / t_d2h / GIB, 2),
+           samples_contiguous=bool(p.samples.is_contiguous()), samples_dtype=str(p.samples.dtype),
            transfer_bytes_note="encode D2H copies the worst-case-strided image (raw size + framing)")
 
 
