@@ -3242,7 +3242,10 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
 // returns.  For batches of few units (single long streams), where
 // the parse's work queue would run one wave per CU and the lane-serial guess
 // is most of a unit's time.
-constexpr uint32_t kGuessWaves = 8;
+// (16 waves, one workgroup per CU: 8 waves took 1.5-5 % longer on single
+// 16 MiB streams, 16 x 1 MiB and 32 MiB frames; 4 waves x 4 slots and
+// 16 x 4 slower still -- tools/one_stream_prof.py, profiles/r05_guess_waves_ab.txt)
+constexpr uint32_t kGuessWaves = 16;
 constexpr uint32_t kGuessSlots = 2;  // candidates per lane of a chunk (128-candidate chunks)
 constexpr uint32_t kGuessListWords = 2 * kGuessSlots * kWave;  // a wave's survivors: (position, origin | range)
 __host__ __device__ constexpr size_t guess_lds_bytes(uint32_t bs) {
