@@ -172,3 +172,27 @@ def test_flac_metadata_json_is_nlohmann_dump():
     assert FL.FlacBlockCompressor().metadata_requirements() == (
         '{"bits_per_sample":["range",8,32],"bytes_per_sample":["range",1,4],"endianness":["set",["big","little"]],'
         '"number_of_channels":["range",1,8],"padding":["set",["msb","lsb"]],"signedness":["set",["signed","unsigned"]]}')
+
+
+def _pcmaudio_fixtures():
+    from pathlib import Path
+    return json.loads((Path(__file__).resolve().parent / "golden" / "pcmaudio_fixtures.json").read_text())
+
+
+@pytest.mark.parametrize("fx", _pcmaudio_fixtures(), ids=lambda f: f["file"].rsplit("/", 1)[1])
+def test_oracle_round_trips_reference_pcm_fixtures(fx):
+    """The reference's real PCM fixtures (test/pcmaudio/test{8,12,16,20,24,32}.{wav,aiff}, payload and the metadata
+    the pcmaudio categorizer emits: tests/golden/make_golden.py) through the CPU restatement: samples unpacked as
+    the FLAC compressor's pcm_sample_transformer would (flac.cpp:211), encoded, decoded back exactly."""
+    from oracle import oracle as O
+    m = fx["metadata"]
+    pcm = bytes.fromhex(fx["pcm_hex"])
+    x = O.pcm_unpack(pcm, m["endianness"] == "big", m["signedness"] == "signed", m["padding"] == "lsb",
+                     m["bytes_per_sample"], m["bits_per_sample"])
+    assert x.size == len(pcm) // m["bytes_per_sample"] == 7 * m["number_of_channels"]
+    stream = F.encode(x, m["number_of_channels"], m["bits_per_sample"])
+    st, y, ch, bps = F.decode(stream, x.size)
+    assert st == F.OK and (ch, bps) == (m["number_of_channels"], m["bits_per_sample"])
+    assert np.array_equal(y, x)
+    assert O.pcm_pack(y, m["endianness"] == "big", m["signedness"] == "signed", m["padding"] == "lsb",
+                      m["bytes_per_sample"], m["bits_per_sample"]) == pcm

@@ -203,3 +203,36 @@ def test_trailing_bytes_after_the_last_frame():
     comp = FL.FlacBlockCompressor().compress(data, meta(E.Little, S.Signed, Pd.Msb, 2, 2, 16))
     assert FL.decompress(comp + bytes(7)) == data
     assert FL.decompress(comp + b"\xff\xf8" + bytes(30)) == data
+
+
+def _pcmaudio_fixtures():
+    from pathlib import Path
+    return json.loads((Path(__file__).resolve().parent / "golden" / "pcmaudio_fixtures.json").read_text())
+
+
+@pytest.mark.parametrize("fx", _pcmaudio_fixtures(), ids=lambda f: f["file"].rsplit("/", 1)[1])
+def test_reference_pcm_fixtures_round_trip(fx):
+    """The reference's real PCM fixtures (test/pcmaudio/test{8,12,16,20,24,32}.{wav,aiff}) with the metadata the
+    pcmaudio categorizer emits for them (tests/golden/pcmaudio_fixtures.json) through flac_block_compressor /
+    flac_block_decompressor on the GPU: exact bytes back, the metadata carried in the block header, and the GPU's
+    FLAC stream decoded by the CPU restatement to the samples the transformer unpacks.  Parity unpinned: no
+    libFLAC output exists to compare the stream itself with."""
+    from oracle import oracle as O
+    m = fx["metadata"]
+    pcm = bytes.fromhex(fx["pcm_hex"])
+    comp = FL.FlacBlockCompressor().compress(pcm, json.dumps(m))
+    d = FL.FlacBlockDecompressor(comp)
+    assert json.loads(d.metadata()) == m
+    assert d.uncompressed_size() == len(pcm)
+    assert d.decompress() == pcm
+    x = O.pcm_unpack(pcm, m["endianness"] == "big", m["signedness"] == "signed", m["padding"] == "lsb",
+                     m["bytes_per_sample"], m["bits_per_sample"])
+    st, y, ch, bps = F.decode(d.stream, x.size)
+    assert st == F.OK and (ch, bps) == (m["number_of_channels"], m["bits_per_sample"])
+    assert np.array_equal(y, x)
+    # and the restatement's stream of the same samples decoded by the GPU
+    stream = F.encode(x, m["number_of_channels"], m["bits_per_sample"])
+    nb = m["bytes_per_sample"]
+    flags = (FL.FLAG_BIG_ENDIAN if m["endianness"] == "big" else 0) | (FL.FLAG_SIGNED if m["signedness"] == "signed" else 0) \
+        | (FL.FLAG_LSB_PADDING if m["padding"] == "lsb" else 0) | (nb - 1)
+    assert FL.decompress(FL.frame_header(len(pcm), m["number_of_channels"], m["bits_per_sample"], flags) + stream) == pcm
