@@ -6,6 +6,7 @@ branch counters (ricepp_kernels.hip branch_diag).  One JSON line per repeat.
 Usage: RICEPP_AMD_LIB=... python tools/branch_diag.py <label> [repeats] [nblocks]"""
 import ctypes as C
 import json
+import os
 import sys
 
 import numpy as np
@@ -33,11 +34,19 @@ oc = O.cfg(128, 2, True, 0)
 offs = np.arange(nblocks, dtype=np.int64) * n
 ob, oo, osz, ost = O.encode_batch(oc, x, offs.astype(np.uint64), [n] * nblocks, O.worst_case_bytes(oc, n), nthreads=16)
 d = torch.from_numpy(x.view(np.int16)).to("cuda:0")
+fill = int(os.environ["FILL"]) if "FILL" in os.environ else None
+first = None  # rep 0's output: later reps report the streams that differ from it (run-to-run nondeterminism)
 for rep in range(reps):
     cnt = np.zeros(8, np.uint64)
     if fetch is not None:
         fetch(cnt.ctypes.data, 1)
-    enc = codec.encode_batch(cfg, d, offs, [n] * nblocks)
+    if fill is None:
+        enc = codec.encode_batch(cfg, d, offs, [n] * nblocks)
+    else:  # output buffer pre-filled with one byte value (default: torch.empty, whatever was there)
+        cap = (O.worst_case_bytes(oc, n) + 15) // 16 * 16
+        outbuf = torch.full((cap * nblocks,), fill, dtype=torch.uint8, device="cuda:0")
+        enc = codec.encode_batch(cfg, d, offs, [n] * nblocks, out=outbuf,
+                                 out_offsets=np.arange(nblocks, dtype=np.int64) * cap)
     torch.cuda.synchronize()
     if fetch is not None:
         fetch(cnt.ctypes.data, 1)
@@ -62,6 +71,15 @@ for rep in range(reps):
                 spans.append(int(dif[-1] - dif[0]) + 1)
     rec = {"label": label, "rep": rep, "streams": nblocks, "wrong_streams": wrong, "wrong_bytes": wrong_bytes,
            "extra_bits": extra_bits, "missing_bits": missing_bits}
+    blocks_out = [bytes(data[enc.offsets[i]:enc.offsets[i] + sizes[i]]) for i in range(nblocks)]
+    if first is None:
+        first = blocks_out
+        if os.environ.get("DUMP"):  # the first 64 wrong streams of rep 0, for offline analysis
+            bad = [i for i in range(nblocks) if blocks_out[i] != bytes(ob[int(oo[i]):int(oo[i]) + int(osz[i])])][:64]
+            np.savez_compressed(os.environ["DUMP"], idx=np.array(bad, np.int64),
+                                **{f"s{i}": np.frombuffer(blocks_out[i], np.uint8) for i in bad})
+    else:
+        rec["differ_from_rep0"] = sum(1 for i in range(nblocks) if blocks_out[i] != first[i])
     if first_bits:
         fb = np.array(first_bits)
         rec.update({"first_diff_bit_pct": [int(np.percentile(fb, q)) for q in (0, 10, 50, 90, 100)],
