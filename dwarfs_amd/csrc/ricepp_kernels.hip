@@ -217,46 +217,6 @@ __device__ __forceinline__ uint32_t gsum(uint32_t v) {
   return v;
 }
 
-// Wave-uniform "any active lane has c", branched on through a VCC written by
-// the scalar unit.  __any() compiles to v_cmp -> s_cbranch_vccz; at the
-// emission fast-path test that branch measured to go the wrong way now and
-// then on gfx950 with several waves per SIMD (bs 128 cs 2 high-entropy
-// batches: most 64 KiB streams wrong, run to run different; through the
-// scalar unit: none).  DESIGN.md section 4 "Uniform branches".
-__device__ __forceinline__ bool wave_any_salu(bool c) {
-  return __builtin_amdgcn_readfirstlane((uint32_t)(__builtin_amdgcn_ballot_w64(c) != 0)) != 0u;
-}
-
-#ifdef RPP_DIAG_BRANCH_CHECK
-// Diagnostic build only: counts how the emission's uniform branch went
-// against the condition re-evaluated after it (tools/branch_diag.py).
-// [0] fast path entered, [1] fast path entered although a lane needs the
-// slow one, [2] slow path entered, [3] slow path entered although no lane
-// needs it; for the wrong fast entries: [4] EXEC high half empty, [5] EXEC
-// low half empty, [6] a wide lane in the low half, [7] a wide lane in the
-// high half.
-__device__ unsigned long long g_branch_diag[8];
-__device__ __forceinline__ void branch_diag(bool fast, bool wide) {
-  const uint64_t ex = __builtin_amdgcn_read_exec();
-  const uint64_t wb = __builtin_amdgcn_ballot_w64(wide);
-  const bool first = lane_id() == (uint32_t)__builtin_ctzll(ex);
-  if (!first) return;
-  if (fast) {
-    atomicAdd(&g_branch_diag[0], 1ull);
-    if (wb) {
-      atomicAdd(&g_branch_diag[1], 1ull);
-      if ((ex >> 32) == 0) atomicAdd(&g_branch_diag[4], 1ull);
-      if ((uint32_t)ex == 0) atomicAdd(&g_branch_diag[5], 1ull);
-      if ((uint32_t)wb) atomicAdd(&g_branch_diag[6], 1ull);
-      if (wb >> 32) atomicAdd(&g_branch_diag[7], 1ull);
-    }
-  } else {
-    atomicAdd(&g_branch_diag[2], 1ull);
-    if (!wb) atomicAdd(&g_branch_diag[3], 1ull);
-  }
-}
-#endif
-
 // Per-lane sub-block geometry of one encode iteration.
 struct EncGeom {
   uint32_t n;        // samples in this lane's sub-block (0: no sub-block)
@@ -350,12 +310,16 @@ __device__ __forceinline__ void emit_bits(uint32_t* win, uint32_t rel, uint32_t 
   atomicOr(&win[w + 1], (v >> 1) >> (31u - sh));
 }
 
-// The same for codes of <= 32 bits by one 64-bit shift.
+// The same for codes of <= 32 bits.  32-bit shifts only: a 64-bit shift
+// (v_lshlrev_b64) whose amount the register allocator happens to place in the
+// last VGPR of the kernel's allocation reads a wrong amount on gfx950 while
+// other waves share the SIMD -- the round-5 bs 128 cs 2 fault (DESIGN.md §4
+// "64-bit shifts and the last VGPR"; tools/isa_audit.py guards the build).
 __device__ __forceinline__ void emit_bits64(uint32_t* win, uint32_t rel, uint32_t v) {
-  const uint64_t x = (uint64_t)v << (rel & 31u);
+  const uint32_t sh = rel & 31u;
   uint32_t* w = win + (rel >> 5);
-  atomicOr(w, (uint32_t)x);
-  atomicOr(w + 1, (uint32_t)(x >> 32));
+  atomicOr(w, v << sh);
+  atomicOr(w + 1, (v >> 1) >> (31u - sh));
 }
 
 constexpr uint32_t kEncWin = 1024;      // LDS output window (words, 4 KiB)
@@ -493,7 +457,7 @@ __device__ __forceinline__ void enc_plan_b(EncPlan<SPL>& P, EncState& st, uint32
   walk_step(P.walking && P.cand > 0 && P.cand < 14);
   for (;;) {
     const bool act = P.walking && P.cand > 0 && P.cand < 14;
-    if (!wave_any_salu(act)) break;
+    if (!__any(act)) break;
     walk_step(act);
   }
   // encode.h:127-156: 0 = all-zero, 1 = Rice, 2 = raw
@@ -538,16 +502,7 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
     // the pair (2h, 2h+1) spans k + q_(2h+1) + k bits from code 2h's '1':
     // when that fits 32 bits for every pair of the wave (fs <= 13 and unary
     // runs short: Poisson data), one 64-bit shift and two ds_or_b32 per pair
-    const bool wide = 2u * k + (as_u32(qmax) >> 16) > 32u;
-#ifdef RPP_DIAG_VALU_ANY
-    // diagnostic only: the round-5 form (v_cmp -> vcc -> s_cbranch_vccz)
-    if (!__any(wide)) {
-#else
-    if (!wave_any_salu(wide)) {
-#endif
-#ifdef RPP_DIAG_BRANCH_CHECK
-      branch_diag(true, wide);
-#endif
+    if (!__any(2u * k + (as_u32(qmax) >> 16) > 32u)) {
 #pragma unroll
       for (uint32_t h = 0; h < SPL / 2; ++h) {
         const uint32_t qq = as_u32(qv[h]);
@@ -558,9 +513,6 @@ __device__ __forceinline__ void enc_emit(const EncPlan<SPL>& P, EncState& st, ui
         e += d;
       }
     } else {
-#ifdef RPP_DIAG_BRANCH_CHECK
-      branch_diag(false, wide);
-#endif
 #pragma unroll
       for (uint32_t h = 0; h < SPL / 2; ++h) {
         const uint32_t qq = as_u32(qv[h]);
@@ -3368,18 +3320,6 @@ int rpp_parse_diag_read(unsigned long long* out16, int reset) {
   }
   return RPP_OK;
 }
-
-#ifdef RPP_DIAG_BRANCH_CHECK
-// Diagnostic build only: copies (and optionally clears) the branch counters.
-int rpp_branch_diag_fetch(uint64_t* out8, int reset) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_branch_diag), sizeof(uint64_t) * 8) != hipSuccess) return RPP_HIP_ERROR;
-  if (reset) {
-    uint64_t z[8] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_branch_diag), z, sizeof z) != hipSuccess) return RPP_HIP_ERROR;
-  }
-  return RPP_OK;
-}
-#endif
 
 #ifdef RPP_STATS
 // Diagnostic build only: copies (and optionally clears) the loop counters.

@@ -323,8 +323,9 @@ def test_full_size_4096x64k_benchmark_generator_bit_exact():
 
 def test_full_size_4096x64k_generator_two_streams_bit_exact():
     """Two component streams (bs 128 cs 2) on high-entropy data: the launch that runs several encode waves per SIMD
-    and takes the emission slow path in almost every group (the fast/slow test once branched on a v_cmp-written
-    VCC and went the wrong way in most streams here; DESIGN.md section 4 "Uniform branches")."""
+    and takes the emission slow path in almost every group: the round-5 build corrupted most streams here, a 64-bit
+    shift taking its amount from the kernel's last allocated VGPR (DESIGN.md section 4 "64-bit shifts and the last
+    VGPR")."""
     _full_size("benchmark", cs=2)
 
 

@@ -1,4 +1,4 @@
-"""Diagnostic (DESIGN.md §4 "Uniform branches"): builds libricepp_amd_<name>.so
+"""Diagnostic (DESIGN.md §4 "64-bit shifts and the last VGPR"): builds libricepp_amd_<name>.so
 from the RPP_DIAG_VALU_ANY build of ricepp_kernels.hip with its bs 128 cs 2
 encode kernel's emission branches edited in the gfx950 assembly, to test
 what the fault depends on.  Edits (before each `s_cbranch_vccz` that follows
@@ -21,7 +21,9 @@ the emission's `v_cmp_lt_u32 vcc, 32, vN`):
   sh64d / sh64sd  controls: the same copies made, but the shift still reads its original registers
   vg144 / vg137 / acc140  no code change; the kernel's VGPR count in its descriptor and metadata set to 144 / 137
         (accum_offset 144 / 140), or only accum_offset raised to 140
-Usage: python tools/asm_variant.py <edit>  (writes dwarfs_amd/lib/libricepp_amd_asm_<edit>.so)"""
+Usage: python tools/asm_variant.py <edit>  (writes dwarfs_amd/lib/libricepp_amd_asm_<edit>.so)
+Run on the round-6 investigation's source (git show bfbb877 -- the round-5 kernels with the RPP_DIAG_VALU_ANY
+switch; today's source has neither the switch nor the 64-bit emission shift)."""
 import re
 import shlex
 import subprocess

@@ -1,4 +1,4 @@
-"""Diagnostic for DESIGN.md §4 "Uniform branches": encodes 4096 x 64 KiB
+"""Diagnostic for DESIGN.md §4 "64-bit shifts and the last VGPR": encodes 4096 x 64 KiB
 benchmark-generator blocks at bs 128 cs 2 with the library named by
 RICEPP_AMD_LIB (a tools/variant.sh build), counts the streams that differ from
 the oracle, and -- for a -DRPP_DIAG_BRANCH_CHECK build -- reads the emission
