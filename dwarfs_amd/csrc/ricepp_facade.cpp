@@ -78,6 +78,10 @@ inline uint64_t now_ns() {
              std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
+// batch trace (set_facade_trace): records appended when a batch is released
+std::atomic<bool> g_trace_on{false};
+std::mutex g_trace_mu;
+std::vector<facade_batch_record> g_trace;
 
 int current_device() {
   int d = 0;
@@ -360,7 +364,8 @@ struct batch {
   bool packed = true;  // encode: outputs packed back to back (else at their slots)
   std::atomic<uint32_t> done{0};      // results published (callers wait on it)
   std::atomic<size_t> finished{0};    // callers that have copied out
-  uint64_t t_close = 0, t_launch = 0, t_done = 0;
+  uint64_t t_open = 0, t_close = 0, t_ready = 0, t_launch = 0, t_done = 0;
+  int inflight_at_close = 0;
 };
 
 constexpr size_t kMaxBatchBlocks = 8192;
@@ -495,6 +500,7 @@ class batch_queue {
     lk.unlock();
     device_ctx* c = nullptr;
     auto* b = new batch;
+    b->t_open = now_ns();
     try {
       c = ctx_pool::get().acquire(dev_, encode_ ? 0 : 1);
       const size_t big = std::max(need_in(r), need_out(r));
@@ -533,6 +539,7 @@ class batch_queue {
   void close(batch* b) {
     b->closed = true;
     b->t_close = now_ns();
+    b->inflight_at_close = inflight_;
     ++inflight_;
     if (open_ == b) {
       open_ = nullptr;
@@ -547,6 +554,7 @@ class batch_queue {
   // (lk held) closed and every input copied in: the driver launches it
   // (once the queue is stopping, nothing more is launched)
   void make_ready(batch* b) {
+    b->t_ready = now_ns();
     if (stopping_) {
       fail(b, "ricepp_amd: facade shut down");
       return;
@@ -671,7 +679,14 @@ class batch_queue {
   // (lk held) the last caller has copied its result out; returns the
   // context, for the caller to pool once it has dropped the lock
   device_ctx* release(batch* b) {
-    g_finish_ns.fetch_add(now_ns() - b->t_done, std::memory_order_relaxed);
+    const uint64_t t_release = now_ns();
+    g_finish_ns.fetch_add(t_release - b->t_done, std::memory_order_relaxed);
+    if (g_trace_on.load(std::memory_order_relaxed)) {
+      std::lock_guard<std::mutex> tl(g_trace_mu);
+      g_trace.push_back(facade_batch_record{encode_, (uint32_t)b->reqs.size(), b->in_fill, b->out_fill,
+                                            b->inflight_at_close, b->t_open, b->t_close, b->t_ready, b->t_launch,
+                                            b->t_done, t_release});
+    }
     device_ctx* c = b->ctx;
     delete b;
     --alive_;
@@ -1047,6 +1062,14 @@ facade_stats get_facade_stats() {
 }
 
 void shutdown_facade() { shutdown_all(); }
+
+void set_facade_trace(bool on) { g_trace_on.store(on); }
+std::vector<facade_batch_record> take_facade_trace() {
+  std::lock_guard<std::mutex> tl(g_trace_mu);
+  std::vector<facade_batch_record> out;
+  out.swap(g_trace);
+  return out;
+}
 
 // ---- block_compressor (src/compression/ricepp.cpp:57-182, 272-296) ----
 

@@ -252,6 +252,20 @@ struct facade_stats {
 };
 facade_stats get_facade_stats();
 
+// ---- facade batch trace (diagnostics: how batches formed and overlapped) ----
+// One record per batch once its last caller has left it; times are
+// steady_clock nanoseconds.  Off unless enabled; take_facade_trace() returns
+// the records so far and clears them.
+struct facade_batch_record {
+  bool encode;
+  uint32_t requests;
+  uint64_t in_bytes, out_bytes;
+  int inflight_at_close;  // batches of the queue on the device when this one closed
+  uint64_t t_open, t_close, t_ready, t_launch, t_done, t_release;
+};
+void set_facade_trace(bool on);
+std::vector<facade_batch_record> take_facade_trace();
+
 // Stops the facade's queues: batches on the device complete, batches not yet
 // launched fail (std::runtime_error), calls made afterwards fail, and the
 // queue threads are joined.  Registered with std::atexit when the first queue

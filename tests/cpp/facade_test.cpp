@@ -409,6 +409,70 @@ int main(int argc, char** argv) {
   return failures ? 1 : 0;
 }
 
+// Summary of a run's batch trace (facade_test --bench ... --trace): per
+// direction the batches, their sizes, how many were on the device at once,
+// and the mean time per batch in each phase (open -> close: gathering
+// callers; close -> ready: the last caller's copy in; ready -> launch: the
+// driver; launch -> done: device; done -> release: copies out).
+std::string trace_summary(std::vector<ricepp_amd::facade_batch_record> recs, std::chrono::steady_clock::time_point w0,
+                          std::chrono::steady_clock::time_point w1, std::chrono::steady_clock::time_point w2) {
+  auto ns = [](std::chrono::steady_clock::time_point t) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t.time_since_epoch()).count();
+  };
+  std::string out;
+  for (int enc = 1; enc >= 0; --enc) {
+    std::vector<ricepp_amd::facade_batch_record> v;
+    for (auto& r : recs)
+      if (r.encode == (enc == 1)) v.push_back(r);
+    std::sort(v.begin(), v.end(), [](auto& a, auto& b) { return a.t_launch < b.t_launch; });
+    const uint64_t a = ns(enc ? w0 : w1), z = ns(enc ? w1 : w2);
+    double ph[5] = {0, 0, 0, 0, 0};
+    uint32_t rmin = ~0u, rmax = 0, rsum = 0;
+    int closed_busy = 0;
+    std::string sizes;
+    for (auto& r : v) {
+      ph[0] += r.t_close - r.t_open;
+      ph[1] += r.t_ready - r.t_close;
+      ph[2] += r.t_launch - r.t_ready;
+      ph[3] += r.t_done - r.t_launch;
+      ph[4] += r.t_release - r.t_done;
+      rmin = std::min(rmin, r.requests);
+      rmax = std::max(rmax, r.requests);
+      rsum += r.requests;
+      closed_busy += r.inflight_at_close > 0;
+      sizes += (sizes.empty() ? "" : ",") + std::to_string(r.requests);
+    }
+    // time with >= 2 batches between launch and done, over the run's wall time
+    std::vector<std::pair<uint64_t, int>> ev;
+    for (auto& r : v) {
+      ev.emplace_back(r.t_launch, +1);
+      ev.emplace_back(r.t_done, -1);
+    }
+    std::sort(ev.begin(), ev.end());
+    uint64_t two = 0, idle = 0, prev = a;
+    int cur = 0;
+    for (auto& [t, d] : ev) {
+      const uint64_t tt = std::clamp(t, a, z);
+      if (cur >= 2) two += tt - prev;
+      if (cur == 0) idle += tt - prev;
+      prev = tt;
+      cur += d;
+    }
+    if (prev < z && cur == 0) idle += z - prev;
+    const double nb = v.empty() ? 1.0 : double(v.size()), wall = double(z - a);
+    char buf[640];
+    std::snprintf(buf, sizeof buf,
+                  ", \"%s_trace\": {\"batches\": %zu, \"requests\": [%s], \"closed_while_busy\": %d, "
+                  "\"two_in_flight_frac\": %.3f, \"device_idle_frac\": %.3f, \"us_per_batch\": {\"gather\": %.0f, "
+                  "\"stage\": %.0f, \"driver\": %.0f, \"device\": %.0f, \"finish\": %.0f}}",
+                  enc ? "encode" : "decode", v.size(), sizes.c_str(), closed_busy, two / wall, idle / wall,
+                  ph[0] / nb / 1e3, ph[1] / nb / 1e3, ph[2] / nb / 1e3, ph[3] / nb / 1e3, ph[4] / nb / 1e3);
+    out += buf;
+    (void)rmin; (void)rmax; (void)rsum;
+  }
+  return out;
+}
+
 // ---- facade throughput (facade_test --bench [blocks] [threads...]) ----
 // DwarFS's worker_group shape: T threads, each compressing / decompressing
 // its share of B independent 64 KiB blocks through the facade (host spans in
@@ -420,8 +484,12 @@ int bench(int argc, char** argv) {
   std::vector<int> threads;
   size_t kib = 64;
   int depth = 0;  // 0: the library's default
+  int repeat = 1;
+  bool trace = false;
   for (int i = 3; i < argc; ++i) {
     if (std::string(argv[i]).rfind("--kib=", 0) == 0) kib = std::strtoul(argv[i] + 6, nullptr, 10);
+    else if (std::string(argv[i]).rfind("--repeat=", 0) == 0) repeat = std::atoi(argv[i] + 9);
+    else if (std::string(argv[i]) == "--trace") trace = true;
     else if (std::string(argv[i]).rfind("--depth=", 0) == 0) depth = std::atoi(argv[i] + 8);
     else if (std::string(argv[i]).rfind("--pack-max-mib=", 0) == 0)
       ricepp_amd::set_facade_pack_limit(std::strtoull(argv[i] + 15, nullptr, 10) << 20);
@@ -472,11 +540,21 @@ int bench(int argc, char** argv) {
     };
     run(true);  // warm the contexts (both directions: decode grows their buffers differently)
     run(false);
+    for (int rep = 0; rep < repeat; ++rep) {
+    if (trace) {
+      ricepp_amd::set_facade_trace(true);
+      (void)ricepp_amd::take_facade_trace();
+    }
     auto s0 = ricepp_amd::get_facade_stats();
+    const auto w0 = std::chrono::steady_clock::now();
     double te = run(true);
+    const auto w1 = std::chrono::steady_clock::now();
     auto s1 = ricepp_amd::get_facade_stats();
     double td = run(false);
+    const auto w2 = std::chrono::steady_clock::now();
     auto s2 = ricepp_amd::get_facade_stats();
+    std::string trace_json;
+    if (trace) trace_json = trace_summary(ricepp_amd::take_facade_trace(), w0, w1, w2);
     if (failed.load()) return 3;
     bool ok = true;
     int reported = 0;
@@ -506,14 +584,15 @@ int bench(int argc, char** argv) {
                 "\"encode_GiBps\": %.3f, \"decode_GiBps\": %.3f, \"encode_launches\": %.0f, "
                 "\"decode_launches\": %.0f, \"encode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, "
                 "\"device_events\": %.1f, \"finish\": %.1f}, \"decode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, "
-                "\"device_events\": %.1f, \"finish\": %.1f}, \"roundtrip_ok\": %s}\n",
+                "\"device_events\": %.1f, \"finish\": %.1f}, \"roundtrip_ok\": %s%s}\n",
                 T, depth, blocks, n * 2, gib / te, gib / td, ne, nd, (s1.stage_ns - s0.stage_ns) / 1e3 / ne,
                 (s1.device_ns - s0.device_ns) / 1e3 / ne, (s1.device_event_ns - s0.device_event_ns) / 1e3 / ne,
                 (s1.finish_ns - s0.finish_ns) / 1e3 / ne, (s2.stage_ns - s1.stage_ns) / 1e3 / nd,
                 (s2.device_ns - s1.device_ns) / 1e3 / nd, (s2.device_event_ns - s1.device_event_ns) / 1e3 / nd,
-                (s2.finish_ns - s1.finish_ns) / 1e3 / nd, ok ? "true" : "false");
+                (s2.finish_ns - s1.finish_ns) / 1e3 / nd, ok ? "true" : "false", trace_json.c_str());
     std::fflush(stdout);
     if (!ok) return 1;
+    }
   }
   return 0;
 }
