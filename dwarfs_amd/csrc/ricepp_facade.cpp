@@ -61,7 +61,8 @@ rpp_config to_rpp(codec_config const& c) {
 
 size_t align16(size_t v) { return (v + 15) & ~size_t{15}; }
 
-std::atomic<uint64_t> g_enc_launches{0}, g_enc_blocks{0}, g_dec_launches{0}, g_dec_blocks{0}, g_ctx_created{0};
+std::atomic<uint64_t> g_enc_launches{0}, g_enc_blocks{0}, g_dec_launches{0}, g_dec_blocks{0}, g_ctx_created{0},
+    g_buffer_grows{0}, g_buffer_grow_ns{0};
 std::atomic<uint32_t> g_ctx_faults{0};     // inject_context_failures
 std::atomic<uint32_t> g_launch_faults{0};  // inject_launch_failures
 // a test hook: throws once per injected launch failure
@@ -155,6 +156,8 @@ class device_ctx {
   uint8_t* workspace(size_t bytes) { return grow_dev(wbuf_, wcap_, bytes); }
   uint8_t* pin_in(size_t bytes) { return grow_pinned(hin_, hin_cap_, bytes); }
   uint8_t* pin_out(size_t bytes) { return grow_pinned(hout_, hout_cap_, bytes); }
+  size_t pinned_capacity() const { return hin_cap_ + hout_cap_; }
+  bool pinned_fits(size_t in, size_t out) const { return hin_ && hout_ && in <= hin_cap_ && out <= hout_cap_; }
   // the device-side address of a pinned buffer
   uint8_t* device_view(uint8_t* pinned) {
     void* d = nullptr;
@@ -203,11 +206,14 @@ class device_ctx {
     if (bytes <= cap && p) return p;
     size_t n = cap ? cap : size_t{1} << 20;
     while (n < bytes) n *= 2;
+    const uint64_t t0 = now_ns();
     if (p) (void)hipFree(p);  // (the context is idle: its last batch has completed)
     p = nullptr;
     cap = 0;
     void* q = nullptr;
     hip_check(hipMalloc(&q, n), "hipMalloc");
+    g_buffer_grows.fetch_add(1, std::memory_order_relaxed);
+    g_buffer_grow_ns.fetch_add(now_ns() - t0, std::memory_order_relaxed);
     p = static_cast<uint8_t*>(q);
     cap = n;
     return p;
@@ -217,11 +223,14 @@ class device_ctx {
     if (bytes <= cap && p) return p;
     size_t n = cap ? cap : size_t{1} << 20;
     while (n < bytes) n *= 2;
+    const uint64_t t0 = now_ns();
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
     void* q = nullptr;
     hip_check(hipHostMalloc(&q, n, hipHostMallocMapped), "hipHostMalloc");
+    g_buffer_grows.fetch_add(1, std::memory_order_relaxed);
+    g_buffer_grow_ns.fetch_add(now_ns() - t0, std::memory_order_relaxed);
     p = static_cast<uint8_t*>(q);
     cap = n;
     return p;
@@ -254,14 +263,27 @@ class ctx_pool {
   // decode size their device and pinned buffers differently, and a context
   // handed from one to the other regrew them (hipFree / hipHostFree
   // synchronise the device) -- one pool per kind keeps them grown
-  device_ctx* acquire(int dev, int kind) {
+  // A batch asks for the pinned capacity it will use: the pooled context that
+  // already holds enough and the least of it, else the one holding the most
+  // (growing a buffer frees the old one first, which synchronises the
+  // device: a 16 MiB-block batch regrowing 256 MiB of pinned memory stalled
+  // both streams for ~70 ms, profiles/r06_facade_16m.jsonl).
+  device_ctx* acquire(int dev, int kind, size_t pin_in = 0, size_t pin_out = 0) {
     if (g_shutdown.load(std::memory_order_acquire)) throw std::runtime_error("ricepp_amd: facade shut down");
     {
       std::lock_guard<std::mutex> lk(mu_);
       auto& v = free_[{dev, kind}];
       if (!v.empty()) {
-        device_ctx* c = v.back();
-        v.pop_back();
+        size_t best = v.size() - 1;  // (the most recent: LIFO when nothing is asked)
+        if (pin_in || pin_out) {
+          for (size_t i = 0; i < v.size(); ++i) {
+            const bool fi = v[i]->pinned_fits(pin_in, pin_out), fb = v[best]->pinned_fits(pin_in, pin_out);
+            const size_t ci = v[i]->pinned_capacity(), cb = v[best]->pinned_capacity();
+            if (fi != fb ? fi : (fi ? ci < cb : ci > cb)) best = i;
+          }
+        }
+        device_ctx* c = v[best];
+        v.erase(v.begin() + best);
         return c;
       }
     }
@@ -364,6 +386,7 @@ struct batch {
   bool packed = true;  // encode: outputs packed back to back (else at their slots)
   std::atomic<uint32_t> done{0};      // results published (callers wait on it)
   std::atomic<size_t> finished{0};    // callers that have copied out
+  size_t join = 1;  // requests of the opening one's size it was sized for
   uint64_t t_open = 0, t_close = 0, t_ready = 0, t_launch = 0, t_done = 0;
   int inflight_at_close = 0;
 };
@@ -388,6 +411,14 @@ std::atomic<size_t> g_pack_max{~size_t{0}};
 // batches of one queue on the device at once (set_facade_pipeline_depth
 // changes it for benchmarks)
 std::atomic<int> g_max_active{2};
+// A batch of large requests (one opened with room for several, kLargeJoin)
+// that a caller finishes staging while another batch is on the device closes
+// only once it holds this many requests (else the completion of the batch on
+// the device closes it): DwarFS-style worker pools finish a batch together
+// and re-enter one by one, and closing at the first one's staging split them
+// into uneven batches -- 8, 1, 7, 1, 8 ... of 16 MiB blocks
+// (profiles/r06_facade_16m_*.jsonl).  set_facade_large_min_fill changes it.
+std::atomic<int> g_large_min_fill{4};
 // batches alive per queue beyond those on the device (open + being copied
 // out); a caller that finds none with room waits for one to be released
 constexpr int kSpareBatches = 2;
@@ -422,7 +453,10 @@ class batch_queue {
     if (r.in_bytes) std::memcpy(r.pin_in, r.in, r.in_bytes);
     lk.lock();
     ++b->staged;
-    if (!b->closed && (stopping_ || inflight_ < g_max_active.load(std::memory_order_relaxed))) close(b);
+    if (!b->closed && (stopping_ || (inflight_ < g_max_active.load(std::memory_order_relaxed) &&
+                                     (inflight_ == 0 || b->join == 1 ||
+                                      b->reqs.size() >= std::min<size_t>(b->join, (size_t)g_large_min_fill.load())))))
+      close(b);
     else if (b->closed && b->staged == b->reqs.size()) make_ready(b);
     lk.unlock();
     while (!b->done.load(std::memory_order_acquire)) b->done.wait(0, std::memory_order_acquire);
@@ -502,13 +536,14 @@ class batch_queue {
     auto* b = new batch;
     b->t_open = now_ns();
     try {
-      c = ctx_pool::get().acquire(dev_, encode_ ? 0 : 1);
       const size_t big = std::max(need_in(r), need_out(r));
       const size_t join = need_out(r) > kBatchOut / 4 || need_in(r) > kBatchIn / 4
                               ? std::clamp<size_t>(kLargeJoinBudget / big, 1, kLargeJoin)
                               : 1;
+      b->join = join;
       b->in_cap = std::max(kBatchIn, join * need_in(r) + arrays_in(join));
       b->out_cap = std::max(kBatchOut, join * need_out(r) + arrays_out(join));
+      c = ctx_pool::get().acquire(dev_, encode_ ? 0 : 1, b->in_cap, b->out_cap);
       device_guard g{dev_};
       b->pin_in = c->pin_in(b->in_cap);
       b->pin_out = c->pin_out(b->out_cap);
@@ -1054,11 +1089,12 @@ void inject_launch_failures(uint32_t n) { g_launch_faults.store(n); }
 
 void set_facade_pipeline_depth(int batches) { g_max_active.store(std::max(1, std::min(batches, 16))); }
 void set_facade_pack_limit(size_t bytes) { g_pack_max.store(bytes); }
+void set_facade_large_min_fill(int requests) { g_large_min_fill.store(std::max(1, requests)); }
 
 facade_stats get_facade_stats() {
   return facade_stats{g_enc_launches.load(), g_enc_blocks.load(), g_dec_launches.load(), g_dec_blocks.load(),
                       g_ctx_created.load(),  g_stage_ns.load(),   g_device_ns.load(),    g_finish_ns.load(),
-                      g_device_event_ns.load()};
+                      g_device_event_ns.load(), g_buffer_grows.load(), g_buffer_grow_ns.load()};
 }
 
 void shutdown_facade() { shutdown_all(); }

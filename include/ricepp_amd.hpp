@@ -249,6 +249,10 @@ struct facade_stats {
   // summed over batches (ns): the device part by the device's clock (events
   // recorded before the batch's first copy and after its last operation)
   uint64_t device_event_ns;
+  // context buffers (re)allocated, and the time spent doing it (ns): a
+  // pinned or device buffer that grows is freed first, which synchronises
+  // the whole device
+  uint64_t buffer_grows, buffer_grow_ns;
 };
 facade_stats get_facade_stats();
 
@@ -290,5 +294,9 @@ void set_facade_pipeline_depth(int batches);
 // the host by one DMA copy of their slots instead of being packed into mapped
 // host memory by a kernel (default: always packed).
 void set_facade_pack_limit(size_t bytes);
+// Benchmarks: a batch of large requests (blocks of 4 MiB and up) that fills
+// while another batch is on the device goes out once it holds this many
+// requests (default 4; 1 = as soon as its first caller has copied in).
+void set_facade_large_min_fill(int requests);
 
 }  // namespace ricepp_amd

@@ -429,7 +429,7 @@ std::string trace_summary(std::vector<ricepp_amd::facade_batch_record> recs, std
     double ph[5] = {0, 0, 0, 0, 0};
     uint32_t rmin = ~0u, rmax = 0, rsum = 0;
     int closed_busy = 0;
-    std::string sizes;
+    std::string sizes;  // (at most 40 listed)
     for (auto& r : v) {
       ph[0] += r.t_close - r.t_open;
       ph[1] += r.t_ready - r.t_close;
@@ -440,7 +440,7 @@ std::string trace_summary(std::vector<ricepp_amd::facade_batch_record> recs, std
       rmax = std::max(rmax, r.requests);
       rsum += r.requests;
       closed_busy += r.inflight_at_close > 0;
-      sizes += (sizes.empty() ? "" : ",") + std::to_string(r.requests);
+      if (&r - v.data() < 40) sizes += (sizes.empty() ? "" : ",") + std::to_string(r.requests);
     }
     // time with >= 2 batches between launch and done, over the run's wall time
     std::vector<std::pair<uint64_t, int>> ev;
@@ -460,7 +460,7 @@ std::string trace_summary(std::vector<ricepp_amd::facade_batch_record> recs, std
     }
     if (prev < z && cur == 0) idle += z - prev;
     const double nb = v.empty() ? 1.0 : double(v.size()), wall = double(z - a);
-    char buf[640];
+    char buf[1024];
     std::snprintf(buf, sizeof buf,
                   ", \"%s_trace\": {\"batches\": %zu, \"requests\": [%s], \"closed_while_busy\": %d, "
                   "\"two_in_flight_frac\": %.3f, \"device_idle_frac\": %.3f, \"us_per_batch\": {\"gather\": %.0f, "
@@ -490,6 +490,8 @@ int bench(int argc, char** argv) {
     if (std::string(argv[i]).rfind("--kib=", 0) == 0) kib = std::strtoul(argv[i] + 6, nullptr, 10);
     else if (std::string(argv[i]).rfind("--repeat=", 0) == 0) repeat = std::atoi(argv[i] + 9);
     else if (std::string(argv[i]) == "--trace") trace = true;
+    else if (std::string(argv[i]).rfind("--min-fill=", 0) == 0)
+      ricepp_amd::set_facade_large_min_fill(std::atoi(argv[i] + 11));
     else if (std::string(argv[i]).rfind("--depth=", 0) == 0) depth = std::atoi(argv[i] + 8);
     else if (std::string(argv[i]).rfind("--pack-max-mib=", 0) == 0)
       ricepp_amd::set_facade_pack_limit(std::strtoull(argv[i] + 15, nullptr, 10) << 20);
@@ -538,8 +540,14 @@ int bench(int argc, char** argv) {
       for (auto& th : pool) th.join();
       return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     };
-    run(true);  // warm the contexts (both directions: decode grows their buffers differently)
-    run(false);
+    // warm the contexts (both directions: decode grows their buffers
+    // differently); twice, since batches fill differently from pass to pass
+    // and a context first reached by a later pass grows its pinned buffers
+    // then (each run reports contexts_created and buffer_grows)
+    for (int w = 0; w < 2; ++w) {
+      run(true);
+      run(false);
+    }
     for (int rep = 0; rep < repeat; ++rep) {
     if (trace) {
       ricepp_amd::set_facade_trace(true);
@@ -584,12 +592,15 @@ int bench(int argc, char** argv) {
                 "\"encode_GiBps\": %.3f, \"decode_GiBps\": %.3f, \"encode_launches\": %.0f, "
                 "\"decode_launches\": %.0f, \"encode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, "
                 "\"device_events\": %.1f, \"finish\": %.1f}, \"decode_us_per_batch\": {\"stage\": %.1f, \"device\": %.1f, "
-                "\"device_events\": %.1f, \"finish\": %.1f}, \"roundtrip_ok\": %s%s}\n",
+                "\"device_events\": %.1f, \"finish\": %.1f}, \"contexts_created\": %llu, \"buffer_grows\": %llu, "
+                "\"buffer_grow_ms\": %.2f, \"roundtrip_ok\": %s%s}\n",
                 T, depth, blocks, n * 2, gib / te, gib / td, ne, nd, (s1.stage_ns - s0.stage_ns) / 1e3 / ne,
                 (s1.device_ns - s0.device_ns) / 1e3 / ne, (s1.device_event_ns - s0.device_event_ns) / 1e3 / ne,
                 (s1.finish_ns - s0.finish_ns) / 1e3 / ne, (s2.stage_ns - s1.stage_ns) / 1e3 / nd,
                 (s2.device_ns - s1.device_ns) / 1e3 / nd, (s2.device_event_ns - s1.device_event_ns) / 1e3 / nd,
-                (s2.finish_ns - s1.finish_ns) / 1e3 / nd, ok ? "true" : "false", trace_json.c_str());
+                (s2.finish_ns - s1.finish_ns) / 1e3 / nd, (unsigned long long)(s2.contexts_created - s0.contexts_created),
+                (unsigned long long)(s2.buffer_grows - s0.buffer_grows), (s2.buffer_grow_ns - s0.buffer_grow_ns) / 1e6,
+                ok ? "true" : "false", trace_json.c_str());
     std::fflush(stdout);
     if (!ok) return 1;
     }
