@@ -69,7 +69,8 @@ struct Workspace {
   uint32_t* tile_lt;    // [max_tiles] its index within the stream
   uint64_t* lvl_cnt;    // [levels + 1] streams with more than l tiles
   uint64_t* lvl_base;   // [levels + 1]
-  uint32_t* sb_pos;     // [max_sb + B]
+  uint32_t* sb_pos;     // [max_sb + B] bit positions from the stream's 4-aligned base, low 32 bits
+  uint32_t* tile_hi;    // [max_tiles] high 32 bits of the position of each tile's first sub-block
   uint32_t* counter;    // [1]
   // segmented decode (L != 0)
   uint64_t* ucnt;       // [B + 1] units per stream
@@ -88,7 +89,7 @@ struct Workspace {
   uint32_t* queue;      // [1]
   uint64_t* cnt2;       // [U_max + 1] exact positions per unit
   uint64_t* off2;       // [U_max + 1]
-  uint32_t* guard;      // [1] 1: the batch exceeds the promised sizes (rpp_seg_plan_kernel)
+  uint32_t* guard;      // [2] 1: the batch exceeds the promised sizes (rpp_seg_plan_kernel); the stage choice
   uint64_t bytes;
   uint64_t max_tiles;
   uint64_t units_max;
@@ -132,6 +133,7 @@ Workspace layout(const rpp_config* cfg, uint64_t total_samples, uint64_t max_str
   w.lvl_cnt = reinterpret_cast<uint64_t*>(take(((uint64_t)w.levels + 1) * 8));
   w.lvl_base = reinterpret_cast<uint64_t*>(take(((uint64_t)w.levels + 1) * 8));
   w.sb_pos = reinterpret_cast<uint32_t*>(take((max_sb + B) * 4));
+  w.tile_hi = reinterpret_cast<uint32_t*>(take(max_tiles * 4));
   w.counter = reinterpret_cast<uint32_t*>(take(256));
   w.guard = reinterpret_cast<uint32_t*>(take(256));
   w.max_tiles = max_tiles;
@@ -213,6 +215,7 @@ struct ExtractParams {
   const uint64_t* out_off;
   int32_t* status;        // of the parse pass: streams that failed are skipped; RPP_INTERNAL_ERROR on a stalled look-back
   const uint32_t* sb_pos;
+  const uint32_t* tile_hi;
   const uint64_t* sb_base;
   const uint64_t* tile_base;
   const uint32_t* tile_map;
@@ -223,6 +226,9 @@ struct ExtractParams {
   uint32_t nblocks;
   uint32_t bs, be, ulsb;
   uint32_t dbg;  // rpp_decode_options::test_flags (RPP_TEST_*)
+  // (batches of many tiles: both stage sizes are launched, and the one
+  // rpp_seg_plan_kernel did not choose returns at once; nullptr: run)
+  const uint32_t* stage_sel;
 };
 
 // pixel traits (ricepp/ricepp_cpuspecific_traits.h:63-75)
@@ -366,6 +372,7 @@ __global__ __launch_bounds__(kTile, STAGE == kStageWords ? 2 : 3) void rpp_extra
   const uint32_t selbe = be ? 0x02030001u : 0x03020100u;  // byte-swap each half
   const uint32_t chunk_len = CS * (BS ? BS : p.bs);
   const uint64_t total_tiles = *p.n_tiles;
+  if (p.stage_sel && *p.stage_sel != (STAGE == kStageWords ? 1u : 0u)) return;  // (uniform)
 
   const bool timing = (p.dbg & RPP_TEST_PHASE_TIMERS) && tid < 64;
   // fault injection: tile 1 of every stream never publishes, its successors
@@ -403,10 +410,19 @@ __global__ __launch_bounds__(kTile, STAGE == kStageWords ? 2 : 3) void rpp_extra
     const uint32_t k0 = lt * kTile;
     const uint32_t kcount = min(kTile, nsb - k0);
     const uint32_t* pos_tab = p.sb_pos + p.sb_base[b];
+    // the tile's frame: its words from the one holding its first sub-block's
+    // header (sb_pos holds the positions' low 32 bits, tile_hi the high bits
+    // of the tile's first one; a tile spans a few Mbit at most, so the
+    // positions relative to it are the low bits' differences)
+    const uint64_t wt = ((uint64_t)p.tile_hi[t] << 27) | (pos_tab[k0] >> 5);
+    const uint32_t fbit = 32u * (uint32_t)wt;  // (the frame's first bit, mod 2^32)
+    const uint8_t* tbase = base + 4 * wt;
+    const uint32_t tbytes =
+        nbytes > 4 * wt ? (uint32_t)min<uint64_t>(nbytes - 4 * wt, rpp_internal::kSegWinBytes) : 0u;
     const uint32_t k = k0 + tid;
     const bool active = tid < kcount;
-    const uint32_t start = active ? pos_tab[k] : 0u;
-    const uint32_t end = active ? pos_tab[k + 1] : 0u;
+    const uint32_t start = active ? pos_tab[k] - fbit : 0u;
+    const uint32_t end = active ? pos_tab[k + 1] - fbit : 0u;
     const uint32_t comp = k % CS;
     const uint32_t cbase = (k / CS) * chunk_len;
     const uint32_t n = active ? min(N - cbase, chunk_len) / CS : 0u;
@@ -417,24 +433,24 @@ __global__ __launch_bounds__(kTile, STAGE == kStageWords ? 2 : 3) void rpp_extra
     //      registers held: every wave issues its 256-byte chunks back to
     //      back), the chunk holding the stream's end word by word (zero past
     //      the last byte) ----
-    const uint32_t w0 = pos_tab[k0] >> 5;
-    const uint32_t wend = (pos_tab[k0 + kcount] >> 5) + 2;
+    const uint32_t w0 = 0;
+    const uint32_t wend = ((pos_tab[k0 + kcount] - fbit) >> 5) + 2;
     const uint32_t nst = min(wend - w0, STAGE);
     {
       const uint32_t l = tid & 63u, wv = tid >> 6;
       for (uint32_t c = wv; 64 * c < nst; c += kTile / 64) {
         const uint32_t wq = w0 + 64 * c;
-        if (4 * (wq + 64) <= nbytes) {
-          glds4(base + 4 * (wq + l), __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&stage[64 * c]));
+        if (4 * (wq + 64) <= tbytes) {
+          glds4(tbase + 4 * (wq + l), __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&stage[64 * c]));
         } else {
-          stage[64 * c + l] = stream_word(base, nbytes, wq + l);
+          stage[64 * c + l] = stream_word(tbase, tbytes, wq + l);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     stamp(1);
-    const Reader rd{stage, w0, nst, base, nbytes};
+    const Reader rd{stage, w0, nst, tbase, tbytes};
 
     // ---- fast lanes: Rice, a full sub-block, staged, every code <= 32 bits ----
     uint32_t hdr = 0;
@@ -663,6 +679,8 @@ struct SegArgs {
   const uint64_t* n_samples;
   const uint64_t* sb_base;
   uint32_t* sb_pos;
+  uint32_t* tile_hi;     // (the sb_pos entries of tile starts also write their high bits here)
+  const uint64_t* tile_base;
   int32_t* status;
   uint64_t* cnt;  // [U_max + 1] exact positions per unit
   uint64_t* off;  // [U_max + 1] their exclusive scan
@@ -697,16 +715,17 @@ __global__ void rpp_seg_map_kernel(SegArgs a, uint32_t* unit_map, uint64_t* pl_c
   uint64_t cap = 0;
   if (nu > 1) {
     const uint32_t L = a.sv.seg_log2;
-    const uint32_t Eend =
+    const uint64_t Eend =
         rpp_internal::seg_last_bit((uint32_t)(a.in_off[i] & 3u), a.in_bytes[i], a.n_samples[i], a.bs, a.cs);
-    const uint64_t S = k << L, E = k + 1 == nu ? (uint64_t)Eend + 1 : S + (1ull << L);
+    const uint64_t S = k << L, E = k + 1 == nu ? Eend + 1 : S + (1ull << L);
     cap = align_up((E - S) / max(a.bs, 32u) + 64, 4);
   }
   pl_cnt[u] = cap;
 }
 
 struct UnitGeo {
-  uint32_t b, u0, nu, S, E;
+  uint32_t b, u0, nu;
+  uint64_t S, E;  // the unit's region [S, E) of the stream (bits from its 4-aligned base)
 };
 __device__ __forceinline__ UnitGeo unit_geo(const SegArgs& a, uint32_t u) {
   UnitGeo g;
@@ -714,8 +733,8 @@ __device__ __forceinline__ UnitGeo unit_geo(const SegArgs& a, uint32_t u) {
   g.u0 = (uint32_t)a.sv.unit_base[g.b];
   g.nu = (uint32_t)a.sv.unit_base[g.b + 1] - g.u0;
   const uint32_t j = u - g.u0, L = a.sv.seg_log2;
-  g.S = j << L;
-  g.E = g.S + (1u << L);
+  g.S = (uint64_t)j << L;
+  g.E = g.S + (1ull << L);
   if (g.nu > 1 && j + 1 == g.nu)
     g.E = rpp_internal::seg_last_bit((uint32_t)(a.in_off[g.b] & 3u), a.in_bytes[g.b], a.n_samples[g.b], a.bs, a.cs) + 1;
   return g;
@@ -889,7 +908,9 @@ __global__ void rpp_seg_count_kernel(SegArgs a) {
 }
 
 // each unit's exact positions into the stream's sb_pos: its list from ulo,
-// then its own overshoot entries; entries past the stream's nsb + 1 dropped
+// then its own overshoot entries; entries past the stream's nsb + 1 dropped.
+// (list entries are relative to the unit's first bit S, overshoot entries to
+// the next unit's, E: ricepp_internal.h)
 __global__ __launch_bounds__(kSegThreads) void rpp_seg_write_kernel(SegArgs a) {
   const uint32_t u = blockIdx.x, tid = threadIdx.x;
   if (u >= (uint32_t)a.sv.unit_base[a.nblocks]) return;
@@ -901,15 +922,20 @@ __global__ __launch_bounds__(kSegThreads) void rpp_seg_write_kernel(SegArgs a) {
   const uint32_t chunk_len = a.bs * a.cs;
   const uint64_t cap = (N + chunk_len - 1) / chunk_len * a.cs + 1;
   uint32_t* dst = a.sb_pos + a.sb_base[g.b];
+  uint32_t* hi = a.tile_hi + a.tile_base[g.b];
   const uint64_t idx0 = a.off[u] - a.off[g.u0];
   const uint32_t n = us_word(a, u, rpp_internal::kUsNpos);
   const uint32_t nl = n > lo ? n - lo : 0u;
   const uint32_t* l = a.sv.plist + a.sv.pl_base[u] + lo;
+  auto put = [&](uint64_t e, uint64_t pos) {
+    dst[e] = (uint32_t)pos;
+    if (e % kTile == 0 && e + 1 < cap) hi[e / kTile] = (uint32_t)(pos >> 32);  // (a tile's first sub-block)
+  };
   for (uint32_t i = tid; i < nl; i += kSegThreads)
-    if (idx0 + i < cap) dst[idx0 + i] = l[i];
+    if (idx0 + i < cap) put(idx0 + i, g.S + l[i]);
   const uint32_t nov = a.sv.uov[u];
   for (uint32_t i = tid; i < nov; i += kSegThreads)
-    if (idx0 + nl + i < cap) dst[idx0 + nl + i] = a.sv.ovr[kSegOvr * u + i];
+    if (idx0 + nl + i < cap) put(idx0 + nl + i, g.E + a.sv.ovr[kSegOvr * u + i]);
 }
 
 // One sub-block of n samples from bit `pos` (decode.h:42-83, positions only);
@@ -963,15 +989,27 @@ __global__ void rpp_seg_tail_kernel(SegArgs a) {
     st = (a.sv.sflags[b] & kSfPastRegion) ? kSegFallback : RPP_TRUNCATED_INPUT;
     if (st == kSegFallback) atomicAdd(&g_seg_diag[3], 1ull);
   } else if (rag) {
+    // (in the frame of the word holding the chunk's first header)
     const uint64_t ioff = a.in_off[b];
     const uint32_t mis = (uint32_t)(ioff & 3u);
-    const uint32_t nbytes = (uint32_t)a.in_bytes[b] + mis;
     uint32_t* dst = a.sb_pos + a.sb_base[b];
-    const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
-    uint32_t pos = dst[nsb - cs];
+    uint32_t* hi = a.tile_hi + a.tile_base[b];
+    // the 64-bit position of the last chunk's first header: its low bits
+    // against its tile's first entry
+    const uint32_t e0 = nsb - cs, f0 = e0 / kTile * kTile;
+    const uint64_t ref = ((uint64_t)hi[e0 / kTile] << 32) | dst[f0];
+    const uint64_t wt = (ref + (uint32_t)(dst[e0] - (uint32_t)ref)) >> 5;
+    const uint64_t nbytes64 = a.in_bytes[b] + mis, lim64 = rpp_internal::seg_read_limit(mis, a.in_bytes[b]);
+    const uint32_t nbytes = nbytes64 > 4 * wt ? (uint32_t)min<uint64_t>(nbytes64 - 4 * wt, rpp_internal::kSegWinBytes) : 0u;
+    const uint32_t lim = lim64 > 32 * wt ? (uint32_t)min<uint64_t>(lim64 - 32 * wt, rpp_internal::kSegWinBits) : 0u;
+    uint32_t pos = (uint32_t)(dst[nsb - cs] & 31u);
     for (uint32_t c = 0; c < cs && st == RPP_OK; ++c) {
-      if (!seg_parse_one(a.in + (ioff - mis), nbytes, lim, pos, rag / cs)) st = RPP_TRUNCATED_INPUT;
-      else dst[nsb - cs + 1 + c] = pos;
+      if (!seg_parse_one(a.in + (ioff - mis) + 4 * wt, nbytes, lim, pos, rag / cs)) st = RPP_TRUNCATED_INPUT;
+      else {
+        const uint32_t e = nsb - cs + 1 + c;
+        dst[e] = (uint32_t)(32 * wt + pos);
+        if (e % kTile == 0 && e < nsb) hi[e / kTile] = (uint32_t)((32 * wt + pos) >> 32);
+      }
     }
   }
   a.status[b] = st;
@@ -1174,7 +1212,7 @@ __global__ __launch_bounds__(kPlanThreads) void rpp_seg_plan_kernel(PlanArgs q) 
   using namespace rpp_internal;
   __shared__ uint64_t sh[kPlanThreads / 64 + 1];
   __shared__ uint32_t bad;
-  __shared__ unsigned long long sum;
+  __shared__ unsigned long long sum, sbits, stiles;
   const SegArgs& a = q.a;
   const uint32_t t = threadIdx.x, B = a.nblocks;
   const uint64_t U = a.sv.units_max;
@@ -1195,6 +1233,8 @@ __global__ __launch_bounds__(kPlanThreads) void rpp_seg_plan_kernel(PlanArgs q) 
     *a.sv.queue = 0;
     bad = 0;
     sum = 0;
+    sbits = 0;
+    stiles = 0;
   }
   __syncthreads();
   // the batch against the workspace's promise (rpp_decode_workspace_bytes):
@@ -1212,6 +1252,7 @@ __global__ __launch_bounds__(kPlanThreads) void rpp_seg_plan_kernel(PlanArgs q) 
   if (t == 0) *q.guard = guard ? 1u : 0u;
   // units (one per 2^L bits of a stream's header range, 1 for short or
   // undecodable streams), sub-blocks + 1 and tiles of the split streams
+  unsigned long long pbits = 0, ptiles = 0;
   for (uint32_t i = t; i <= B; i += kPlanThreads) {
     uint64_t c = 0, nsb = 0;
     if (i < B) {
@@ -1219,12 +1260,18 @@ __global__ __launch_bounds__(kPlanThreads) void rpp_seg_plan_kernel(PlanArgs q) 
       c = 1;
       if (!guard && seg_stream_ok(n, nb, a.cs))
         c = (seg_last_bit((uint32_t)(a.in_off[i] & 3u), nb, n, a.bs, a.cs) >> a.sv.seg_log2) + 1;
-      if (!guard && c > 1) nsb = (n + q.chunk_len - 1) / q.chunk_len * a.cs;
+      if (!guard && c > 1) {
+        nsb = (n + q.chunk_len - 1) / q.chunk_len * a.cs;
+        pbits += 8 * nb;
+        ptiles += (nsb + kTile - 1) / kTile;
+      }
     }
     q.ucnt[i] = c;
     q.sb_cnt[i] = i < B ? nsb + 1 : 0;
     q.tile_cnt[i] = (nsb + kTile - 1) / kTile;
   }
+  atomicAdd(&sbits, pbits);
+  atomicAdd(&stiles, ptiles);
   // histogram of the tile counts (into lvl_base) for the levels
   for (uint32_t l = t; l <= q.levels; l += kPlanThreads) q.lvl_base[l] = 0;
   __syncthreads();
@@ -1232,6 +1279,12 @@ __global__ __launch_bounds__(kPlanThreads) void rpp_seg_plan_kernel(PlanArgs q) 
     atomicAdd(reinterpret_cast<unsigned long long*>(&q.lvl_base[(size_t)std::min<uint64_t>(q.tile_cnt[i], q.levels)]),
               1ull);
   __syncthreads();
+  // the extraction's stage: the 48 KiB one (three workgroups per CU) unless
+  // the split streams' tiles average more than 90 % of its bits (then many
+  // lanes would read past it: generator data at 14 bits per sample, one
+  // 2^29-sample stream, 11.8 -> 10.1 ms with 64 KiB; the configs[3] mix at
+  // ~8 bits per sample 5 % slower with it -- profiles/r06_giant_stage_ab.jsonl)
+  if (t == 0) q.guard[1] = sbits * 10 > stiles * 9 * 32 * kStageWordsMany ? 1u : 0u;
   plan_exscan(q.ucnt, (uint64_t)B + 1, const_cast<uint64_t*>(a.sv.unit_base), sh);
   plan_exscan(q.sb_cnt, (uint64_t)B + 1, const_cast<uint64_t*>(a.sb_base), sh);
   plan_exscan(q.tile_cnt, (uint64_t)B + 1, q.tile_base, sh);
@@ -1322,6 +1375,8 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
   a.n_samples = d_n_samples;
   a.sb_base = w.sb_base;
   a.sb_pos = w.sb_pos;
+  a.tile_hi = w.tile_hi;
+  a.tile_base = w.tile_base;
   a.status = d_status;
   a.cnt = w.cnt2;
   a.off = w.off2;
@@ -1369,13 +1424,17 @@ int rpp_decode_batch_ex(const rpp_config* cfg, const uint8_t* d_in, const uint64
   hipLaunchKernelGGL(rpp_seg_tail_kernel, dim3(g256), dim3(256), 0, s, a);
   // (a batch of more tiles than the grid holds: the smaller stage, three
   // workgroups per CU)
-  const ExtractKernel k = w.max_tiles >= kMaxExtractGrid ? extract_kernel<kStageWordsMany>(cfg)
-                                                         : extract_kernel<kStageWords>(cfg);
-  ExtractParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_out, d_out_offsets, d_status, w.sb_pos, w.sb_base,
+  // (a batch that can have more tiles than the grid holds: both stages, the
+  // plan kernel's choice by density runs; fewer: the 64 KiB stage)
+  const bool many = w.max_tiles >= kMaxExtractGrid;
+  ExtractParams p{d_in, d_in_offsets, d_in_bytes, d_n_samples, d_out, d_out_offsets, d_status, w.sb_pos, w.tile_hi,
+                  w.sb_base,
                   w.tile_base, w.tile_map, w.tile_lt, w.lvl_base + w.levels, w.tile_state, w.counter, nblocks,
-                  cfg->block_size, cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count, test};
+                  cfg->block_size, cfg->big_endian ? 1u : 0u, cfg->unused_lsb_count, test,
+                  many ? w.guard + 1 : nullptr};
   const uint32_t grid = (uint32_t)std::min<uint64_t>(w.max_tiles, kMaxExtractGrid);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kTile), 0, s, p);
+  hipLaunchKernelGGL(extract_kernel<kStageWords>(cfg), dim3(grid), dim3(kTile), 0, s, p);
+  if (many) hipLaunchKernelGGL(extract_kernel<kStageWordsMany>(cfg), dim3(grid), dim3(kTile), 0, s, p);
   if (hipGetLastError() != hipSuccess) return RPP_HIP_ERROR;
   // join the side stream, then the streams whose exact chain left the region
   // the units cover or whose lists overflowed (the fused kernel)

@@ -26,13 +26,26 @@ namespace rpp_internal {
 // keep 32-bit bit positions for any data: streams below 2^27 samples (longer
 // ones are encoded in segments, decoded by the other kernels).
 constexpr uint64_t kSegMaxSamples = UINT64_C(1) << 27;
-// The segmented decode's unit, overshoot and sub-block positions are 32-bit
-// bit positions from the stream's 4-aligned base: it takes streams of any
-// sample count whose bytes stay below 2^29 minus room for a window's reads
-// past the end (round 5; before, streams below 2^27 samples only).  Longer
-// streams (compressed past 512 MiB) are decoded one wave each by the fused
-// kernel, which rebases its positions as it goes.
-constexpr uint64_t kSegMaxBytes = (UINT64_C(1) << 29) - (UINT64_C(1) << 16);
+// The segmented decode's positions (round 6): a unit's parse works in a
+// frame that starts at its unit's first bit S = j 2^L (its wave reads the
+// stream from byte S / 8 on), and every position a unit leaves behind is
+// stored relative to the S of the unit it belongs to -- list entries and the
+// start / rerun / guess words to the unit's own, overshoot entries to the
+// next unit's (so that the stitch compares them with that unit's list as
+// they are) -- which keeps them far below 2^32 and the sentinels below.  The
+// sub-block start list the extraction reads (sb_pos) holds the low 32 bits of
+// the positions from the stream's 4-aligned base, and a per-tile word the
+// high bits of the tile's first position (a tile spans a few Mbit at most).  Before round 6 all of them were 32-bit
+// positions from the stream's base, which limited the segmented decode to
+// streams compressed below 2^29 bytes; now any stream below
+// RPP_MAX_STREAM_SAMPLES whose byte count fits 32 bits takes it.  A wave's
+// frame is at most kSegWinBits long: a serial pass (which parses from one
+// unit to the stream's end) that would leave it hands the stream to the
+// fused kernel, which rebases its positions as it goes.
+constexpr uint64_t kSegMaxBytes = (UINT64_C(1) << 32) - (UINT64_C(1) << 16);
+constexpr uint32_t kSegWinBytes = UINT32_C(1) << 28;
+constexpr uint32_t kSegWinBits = 8u * kSegWinBytes;         // 2^31
+constexpr uint32_t kSegSerialEnd = kSegWinBits - (1u << 24);  // a serial pass's region ends here at the latest
 __host__ __device__ inline bool seg_stream_fits(uint64_t n, uint64_t nb, uint32_t cs) {
   return n % cs == 0 && n < RPP_MAX_STREAM_SAMPLES && nb < kSegMaxBytes;
 }
@@ -74,13 +87,19 @@ struct SegView {
 // Last bit position a header (or the end) of a well-formed stream can take,
 // relative to the 4-aligned base (bit 0 at 8 * mis): the stream's bytes,
 // clamped to rpp_worst_case_bytes of its sample count (codec.h:45-55 bound).
-__host__ __device__ inline uint32_t seg_last_bit(uint32_t mis, uint64_t in_bytes, uint64_t n, uint32_t bs,
+__host__ __device__ inline uint64_t seg_last_bit(uint32_t mis, uint64_t in_bytes, uint64_t n, uint32_t bs,
                                                   uint32_t cs) {
   const uint64_t per = n / cs;
   const uint64_t num = 16 + 4 * ((per + bs - 1) / bs) + 16 * per;
   const uint64_t wc = (num * cs + 7) / 8;
   const uint64_t nb = in_bytes < wc ? in_bytes : wc;
-  return (uint32_t)(8u * mis + 8u * nb);
+  return 8ull * mis + 8ull * nb;
+}
+
+// a stream's last readable bit + 1 from its 4-aligned base: the reader pulls
+// whole 8-byte packets (bitstream_reader.h:149-183), zero past its last byte
+__host__ __device__ inline uint64_t seg_read_limit(uint32_t mis, uint64_t in_bytes) {
+  return 8ull * mis + 64ull * ((in_bytes + 7) >> 3);
 }
 
 // rpp_decode_kernel: one wave per stream, parse and values fused (any bs).

@@ -2698,8 +2698,14 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
     const bool multi = SEG && nunits > 1;
 
     // ---- per-stream setup (wave-uniform) ----
+    // SEG: the wave works in its unit's frame (ricepp_internal.h): bit 0 is
+    // the unit's first bit S_abs = ju 2^L of the stream, the stream is read
+    // from byte S_abs / 8 on (a multiple of 128: alignment kept), and the
+    // positions it stores are relative to the unit they belong to
+    const uint32_t L = p.sv.seg_log2;
     int32_t status = RPP_OK;
-    uint32_t N = 0, nbytes = 0, mis = 0;
+    uint32_t N = 0, nbytes = 0, mis = 0, lim = 0;
+    uint64_t Eend64 = 0;
     const uint8_t* in = p.in;
     {
       const uint64_t n64 = p.n_samples[b];
@@ -2710,29 +2716,32 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       } else {
         N = (uint32_t)n64;
         mis = (uint32_t)(ioff & 3u);
-        nbytes = (uint32_t)nb64 + mis;  // bytes from the aligned base
         in = p.in + (ioff - mis);
+        // last readable bit + 1 (seg_read_limit), bytes from the aligned base
+        const uint64_t lim64 = seg_read_limit(mis, nb64), nbytes64 = nb64 + mis;
+        const uint64_t sabs = multi ? (uint64_t)ju << L : 0u;
+        in += sabs >> 3;
+        nbytes = nbytes64 > (sabs >> 3) ? (uint32_t)min<uint64_t>(nbytes64 - (sabs >> 3), kSegWinBytes) : 0u;
+        lim = lim64 > sabs ? (uint32_t)min<uint64_t>(lim64 - sabs, kSegWinBits) : 0u;
+        if (multi) Eend64 = seg_last_bit(mis, nb64, N, bs, CS) - sabs;
       }
     }
     uint32_t* const pos_out = multi ? nullptr : p.sb_pos + p.sb_base[b];
     const bool aligned16 = ((uintptr_t)in & 15u) == 0;
-    // last readable bit + 1: the reader pulls whole 8-byte packets of the
-    // stream (bitstream_reader.h:149-183), zero past its last byte
-    const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
     const uint32_t chunk_len = CS * bs;
     const uint32_t nchunks = status == RPP_OK ? (N + chunk_len - 1) / chunk_len : 0u;
 
-    // ---- SEG: the unit's region [S, E) of header positions ----
-    const uint32_t L = p.sv.seg_log2;
+    // ---- SEG: the unit's region [S, E) of header positions (frame: S = 0) ----
     const bool serial = multi && p.sv.pass == 2;
-    uint32_t S = 0, E = 0, Eend = 0;
+    uint32_t S = 0, E = 0;
     bool last = false;
     if (multi) {
-      Eend = seg_last_bit(mis, nbytes - mis, N, bs, CS);
-      S = ju << L;
       last = ju + 1 == nunits;
-      E = last ? Eend + 1 : S + (1u << L);
-      if (serial) E = Eend + 1;
+      E = last ? (uint32_t)(Eend64 + 1) : 1u << L;
+      // (a serial pass parses to the stream's end: one that would leave the
+      // frame stops at kSegSerialEnd, past its region, and the fused kernel
+      // takes the stream)
+      if (serial) E = (uint32_t)min<uint64_t>(Eend64 + 1, kSegSerialEnd);
     }
 
     // ---- SEG: the first header of the unit ----
@@ -2864,6 +2873,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
       uint32_t novr = 0;
       bool stop = false;
       uint32_t lk = ju;  // (SEG) the unit whose list is being written
+      uint32_t loff = 0;  // (SEG) its first bit in the wave's frame: list entries are relative to it
       uint64_t lbase = multi ? p.sv.pl_base[u] : 0;
       uint32_t lcap = multi ? (uint32_t)(p.sv.pl_base[u + 1] - lbase) : 0;
       auto flush = [&]() {
@@ -2872,7 +2882,7 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
             stop = true;
             if (lane == 0) atomicOr(p.sv.sflags + b, kSfListFull);
           } else if (lane < pcnt) {
-            p.sv.plist[lbase + pstart + lane] = pbuf;
+            p.sv.plist[lbase + pstart + lane] = pbuf - loff;
           }
         } else {
           if (lane < pcnt) pos_out[pstart + lane] = pbuf;
@@ -2889,15 +2899,17 @@ __global__ __launch_bounds__(kWave* kDecMaxWaves) void rpp_parse_kernel(ParsePar
             stop = true;
             if (lane == 0) atomicOr(p.sv.sflags + b, kSfPastRegion);
           } else {
-            if (lane == 0 && novr < kSegOvr) p.sv.ovr[kSegOvr * u + novr] = pos;
+            // (relative to the next unit's first bit, E)
+            if (lane == 0 && novr < kSegOvr) p.sv.ovr[kSegOvr * u + novr] = pos - E;
             if (++novr >= kSegOvr) stop = true;
           }
           return;
         }
-        if (serial && (pos >> L) != lk) {  // into the next unit's region
+        if (serial && (pos >> L) != lk - ju) {  // into the next unit's region
           flush();
           close_list();
-          lk = pos >> L;
+          lk = ju + (pos >> L);
+          loff = (pos >> L) << L;
           lbase = p.sv.pl_base[u0 + lk];
           lcap = (uint32_t)(p.sv.pl_base[u0 + lk + 1] - lbase);
           pstart = 0;
@@ -3271,12 +3283,16 @@ __global__ __launch_bounds__(kWave* kGuessWaves) void rpp_seg_guess_kernel(Parse
   const uint32_t stage_w = p.wave_words - (kListLead + kListWords);
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm) + kTabBytes / 4;
   uint32_t* list = ring + stage_w + wv * kGuessListWords;
+  // the unit's frame (as in rpp_parse_kernel): bit 0 at its first bit
   const uint32_t mis = (uint32_t)(ioff & 3u);
-  const uint32_t nbytes = (uint32_t)nb64 + mis;
-  const uint8_t* in = p.in + (ioff - mis);
-  const uint32_t lim = 8u * mis + 64u * ((nbytes - mis + 7u) >> 3);
-  const uint32_t S = ju << p.sv.seg_log2;
-  const uint32_t w0 = S >> 5;
+  const uint64_t sabs = (uint64_t)ju << p.sv.seg_log2;
+  const uint64_t lim64 = seg_read_limit(mis, nb64), nbytes64 = nb64 + mis;
+  const uint32_t nbytes =
+      nbytes64 > (sabs >> 3) ? (uint32_t)min<uint64_t>(nbytes64 - (sabs >> 3), kSegWinBytes) : 0u;
+  const uint8_t* in = p.in + (ioff - mis) + (sabs >> 3);
+  const uint32_t lim = lim64 > sabs ? (uint32_t)min<uint64_t>(lim64 - sabs, kSegWinBits) : 0u;
+  const uint32_t S = 0;
+  const uint32_t w0 = 0;
   for (uint32_t i = threadIdx.x; i < stage_w; i += blockDim.x) ring[i] = stream_word(in, nbytes, w0 + i);
   __syncthreads();
   const uint32_t end_rel = S < lim ? min(32u * stage_w - 64u, lim - S) : 0u;
@@ -3469,7 +3485,10 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
 
 // (below this many units the parse's work queue leaves wave slots idle: each
 // unit's guess gets kGuessWaves waves of its own)
-constexpr uint32_t kGuessKernelMaxUnits = 2048;
+// (8192 since round 6: one 2^29-sample generator stream, 7343 units of
+// 2^20 bits, 10.1 -> 9.8 ms; the configs[3] mix unchanged --
+// profiles/r06_giant_stage_ab.jsonl)
+constexpr uint32_t kGuessKernelMaxUnits = 8192;
 int launch_seg_guess(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples, const SegView& sv,
                      hipStream_t stream) {

@@ -632,15 +632,20 @@ def _chunked(gen, rng, n, parts=16, **kw):
 
 def test_stream_of_2_29_samples_past_2_32_bits():
     """one stream of 2**29 + 3 samples of the benchmark generator (~14 bits per sample, 7.5e9
-    bits: past 2**32, with the segmented encode's 64-bit unit offsets near their largest and the fused
-    decode rebasing its 32-bit positions seven times; past the segmented decode's 2**29-byte range, so decoded
-    by the fused kernel), encoded byte for byte as the oracle and decoded back."""
+    bits: past 2**32, with the segmented encode's 64-bit unit offsets near their largest), encoded byte for
+    byte as the oracle and decoded back by the default path -- since round 6 the segmented decode, whose
+    units work in frames of their own and whose sub-block positions are 64-bit (checked to have run: units
+    met, no stream handed to the fused kernel) -- and by the fused kernel, which rebases its 32-bit
+    positions seven times."""
     rng = np.random.default_rng(2929)
     n = (1 << 29) + 3
     big = _chunked(datagen.benchmark_data, rng, n)
     cfg = codec.CodecConfig(128, 1, "big", 0)
-    wants = run_batch(cfg, [big])
+    codec.segmented_decode_stats(reset=True)
+    wants = run_batch(cfg, [big], dec=[None, FUSED])
+    st = codec.segmented_decode_stats(reset=True)
     assert 8 * len(wants[0]) > (1 << 32)
+    assert st["met"] > 0 and st["fallback"] == 0, st
 
 
 @pytest.mark.parametrize("bs", [17, 99, 200, 256, 512])

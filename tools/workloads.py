@@ -252,11 +252,14 @@ def case_e2e():
 
 def case_giant():
     """Streams of 2^27 samples and more (DwarFS -S 28..30 blocks): one stream each, decode by the default
-    path (segmented when the stream compresses below 2^29 bytes) against the fused kernel."""
+    path (segmented for any stream below 2^32 bytes since round 6; 2^29 bytes before) against the fused
+    kernel.  The last one, 2^29 + 3 generator samples, compresses to 7.5 Gbit (past 2^32 bits)."""
     cfg = codec.CodecConfig(128, 1, "big", 0)
     for label, n, make in (("2^27+5 generator (~14 bits/sample)", (1 << 27) + 5, lambda n: gen_benchmark(n, 7)),
                            ("2^28 Poisson(1000) (~7.7 bits/sample)", 1 << 28, lambda n: poisson_scaled(n, 1000.0, 0, 8)),
-                           ("2^29 Poisson(1000) (~7.7 bits/sample)", 1 << 29, lambda n: poisson_scaled(n, 1000.0, 0, 9))):
+                           ("2^29 Poisson(1000) (~7.7 bits/sample)", 1 << 29, lambda n: poisson_scaled(n, 1000.0, 0, 9)),
+                           ("2^29+3 generator (~14 bits/sample, 7.5 Gbit)", (1 << 29) + 3,
+                            lambda n: gen_benchmark(n, 11))):
         x = make(n)
         p = pipe_for(cfg, x, [n])
         raw = n * 2
