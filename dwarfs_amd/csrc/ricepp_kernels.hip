@@ -3485,10 +3485,11 @@ int launch_decode_fused(const rpp_config* cfg, const uint8_t* d_in, const uint64
 
 // (below this many units the parse's work queue leaves wave slots idle: each
 // unit's guess gets kGuessWaves waves of its own)
-// (8192 since round 6: one 2^29-sample generator stream, 7343 units of
-// 2^20 bits, 10.1 -> 9.8 ms; the configs[3] mix unchanged --
-// profiles/r06_giant_stage_ab.jsonl)
-constexpr uint32_t kGuessKernelMaxUnits = 8192;
+// (a bound on the batch's worst-case unit count.  Raised to 16384 / 65536 in
+// round 6, the guess kernel made the 7.7 Gbit generator stream slower, 10.1 ->
+// 10.7 ms, with 1 rerun instead of 8, and the configs[3] mix 9 % slower:
+// profiles/r06_guess_bound_ab.jsonl)
+constexpr uint32_t kGuessKernelMaxUnits = 2048;
 int launch_seg_guess(const rpp_config* cfg, const uint8_t* d_in, const uint64_t* d_in_offsets,
                      const uint64_t* d_in_bytes, uint32_t nblocks, const uint64_t* d_n_samples, const SegView& sv,
                      hipStream_t stream) {
