@@ -1,7 +1,8 @@
 """Where the segmented parse spends its time: s_memtime cycles (shader clock) in the guess and in the unit
 chains, sub-blocks parsed, units -- for one 16 MiB Poisson stream and the block mix.
 
-usage: python tools/seg_parse_diag.py"""
+usage: python tools/seg_parse_diag.py            (16 MiB Poisson / generator streams, the 504 MiB mix)
+       python tools/seg_parse_diag.py giant      (one 2^29 + 3-sample generator stream, 7.7 Gbit)"""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -18,12 +19,13 @@ from dwarfs_amd import codec  # noqa: E402
 MIB = 1 << 20
 
 
-def run(name, blocks):
+def run(name, blocks, x=None):
     cfg = codec.CodecConfig(128, 1, "big", 0)
     ns = [len(b) for b in blocks]
     offs = np.zeros(len(ns), np.int64)
     offs[1:] = np.cumsum(ns)[:-1]
-    x = torch.from_numpy(np.concatenate(blocks).view(np.int16)).cuda()
+    if x is None:
+        x = torch.from_numpy(np.concatenate(blocks).view(np.int16)).cuda()
     enc = codec.encode_batch(cfg, x, offs, ns)
     codec.decode_batch(cfg, enc.data, enc.offsets, enc.sizes, ns)
     torch.cuda.synchronize()
@@ -47,6 +49,13 @@ def run(name, blocks):
           f"{codec.segmented_decode_stats()}", flush=True)
 
 
+if sys.argv[1:] == ["giant"]:
+    sys.path.insert(0, str(ROOT / "tools"))
+    from workloads import gen_benchmark  # noqa: E402
+
+    n = (1 << 29) + 3
+    run("one 2^29+3 generator stream", [range(n)], x=gen_benchmark(n, 11))
+    sys.exit(0)
 rng = np.random.default_rng(3)
 run("one 16 MiB Poisson", [datagen.poisson_data(rng, 8 * MIB)])
 run("one 16 MiB generator", [datagen.benchmark_data(rng, 8 * MIB)])
