@@ -72,6 +72,8 @@ EXPORTED_SYMBOLS = (
     "rpp_flac_encode_batch",
     "rpp_flac_decode_workspace_bytes",
     "rpp_flac_decode",
+    "rpp_flac_decode_batch_workspace_bytes",
+    "rpp_flac_decode_batch",
 )
 
 
@@ -224,6 +226,10 @@ def lib() -> C.CDLL:
         L.rpp_flac_decode.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, P, P,
                                       C.c_uint32, P, C.c_uint64, P, P]
         L.rpp_flac_decode.restype = C.c_int
+        L.rpp_flac_decode_batch_workspace_bytes.argtypes = [C.c_uint32, P, P, P, P, P]
+        L.rpp_flac_decode_batch_workspace_bytes.restype = C.c_uint64
+        L.rpp_flac_decode_batch.argtypes = [P, C.c_uint32, P, P, P, P, P, P, P, P, P, P, P, C.c_uint64, P, P]
+        L.rpp_flac_decode_batch.restype = C.c_int
         if L.rpp_abi_version() != 1:
             raise RuntimeError("libricepp_amd.so ABI mismatch")
         _lib = L

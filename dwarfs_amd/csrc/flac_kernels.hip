@@ -764,18 +764,17 @@ __global__ void rpp_flac_block_off_kernel(const uint64_t* sizes, const uint64_t*
 // ---- CRC-16 of frames: per-lane chunks combined by GF(2) shifts ----
 // mode 0: write the CRC after [start, start + len); mode 1: compare with the
 // two bytes there and set ok[f]
-__global__ __launch_bounds__(64) void rpp_flac_crc_kernel(const uint8_t* buf, const uint64_t* starts,
-                                                        const uint64_t* lens, uint32_t frames, uint8_t* wbuf,
-                                                        uint32_t* ok, const uint32_t* count) {
-  __shared__ uint16_t tab[256];
-  const uint32_t lane = lane_id();
-  for (uint32_t i = lane; i < 256; i += kWave) {
+__device__ __forceinline__ void crc16_table(uint16_t* tab) {
+  for (uint32_t i = lane_id(); i < 256; i += kWave) {
     uint16_t d = (uint16_t)(i << 8);
     for (int k = 0; k < 8; ++k) d = (uint16_t)((d & 0x8000) ? (d << 1) ^ 0x8005 : d << 1);
     tab[i] = d;
   }
   __syncthreads();
-  const uint32_t nf = count ? min(*count, frames) : frames;
+}
+__device__ void crc_frames(const uint16_t* tab, const uint8_t* buf, const uint64_t* starts, const uint64_t* lens,
+                           uint32_t nf, uint8_t* wbuf, uint32_t* ok) {
+  const uint32_t lane = lane_id();
   for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
     const uint64_t len = lens[f];
     if (len == ~0ull) continue;  // (decode: a candidate that did not parse)
@@ -798,6 +797,13 @@ __global__ __launch_bounds__(64) void rpp_flac_crc_kernel(const uint8_t* buf, co
     }
   }
 }
+__global__ __launch_bounds__(64) void rpp_flac_crc_kernel(const uint8_t* buf, const uint64_t* starts,
+                                                        const uint64_t* lens, uint32_t frames, uint8_t* wbuf,
+                                                        uint32_t* ok, const uint32_t* count) {
+  __shared__ uint16_t tab[256];
+  crc16_table(tab);
+  crc_frames(tab, buf, starts, lens, count ? min(*count, frames) : frames, wbuf, ok);
+}
 
 // ---- decode ----
 struct FlacDecParams {
@@ -811,7 +817,9 @@ struct FlacDecParams {
   uint64_t* cand_len;  // [max_cand] bytes before the CRC-16 (~0: did not parse)
   uint32_t* cand_ok;   // [max_cand] CRC-16 matches
   uint32_t* cand_redo; // [max_cand] left to the lane decoder by the wave decoder
-  uint32_t redo_only;  // lane decoder: only the candidates marked in cand_redo
+  uint32_t redo_only;  // lane decoder: only the candidates marked in cand_redo (the wave decoder ran)
+  uint32_t use_wave;   // the wave decoder takes this stream's frames (they fit its LDS)
+  uint32_t wide;       // 32-bit samples: int64 scratch, the lane decoder's int64 instance
   uint32_t* ncand;     // candidates found
   uint32_t max_cand;
   void* scratch;       // [max_cand][channels][max_bs] int32 (int64 for 32-bit samples)
@@ -942,7 +950,10 @@ __device__ uint32_t parse_header(const uint8_t* in, uint64_t nbytes, uint64_t p,
   return (uint32_t)(q + 1 - p);
 }
 
-__global__ __launch_bounds__(256) void rpp_flac_scan_kernel(FlacDecParams d) {
+// (every decode kernel takes the batch's table of streams, one FlacDecParams
+// per stream in device memory, and works on stream blockIdx.y)
+__global__ __launch_bounds__(256) void rpp_flac_scan_kernel(const FlacDecParams* tab) {
+  const FlacDecParams& d = tab[blockIdx.y];
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= d.nbytes) return;
   uint32_t at = 0;
@@ -1090,10 +1101,12 @@ __device__ __forceinline__ bool decode_subframe(BitReader& r, T* dst, uint32_t b
 // channel has 33 bits); cand_len = bytes before the CRC-16.  Inter-channel
 // decorrelation and interleaving are left to rpp_flac_place_kernel.
 template <class T>
-__global__ __launch_bounds__(64) void rpp_flac_frame_kernel(FlacDecParams d) {
+__global__ __launch_bounds__(64) void rpp_flac_frame_kernel(const FlacDecParams* tab) {
   __shared__ int64_t rings[32][64];  // each lane's last 32 samples (LPC), lane-minor
   __shared__ int32_t coefs[32][64];  // each lane's LPC coefficients
   __shared__ T stage[64][64];        // each lane's next 64 output samples
+  const FlacDecParams& d = tab[blockIdx.y];
+  if ((d.wide != 0) != (sizeof(T) == 8)) return;  // (the other instance's streams)
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nc = min(*d.ncand, d.max_cand);
   if (c >= nc || (d.redo_only && !d.cand_redo[c])) return;
@@ -1473,10 +1486,12 @@ __device__ bool predict_column(int32_t* s, uint32_t bs, const SubInfo& inf) {
   return lpc_column<32>(s, bs, inf);
 }
 
-__global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(FlacDecParams d) {
+__global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(const FlacDecParams* tab) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ SubInfo info[8];
   __shared__ uint32_t wide;
+  const FlacDecParams& d = tab[blockIdx.y];
+  if (!d.use_wave) return;
   const uint32_t c = blockIdx.x, lane = threadIdx.x;
   const uint32_t nc = min(*d.ncand, d.max_cand);
   if (c >= nc) return;
@@ -1522,6 +1537,14 @@ __global__ __launch_bounds__(64) void rpp_flac_frame_wave_kernel(FlacDecParams d
 
 constexpr uint64_t kNoPlace = ~0ull;
 
+// CRC-16 check of every candidate that parsed, stream blockIdx.y of the table
+__global__ __launch_bounds__(64) void rpp_flac_dec_crc_kernel(const FlacDecParams* tab) {
+  __shared__ uint16_t t16[256];
+  crc16_table(t16);
+  const FlacDecParams& d = tab[blockIdx.y];
+  crc_frames(t16, d.in, d.cand_pos, d.cand_len, min(*d.ncand, d.max_cand), nullptr, d.cand_ok);
+}
+
 __device__ __forceinline__ bool cand_valid(const FlacDecParams& d, uint32_t c) {
   return d.cand_len[c] != ~0ull && d.cand_ok[c];
 }
@@ -1546,7 +1569,8 @@ __device__ __forceinline__ bool cand_first_sample(const FlacDecParams& d, uint32
 // byte 0 starts at sample 0, the valid candidates are exactly the chain the
 // serial walk visits (one contiguous run of samples from 0 covers them all)
 // and place[] is final; otherwise rpp_flac_chain_kernel walks.
-__global__ __launch_bounds__(256) void rpp_flac_link_kernel(FlacDecParams d) {
+__global__ __launch_bounds__(256) void rpp_flac_link_kernel(const FlacDecParams* tab) {
+  const FlacDecParams& d = tab[blockIdx.y];
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nc = min(*d.ncand, d.max_cand);
   if (c >= nc) return;
@@ -1581,8 +1605,9 @@ __global__ __launch_bounds__(256) void rpp_flac_link_kernel(FlacDecParams d) {
 // One lane: accepts the links, or walks the chain of frames from byte 0
 // (each frame starts where the previous one's CRC-16 ends) and places the
 // frames it visits
-__global__ void rpp_flac_chain_kernel(FlacDecParams d) {
+__global__ void rpp_flac_chain_kernel(const FlacDecParams* tab) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const FlacDecParams& d = tab[blockIdx.y];
   const uint32_t nc = min(*d.ncand, d.max_cand);
   const uint32_t head = d.nbytes ? d.cand_at[0] : 0u;
   if (d.nsamples && !d.link_acc[1] && d.link_acc[0] == d.nsamples && head && d.place[head - 1] == 0) {
@@ -1622,7 +1647,9 @@ __global__ void rpp_flac_chain_kernel(FlacDecParams d) {
 // One block per candidate on the chain: planar subframes to interleaved
 // samples, undoing the stereo decorrelation (left/side, side/right, mid/side)
 template <class T>
-__global__ __launch_bounds__(256) void rpp_flac_place_kernel(FlacDecParams d) {
+__global__ __launch_bounds__(256) void rpp_flac_place_kernel(const FlacDecParams* tab) {
+  const FlacDecParams& d = tab[blockIdx.y];
+  if ((d.wide != 0) != (sizeof(T) == 8)) return;
   const uint32_t c = blockIdx.x;
   if (c >= min(*d.ncand, d.max_cand) || *d.status != RPP_OK) return;
   const uint64_t first = d.place[c];
@@ -1820,10 +1847,117 @@ uint64_t rpp_flac_decode_workspace_bytes(uint64_t nbytes, uint32_t channels, uin
                                          uint32_t max_candidates) {
   const uint64_t mc = max_candidates;
   const uint64_t per = (uint64_t)max_blocksize * channels;
-  // (the take() layout below, 16-byte aligned pieces; per-candidate scratch
-  // of int32 samples, int64 for 32-bit streams)
+  // (the take() layout of flac_decode_many, 16-byte aligned pieces: the
+  // stream's table entry, then per-candidate scratch of int32 samples, int64
+  // for 32-bit streams)
   return 4 * (nbytes + 1) + mc * (8 + 4 + 8 + 4 + 4 + 8) + 7 * 16 + 16 + mc * per * (bps == 32 ? 8 : 4) + 256;
 }
+
+uint64_t rpp_flac_decode_batch_workspace_bytes(uint32_t nblocks, const uint64_t* h_nbytes, const uint32_t* h_channels,
+                                               const uint32_t* h_bps, const uint32_t* h_max_blocksize,
+                                               const uint32_t* h_max_candidates) {
+  if (!nblocks || !h_nbytes || !h_channels || !h_bps || !h_max_blocksize || !h_max_candidates) return 256;
+  uint64_t total = 256;
+  for (uint32_t b = 0; b < nblocks; ++b)
+    total += rpp_flac_decode_workspace_bytes(h_nbytes[b], h_channels[b], h_bps[b], h_max_blocksize[b],
+                                             h_max_candidates[b]);
+  return total;
+}
+
+}  // extern "C"
+
+namespace {
+
+// The decode of nblocks streams in one sequence of launches (each kernel's
+// grid: .x over a stream's bytes or candidates, .y over the streams; the
+// table of per-stream parameters is copied to the head of the workspace).
+// Stream b is byte-for-byte what a decode of it alone gives.
+int flac_decode_many(const uint8_t* d_frames, uint32_t nblocks, const uint64_t* in_off, const uint64_t* nbytes,
+                     const uint32_t* channels, const uint32_t* bps, const uint32_t* max_bs, const uint64_t* nsamples,
+                     int32_t* d_out, const uint64_t* out_off, int32_t* d_status, const uint32_t* max_cand,
+                     void* d_workspace, uint64_t workspace_bytes, uint32_t* d_ncand, hipStream_t s) {
+  if (nblocks > 65535) return RPP_INVALID_ARGUMENT;  // (grid .y)
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    if (channels[b] < 1 || channels[b] > 8 || bps[b] < 4 || bps[b] > 32 || max_bs[b] < 1 || max_bs[b] > 65536)
+      return RPP_UNSUPPORTED_CONFIG;
+    if ((nbytes[b] && !d_frames) || (nsamples[b] && !d_out) || max_cand[b] == 0) return RPP_INVALID_ARGUMENT;
+  }
+  if (!d_status || !d_ncand || !d_workspace) return RPP_INVALID_ARGUMENT;
+  uint8_t* ws = static_cast<uint8_t*>(d_workspace);
+  auto take = [&](uint64_t bytes) {
+    uint8_t* q = ws;
+    ws += (bytes + 15) & ~15ull;
+    return q;
+  };
+  const auto* d_tab = reinterpret_cast<const FlacDecParams*>(take(sizeof(FlacDecParams) * (uint64_t)nblocks));
+  uint64_t* d_link = reinterpret_cast<uint64_t*>(take(16 * (uint64_t)nblocks));
+  std::vector<FlacDecParams> tab(nblocks);
+  uint64_t max_bytes = 0, max_mc = 0, wave_lds = 0;
+  bool any_wave = false, any_lane32 = false, any_wide = false;
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    FlacDecParams& d = tab[b];
+    const uint64_t mc = max_cand[b], per = (uint64_t)max_bs[b] * channels[b];
+    d = FlacDecParams{};
+    d.in = d_frames ? d_frames + in_off[b] : nullptr;
+    d.nbytes = nbytes[b];
+    d.channels = channels[b];
+    d.bps = bps[b];
+    d.max_bs = max_bs[b];
+    d.nsamples = nsamples[b];
+    d.cand_at = reinterpret_cast<uint32_t*>(take(4 * (nbytes[b] + 1)));
+    d.cand_pos = reinterpret_cast<uint64_t*>(take(8 * mc));
+    d.cand_info = reinterpret_cast<uint32_t*>(take(4 * mc));
+    d.cand_len = reinterpret_cast<uint64_t*>(take(8 * mc));
+    d.cand_ok = reinterpret_cast<uint32_t*>(take(4 * mc));
+    d.cand_redo = reinterpret_cast<uint32_t*>(take(4 * mc));
+    d.place = reinterpret_cast<uint64_t*>(take(8 * mc));
+    d.link_acc = d_link + 2 * (uint64_t)b;
+    d.wide = bps[b] == 32;
+    d.scratch = take((d.wide ? 8 : 4) * mc * per);
+    d.ncand = d_ncand + b;
+    d.max_cand = max_cand[b];
+    d.out = d_out ? d_out + out_off[b] : nullptr;
+    d.status = d_status + b;
+    // the wave decoder where the frame's samples fit LDS, the lane decoder for the rest
+    const uint64_t lds = 4ull * (kFWin + 2) + 4ull * per;
+    d.use_wave = !d.wide && lds <= kFlacWaveLds;
+    d.redo_only = d.use_wave;
+    if (d.use_wave) wave_lds = std::max(wave_lds, lds);
+    any_wave |= d.use_wave != 0;
+    any_lane32 |= !d.wide;
+    any_wide |= d.wide != 0;
+    max_bytes = std::max(max_bytes, nbytes[b]);
+    max_mc = std::max(max_mc, mc);
+  }
+  // (the callers' workspace formulas bound this layout; checked all the same)
+  if ((uint64_t)(ws - static_cast<uint8_t*>(d_workspace)) > workspace_bytes) return RPP_INVALID_ARGUMENT;
+  if (nblocks == 0) return RPP_OK;
+  if (hipMemcpyAsync(const_cast<FlacDecParams*>(d_tab), tab.data(), sizeof(FlacDecParams) * (size_t)nblocks,
+                     hipMemcpyHostToDevice, s) != hipSuccess)
+    return RPP_HIP_ERROR;
+  if (hipMemsetAsync(d_ncand, 0, 4 * (size_t)nblocks, s) != hipSuccess) return RPP_HIP_ERROR;
+  const uint32_t B = nblocks, mcx = (uint32_t)max_mc;
+  if (max_bytes) hipLaunchKernelGGL(rpp_flac_scan_kernel, dim3((uint32_t)((max_bytes + 255) / 256), B), dim3(256), 0, s, d_tab);
+  if (any_wave) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rpp_flac_frame_wave_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFlacWaveLds);
+    if (attr != hipSuccess) return RPP_HIP_ERROR;
+    hipLaunchKernelGGL(rpp_flac_frame_wave_kernel, dim3(mcx, B), dim3(64), (size_t)wave_lds, s, d_tab);
+  }
+  if (any_wide) hipLaunchKernelGGL(rpp_flac_frame_kernel<int64_t>, dim3((mcx + 63) / 64, B), dim3(64), 0, s, d_tab);
+  if (any_lane32) hipLaunchKernelGGL(rpp_flac_frame_kernel<int32_t>, dim3((mcx + 63) / 64, B), dim3(64), 0, s, d_tab);
+  hipLaunchKernelGGL(rpp_flac_dec_crc_kernel, dim3(mcx < 4096 ? mcx : 4096, B), dim3(64), 0, s, d_tab);
+  if (hipMemsetAsync(d_link, 0, 16 * (size_t)nblocks, s) != hipSuccess) return RPP_HIP_ERROR;
+  hipLaunchKernelGGL(rpp_flac_link_kernel, dim3((mcx + 255) / 256, B), dim3(256), 0, s, d_tab);
+  hipLaunchKernelGGL(rpp_flac_chain_kernel, dim3(1, B), dim3(1), 0, s, d_tab);
+  if (any_wide) hipLaunchKernelGGL(rpp_flac_place_kernel<int64_t>, dim3(mcx, B), dim3(256), 0, s, d_tab);
+  if (any_lane32) hipLaunchKernelGGL(rpp_flac_place_kernel<int32_t>, dim3(mcx, B), dim3(256), 0, s, d_tab);
+  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+}
+
+}  // namespace
+
+extern "C" {
 
 int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels, uint32_t bps,
                     uint32_t max_blocksize, uint64_t nsamples, int32_t* d_out, int32_t* d_status,
@@ -1832,63 +1966,34 @@ int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels,
   if (channels < 1 || channels > 8 || bps < 4 || bps > 32 || max_blocksize < 1 || max_blocksize > 65536)
     return RPP_UNSUPPORTED_CONFIG;
   if (!d_status || !d_ncand) return RPP_INVALID_ARGUMENT;
-  hipStream_t s = (hipStream_t)stream;
   if (workspace_bytes < rpp_flac_decode_workspace_bytes(nbytes, channels, bps, max_blocksize, max_candidates))
     return RPP_INVALID_ARGUMENT;
   if ((nbytes && !d_frames) || (nsamples && !d_out) || !d_workspace || max_candidates == 0)
     return RPP_INVALID_ARGUMENT;
-  const uint64_t mc = max_candidates, per = (uint64_t)max_blocksize * channels;
-  uint8_t* ws = static_cast<uint8_t*>(d_workspace);
-  auto take = [&](uint64_t bytes) {
-    uint8_t* q = ws;
-    ws += (bytes + 15) & ~15ull;
-    return q;
-  };
-  FlacDecParams d{};
-  d.in = d_frames;
-  d.nbytes = nbytes;
-  d.channels = channels;
-  d.bps = bps;
-  d.max_bs = max_blocksize;
-  d.nsamples = nsamples;
-  d.cand_at = reinterpret_cast<uint32_t*>(take(4 * (nbytes + 1)));
-  d.cand_pos = reinterpret_cast<uint64_t*>(take(8 * mc));
-  d.cand_info = reinterpret_cast<uint32_t*>(take(4 * mc));
-  d.cand_len = reinterpret_cast<uint64_t*>(take(8 * mc));
-  d.cand_ok = reinterpret_cast<uint32_t*>(take(4 * mc));
-  d.cand_redo = reinterpret_cast<uint32_t*>(take(4 * mc));
-  d.place = reinterpret_cast<uint64_t*>(take(8 * mc));
-  d.link_acc = reinterpret_cast<uint64_t*>(take(16));
-  const bool wide = bps == 32;
-  d.scratch = take((wide ? 8 : 4) * mc * per);
-  d.ncand = d_ncand;
-  d.max_cand = max_candidates;
-  d.out = d_out;
-  d.status = d_status;
-  if (hipMemsetAsync(d_ncand, 0, 4, s) != hipSuccess) return RPP_HIP_ERROR;
-  if (nbytes) hipLaunchKernelGGL(rpp_flac_scan_kernel, dim3((uint32_t)((nbytes + 255) / 256)), dim3(256), 0, s, d);
-  // the wave decoder where the frame's samples fit LDS, the lane decoder for the rest
-  const uint64_t lds = 4ull * (kFWin + 2) + 4ull * per;
-  bool wave = !wide && lds <= kFlacWaveLds;
-  if (wave) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rpp_flac_frame_wave_kernel),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFlacWaveLds);
-    wave = attr == hipSuccess;
-  }
-  if (wave) {
-    hipLaunchKernelGGL(rpp_flac_frame_wave_kernel, dim3((uint32_t)mc), dim3(64), (size_t)lds, s, d);
-    d.redo_only = 1;
-  }
-  if (wide) hipLaunchKernelGGL(rpp_flac_frame_kernel<int64_t>, dim3((uint32_t)((mc + 63) / 64)), dim3(64), 0, s, d);
-  else hipLaunchKernelGGL(rpp_flac_frame_kernel<int32_t>, dim3((uint32_t)((mc + 63) / 64)), dim3(64), 0, s, d);
-  hipLaunchKernelGGL(rpp_flac_crc_kernel, dim3((uint32_t)(mc < 4096 ? mc : 4096)), dim3(64), 0, s, d.in, d.cand_pos,
-                     d.cand_len, (uint32_t)mc, nullptr, d.cand_ok, d.ncand);
-  if (hipMemsetAsync(d.link_acc, 0, 16, s) != hipSuccess) return RPP_HIP_ERROR;
-  hipLaunchKernelGGL(rpp_flac_link_kernel, dim3((uint32_t)((mc + 255) / 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(rpp_flac_chain_kernel, dim3(1), dim3(1), 0, s, d);
-  if (wide) hipLaunchKernelGGL(rpp_flac_place_kernel<int64_t>, dim3((uint32_t)mc), dim3(256), 0, s, d);
-  else hipLaunchKernelGGL(rpp_flac_place_kernel<int32_t>, dim3((uint32_t)mc), dim3(256), 0, s, d);
-  return hipGetLastError() == hipSuccess ? RPP_OK : RPP_HIP_ERROR;
+  const uint64_t zero = 0;
+  return flac_decode_many(d_frames, 1, &zero, &nbytes, &channels, &bps, &max_blocksize, &nsamples, d_out, &zero,
+                          d_status, &max_candidates, d_workspace, workspace_bytes, d_ncand, (hipStream_t)stream);
+}
+
+int rpp_flac_decode_batch(const uint8_t* d_frames, uint32_t nblocks, const uint64_t* h_in_off,
+                          const uint64_t* h_nbytes, const uint32_t* h_channels, const uint32_t* h_bps,
+                          const uint32_t* h_max_blocksize, const uint64_t* h_nsamples, int32_t* d_out,
+                          const uint64_t* h_out_off, int32_t* d_status, const uint32_t* h_max_candidates,
+                          void* d_workspace, uint64_t workspace_bytes, uint32_t* d_ncand, void* stream) {
+  if (nblocks == 0) return RPP_OK;
+  if (!h_in_off || !h_nbytes || !h_channels || !h_bps || !h_max_blocksize || !h_nsamples || !h_out_off ||
+      !h_max_candidates)
+    return RPP_INVALID_ARGUMENT;
+  for (uint32_t b = 0; b < nblocks; ++b)
+    if (h_channels[b] < 1 || h_channels[b] > 8 || h_bps[b] < 4 || h_bps[b] > 32 || h_max_blocksize[b] < 1 ||
+        h_max_blocksize[b] > 65536)
+      return RPP_UNSUPPORTED_CONFIG;
+  if (workspace_bytes <
+      rpp_flac_decode_batch_workspace_bytes(nblocks, h_nbytes, h_channels, h_bps, h_max_blocksize, h_max_candidates))
+    return RPP_INVALID_ARGUMENT;
+  return flac_decode_many(d_frames, nblocks, h_in_off, h_nbytes, h_channels, h_bps, h_max_blocksize, h_nsamples,
+                          d_out, h_out_off, d_status, h_max_candidates, d_workspace, workspace_bytes, d_ncand,
+                          (hipStream_t)stream);
 }
 
 }  // extern "C"

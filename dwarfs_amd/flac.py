@@ -239,7 +239,9 @@ class FlacBlockDecompressor:
         self._done = True
         return True
 
-    def decompress(self) -> bytes:
+    def _plan(self):
+        """The decode's parameters (None: no samples): frames, channels, bits, bytes per sample, samples per
+        channel, max block size, candidate slots."""
         info, fl = self.info, int(self.frame.flags)
         channels, bits = int(info.channels), int(info.bits_per_sample)
         nbytes = (fl & BYTES_PER_SAMPLE_MASK) + 1
@@ -247,27 +249,47 @@ class FlacBlockDecompressor:
         if n * channels * nbytes != self.uncompressed_size():
             raise RuntimeError("[FLAC] failed to process frame: stream length does not match the block")
         if n == 0:
-            return b""
-        dev = self.device
+            return None
         body = np.frombuffer(self.stream, np.uint8)[self.frames_at:]
+        min_bs = max(16, int(info.min_blocksize) or 16)
+        max_bs = int(info.max_blocksize) or 65535
+        # Frames: at most n // min_bs + 1 (every block but the last holds at
+        # least min_bs samples); spurious sync codes that pass the CRC-8 are
+        # rare and handled by the retry of the callers.  Every candidate gets a
+        # scratch slot of max_bs samples: a STREAMINFO whose block-size range
+        # would make that more than 4x the block's samples (libFLAC writes
+        # min == max; DwarFS's flac compressor uses fixed blocking) is refused
+        # rather than allowed to size the workspace from a crafted header.
+        max_cand = n // min_bs + 65
+        if max_cand * max_bs > 4 * n + 128 * max_bs:
+            raise RuntimeError("[FLAC] failed to process frame: block size range "
+                               f"{int(info.min_blocksize)}..{max_bs} too wide for {n} samples")
+        return body, channels, bits, nbytes, n, max_bs, max_cand
+
+    @staticmethod
+    def _more_candidates(found: int, n: int, max_bs: int) -> int:
+        if found * max_bs > 4 * n + 128 * max_bs:  # (a stream full of false sync codes)
+            raise RuntimeError(f"[FLAC] failed to process frame: {found} frame candidates")
+        return found + 64  # (more sync candidates than estimated: again, with room for all)
+
+    def _finish(self, x: torch.Tensor, st: int, nbytes: int) -> bytes:
+        if st != N.RPP_OK:
+            raise RuntimeError(f"[FLAC] failed to process frame: {N.STATUS_NAMES.get(st, st)}")
+        out = torch.empty(x.numel() * nbytes, dtype=torch.uint8, device=self.device)
+        _transformer(int(self.frame.flags), int(self.frame.bits_per_sample)).pack(out, x)
+        return out.cpu().numpy().tobytes()
+
+    def decompress(self) -> bytes:
+        plan = self._plan()
+        if plan is None:
+            return b""
+        body, channels, bits, nbytes, n, max_bs, max_cand = plan
+        dev = self.device
         d_in = torch.from_numpy(body.copy()).to(dev)
         x = torch.empty(n * channels, dtype=torch.int32, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
         ncand = torch.zeros(1, dtype=torch.int32, device=dev)
         L = N.lib()
-        min_bs = max(16, int(info.min_blocksize) or 16)
-        max_bs = int(info.max_blocksize) or 65535
-        # Frames: at most n // min_bs + 1 (every block but the last holds at
-        # least min_bs samples); spurious sync codes that pass the CRC-8 are
-        # rare and handled by the retry below.  Every candidate gets a scratch
-        # slot of max_bs samples: a STREAMINFO whose block-size range would make
-        # that more than 4x the block's samples (libFLAC writes min == max;
-        # DwarFS's flac compressor uses fixed blocking) is refused rather than
-        # allowed to size the workspace from a crafted header.
-        max_cand = n // min_bs + 65
-        if max_cand * max_bs > 4 * n + 128 * max_bs:
-            raise RuntimeError("[FLAC] failed to process frame: block size range "
-                               f"{int(info.min_blocksize)}..{max_bs} too wide for {n} samples")
         s = torch.cuda.current_stream(dev)
         for _ in range(2):
             ws_bytes = int(L.rpp_flac_decode_workspace_bytes(len(body), channels, bits, max_bs, max_cand))
@@ -279,15 +301,61 @@ class FlacBlockDecompressor:
             found = int(ncand.item())
             if found <= max_cand:
                 break
-            if found * max_bs > 4 * n + 128 * max_bs:  # (a stream full of false sync codes)
-                raise RuntimeError(f"[FLAC] failed to process frame: {found} frame candidates")
-            max_cand = found + 64  # (more sync candidates than estimated: again, with room for all)
-        st = int(status.item())
-        if st != N.RPP_OK:
-            raise RuntimeError(f"[FLAC] failed to process frame: {N.STATUS_NAMES.get(st, st)}")
-        out = torch.empty(n * channels * nbytes, dtype=torch.uint8, device=dev)
-        _transformer(fl, int(self.frame.bits_per_sample)).pack(out, x)
-        return out.cpu().numpy().tobytes()
+            max_cand = self._more_candidates(found, n, max_bs)
+        return self._finish(x, int(status.item()), nbytes)
+
+
+def decompress_many(blocks, device="cuda") -> list:
+    """``block_decompressor::decompress`` of every FLAC block in ``blocks``, all streams' frames decoded in one
+    sequence of launches (rpp_flac_decode_batch); byte-identical to decompress() per block (the first failing
+    block raises its error)."""
+    decs = [FlacBlockDecompressor(b, device) for b in blocks]
+    plans = [d._plan() for d in decs]
+    live = [i for i, pl in enumerate(plans) if pl is not None]
+    outs = [b""] * len(decs)
+    if not live:
+        return outs
+    dev = torch.device(device)
+    nb = len(live)
+    body_len = np.array([len(plans[i][0]) for i in live], np.uint64)
+    in_off = np.zeros(nb, np.uint64)
+    in_off[1:] = np.cumsum((body_len + 15) // 16 * 16)[:-1]
+    buf = np.zeros(int(in_off[-1] + body_len[-1]) + 16, np.uint8)
+    for k, i in enumerate(live):
+        buf[int(in_off[k]):int(in_off[k] + body_len[k])] = plans[i][0]
+    d_in = torch.from_numpy(buf).to(dev)
+    ch = np.array([plans[i][1] for i in live], np.uint32)
+    bp = np.array([plans[i][2] for i in live], np.uint32)
+    ns = np.array([plans[i][4] for i in live], np.uint64)
+    mbs = np.array([plans[i][5] for i in live], np.uint32)
+    mc = np.array([plans[i][6] for i in live], np.uint32)
+    vals = ns * ch
+    out_off = np.zeros(nb, np.uint64)
+    out_off[1:] = np.cumsum(vals)[:-1]
+    x = torch.empty(int(vals.sum()), dtype=torch.int32, device=dev)
+    status = torch.zeros(nb, dtype=torch.int32, device=dev)
+    ncand = torch.zeros(nb, dtype=torch.int32, device=dev)
+    L = N.lib()
+    P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    s = torch.cuda.current_stream(dev)
+    for _ in range(2):
+        ws_bytes = int(L.rpp_flac_decode_batch_workspace_bytes(nb, P(body_len), P(ch), P(bp), P(mbs), P(mc)))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        _status(L.rpp_flac_decode_batch(C.c_void_p(d_in.data_ptr()), nb, P(in_off), P(body_len), P(ch), P(bp),
+                                        P(mbs), P(ns), C.c_void_p(x.data_ptr()), P(out_off),
+                                        C.c_void_p(status.data_ptr()), P(mc), C.c_void_p(ws.data_ptr()), ws_bytes,
+                                        C.c_void_p(ncand.data_ptr()), C.c_void_p(s.cuda_stream)), "decode")
+        found = ncand.cpu().numpy().astype(np.int64)
+        over = found > mc
+        if not over.any():
+            break
+        for k in np.nonzero(over)[0]:
+            mc[k] = FlacBlockDecompressor._more_candidates(int(found[k]), int(ns[k]), int(mbs[k]))
+    st = status.cpu().numpy()
+    for k, i in enumerate(live):
+        lo = int(out_off[k])
+        outs[i] = decs[i]._finish(x[lo:lo + int(vals[k])], int(st[k]), plans[i][3])
+    return outs
 
 
 def decompress(data: bytes, device="cuda") -> bytes:

@@ -391,6 +391,23 @@ int rpp_flac_decode(const uint8_t* d_frames, uint64_t nbytes, uint32_t channels,
                     uint32_t max_blocksize, uint64_t nsamples, int32_t* d_out, int32_t* d_status,
                     uint32_t max_candidates, void* d_workspace, uint64_t workspace_bytes, uint32_t* d_ncand,
                     void* stream);
+/* Several streams' frames decoded in one sequence of launches (the
+ * reference decompresses one block per call, flac.cpp:405-489; a batching
+ * caller joins them as the ricepp facade does): stream b is h_nbytes[b]
+ * bytes of frames at d_frames + h_in_off[b] with its STREAMINFO's channels,
+ * bps, max block size and h_nsamples[b] samples per channel, decoded to
+ * d_out + h_out_off[b] (int32 elements) with d_status[b] and d_ncand[b] as
+ * rpp_flac_decode gives them for that stream alone -- byte for byte the
+ * same.  Host arrays (the launches need the sizes); nblocks <= 65535.
+ * Workspace: rpp_flac_decode_batch_workspace_bytes. */
+uint64_t rpp_flac_decode_batch_workspace_bytes(uint32_t nblocks, const uint64_t* h_nbytes, const uint32_t* h_channels,
+                                               const uint32_t* h_bps, const uint32_t* h_max_blocksize,
+                                               const uint32_t* h_max_candidates);
+int rpp_flac_decode_batch(const uint8_t* d_frames, uint32_t nblocks, const uint64_t* h_in_off,
+                          const uint64_t* h_nbytes, const uint32_t* h_channels, const uint32_t* h_bps,
+                          const uint32_t* h_max_blocksize, const uint64_t* h_nsamples, int32_t* d_out,
+                          const uint64_t* h_out_off, int32_t* d_status, const uint32_t* h_max_candidates,
+                          void* d_workspace, uint64_t workspace_bytes, uint32_t* d_ncand, void* stream);
 
 #ifdef __cplusplus
 }

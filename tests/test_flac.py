@@ -117,7 +117,8 @@ def test_flac_symbols_exported():
     for name in ("rpp_flac_frame_header", "rpp_flac_parse_frame", "rpp_flac_stream_header", "rpp_flac_parse_stream",
                  "rpp_flac_frame_bound", "rpp_flac_encode_workspace_bytes", "rpp_flac_encode",
                  "rpp_flac_encode_ex", "rpp_flac_encode_batch_workspace_bytes", "rpp_flac_encode_batch",
-                 "rpp_flac_decode_workspace_bytes", "rpp_flac_decode"):
+                 "rpp_flac_decode_workspace_bytes", "rpp_flac_decode", "rpp_flac_decode_batch_workspace_bytes",
+                 "rpp_flac_decode_batch"):
         assert hasattr(L, name)
 
 

@@ -178,6 +178,38 @@ def test_gpu_encode_batch_matches_single_blocks(level, exh):
         assert FL.decompress(got) == data
 
 
+@pytest.mark.parametrize("level", [5, 8])
+def test_gpu_decode_batch_matches_single_blocks(level):
+    """rpp_flac_decode_batch (FL.decompress_many): blocks of different shapes -- channels 1-3, 8-32 bits (the
+    32-bit block on the lane decoder's int64 instance, the others on the wave decoder), empty, one sample,
+    several frames, trailing bytes after the last frame (the serial chain walk) -- decoded in one sequence
+    of launches give the samples each block gives alone."""
+    shapes = [(2, 3 * 4096 + 5, 2, 16), (1, 100, 1, 8), (3, 4096, 3, 24), (2, 0, 2, 16), (1, 9000, 4, 32),
+              (2, 4096 * 2, 2, 16), (1, 1, 2, 12), (4, 5000, 3, 20)]
+    rng = np.random.default_rng(level + 100)
+    comp = FL.FlacBlockCompressor(level)
+    datas, blocks = [], []
+    for k, (channels, n, nbytes, bits) in enumerate(shapes):
+        x = ar_audio(channels, n, bits, seed=k + 50) if n else np.zeros(0, np.int32)
+        if k == 4:
+            x = rng.integers(-(1 << 31), (1 << 31) - 1, n * channels).astype(np.int32)
+        data = pcm_bytes(x, E.Little, S.Signed, Pd.Msb, nbytes, bits) if n else b""
+        c = comp.compress(data, meta(E.Little, S.Signed, Pd.Msb, channels, nbytes, bits))
+        if k == 5:
+            c += bytes(9)
+        datas.append(data)
+        blocks.append(c)
+    many = FL.decompress_many(blocks)
+    for k, (data, c, got) in enumerate(zip(datas, blocks, many)):
+        assert got == data, k
+        assert got == FL.decompress(c), k
+    # one corrupt block in the batch fails with the single decode's error
+    bad = bytearray(blocks[0])
+    bad[len(bad) // 2] ^= 0x04
+    with pytest.raises(RuntimeError, match="FLAC"):
+        FL.decompress_many([blocks[1], bytes(bad), blocks[2]])
+
+
 def test_empty_block():
     comp = FL.FlacBlockCompressor().compress(b"", meta(E.Big, S.Signed, Pd.Msb, 2, 2, 16))
     assert FL.decompress(comp) == b""
