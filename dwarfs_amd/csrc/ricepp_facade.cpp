@@ -758,6 +758,19 @@ class batch_queue {
       }
     }
   }
+  // Device buffers and workspace are asked for at the batch's capacity (its
+  // pinned staging, `join` requests of its largest one), not at its fill, so
+  // that a context grows them once, on its first batch of a size class: a
+  // later, fuller batch regrowing them (hipFree synchronises the device) put
+  // a 4-7 ms stall into the first timed 16 MiB run (profiles/r06_facade_16m.jsonl)
+  static size_t device_capacity(batch const& b) { return b.in_cap + b.out_cap; }
+  uint64_t workspace_capacity(batch const& b, bool encode) const {
+    if (b.join <= b.reqs.size()) return 0;
+    const uint64_t total = b.join * b.max_samples;
+    const auto j = static_cast<uint32_t>(b.join);
+    return encode ? rpp_encode_workspace_bytes(&cfg_, total, b.max_samples, j)
+                  : rpp_decode_workspace_bytes(&cfg_, total, b.max_samples, j);
+  }
   void launch_encode(batch& b) {
     device_ctx& ctx = *b.ctx;
     const size_t nb = b.reqs.size();
@@ -770,10 +783,10 @@ class batch_queue {
       h64[nb + i] = b.reqs[i]->n_samples;
       h64[2 * nb + i] = b.reqs[i]->out_off;
     }
-    uint8_t* d = ctx.dev(in_total + arr + out_total + 64);
+    uint8_t* d = ctx.dev(std::max(in_total + arr + out_total, device_capacity(b)) + 64);
     const uint64_t ws_bytes =
         rpp_encode_workspace_bytes(&cfg_, b.total_samples, b.max_samples, static_cast<uint32_t>(nb));
-    uint8_t* ws = ws_bytes ? ctx.workspace(ws_bytes) : nullptr;
+    uint8_t* ws = ws_bytes ? ctx.workspace(std::max(ws_bytes, workspace_capacity(b, true))) : nullptr;
     uint8_t* pout_dev = ctx.device_view(b.pin_out);
     auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
     auto* dst = reinterpret_cast<int32_t*>(d + in_total + (6 * nb + 1) * 8);
@@ -870,8 +883,8 @@ class batch_queue {
       g_dec_blocks.fetch_add(nb, std::memory_order_relaxed);
       return;
     }
-    uint8_t* d = ctx.dev(in_total + 4 * nb * 8 + out_total + st_bytes + 64);
-    uint8_t* ws = ctx.workspace(ws_bytes);
+    uint8_t* d = ctx.dev(std::max(in_total + 4 * nb * 8 + out_total + st_bytes, device_capacity(b)) + 64);
+    uint8_t* ws = ctx.workspace(std::max(ws_bytes, workspace_capacity(b, false)));
     auto* d64 = reinterpret_cast<uint64_t*>(d + in_total);
     uint8_t* dout = d + in_total + 4 * nb * 8;
     auto* dst = reinterpret_cast<int32_t*>(dout + out_total);

@@ -541,10 +541,11 @@ int bench(int argc, char** argv) {
       return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     };
     // warm the contexts (both directions: decode grows their buffers
-    // differently); twice, since batches fill differently from pass to pass
-    // and a context first reached by a later pass grows its pinned buffers
-    // then (each run reports contexts_created and buffer_grows)
-    for (int w = 0; w < 2; ++w) {
+    // differently); three times, since batches form differently from pass to
+    // pass and a context first created by a later pass grows its pinned
+    // buffers then, ~50-70 ms (each run reports contexts_created and
+    // buffer_grows)
+    for (int w = 0; w < 3; ++w) {
       run(true);
       run(false);
     }
